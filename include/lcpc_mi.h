@@ -1,0 +1,217 @@
+/*
+ * lcpc_mi.h -- C ABI of liblcpc_mi.so, the MI355X-native lcpc-2d commit / prove / verify
+ * row-encoding path.
+ *
+ * This is the drop-in boundary for the reference's LcEncoding trait and LcCommit /
+ * LcEvalProof API (TrevorGKann/lcpc_proof_of_storage, lcpc-2d/src/lib.rs).  Each entry point
+ * names the reference interface it replaces (file:line).  A Rust FFI shim (see
+ * INTEGRATION.md) passes `&mut [F]` as `uint64_t*` after a size/alignment check: field
+ * elements cross the boundary as `limbs(field)` little-endian u64 words holding ff_derive's
+ * internal Montgomery form, bit-identical to the reference's `struct FtX([u64; N])`.
+ *
+ * Conventions
+ *   - every function returns lcpc_status (0 = OK) unless it returns a size/bool; on error
+ *     lcpc_last_error() returns a thread-local message;
+ *   - "host" pointers are caller-owned CPU memory; "device" pointers are HIP device memory
+ *     of the current device; handles own their device buffers;
+ *   - a handle may be used from several threads; calls on one handle are serialized
+ *     internally (one HIP stream per handle).
+ * No torch / HIP types appear in the signatures; `void *stream` is an optional hipStream_t.
+ */
+#ifndef LCPC_MI_H
+#define LCPC_MI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LCPC_ABI_VERSION 1
+
+typedef enum lcpc_status {
+  LCPC_OK = 0,
+  /* ProverError (lcpc-2d/src/lib.rs:113-132) */
+  LCPC_PROVER_TOO_BIG = 1,
+  LCPC_PROVER_ENCODE = 2,
+  LCPC_PROVER_COMMIT = 3,
+  LCPC_PROVER_COLUMN_NUMBER = 4,
+  LCPC_PROVER_OUTER_TENSOR = 5,
+  /* VerifierError (lcpc-2d/src/lib.rs:139-167) */
+  LCPC_VERIFIER_NUM_COL_OPENS = 10,
+  LCPC_VERIFIER_COLUMN_PATH = 11,
+  LCPC_VERIFIER_COLUMN_EVAL = 12,
+  LCPC_VERIFIER_COLUMN_DEGREE = 13,
+  LCPC_VERIFIER_OUTER_TENSOR = 14,
+  LCPC_VERIFIER_INNER_TENSOR = 15,
+  LCPC_VERIFIER_ENCODING_DIMS = 16,
+  LCPC_VERIFIER_ENCODE = 17,
+  /* fffft::FFTError (encode's Err type, lcpc-ligero-pc/src/lib.rs:159) */
+  LCPC_FFT_NOT_POWER_OF_TWO = 20,
+  LCPC_FFT_TOO_BIG = 21,
+  LCPC_FFT_WRONG_SIZE_PRECOMP = 22,
+  /* boundary-level failures (the Rust code panics / asserts here) */
+  LCPC_ERR_INVALID_ARG = 30,
+  LCPC_ERR_DEVICE = 31,
+  LCPC_ERR_OUT_OF_MEMORY = 32,
+  LCPC_ERR_NO_DEVICE = 33,
+  LCPC_ERR_UNSUPPORTED = 34
+} lcpc_status;
+
+typedef enum lcpc_field {
+  LCPC_FT63 = 0,      /* lcpc-test-fields/src/lib.rs:18-22; PoS WriteableFt63 (same p) */
+  LCPC_FT127 = 1,     /* lcpc-test-fields/src/lib.rs:41-45 */
+  LCPC_FT191 = 2,     /* lcpc-test-fields/src/lib.rs:53-57 (no GPU kernels: unsupported) */
+  LCPC_FT255 = 3,     /* lcpc-test-fields/src/lib.rs:65-69 */
+  LCPC_FT253_192 = 4  /* proof-of-storage/src/fields/ft253_192.rs:6-10 (big-endian repr) */
+} lcpc_field;
+
+typedef struct lcpc_encoding lcpc_encoding;
+typedef struct lcpc_commit lcpc_commit;
+typedef struct lcpc_proof lcpc_proof;
+typedef struct lcpc_transcript lcpc_transcript;
+
+/* ------------------------------------------------------------------ library */
+int lcpc_abi_version(void);
+const char *lcpc_last_error(void);
+/* Selects the HIP device used by handles created afterwards on this thread. */
+lcpc_status lcpc_set_device(int device);
+int lcpc_device_count(void);
+/* u64 limbs per element (1, 2, 3, 4, 4); 0 for an unknown field */
+int lcpc_field_limbs(lcpc_field f);
+/* NUM_BITS of the field (SizedField::CLOG2, lcpc-2d/src/lib.rs:69-72) */
+int lcpc_field_num_bits(lcpc_field f);
+
+/* ------------------------------------------------------------------ parameters
+ * n_degree_tests (lcpc-2d/src/lib.rs:642-645), log2 (:857-859) */
+size_t lcpc_n_degree_tests(size_t lambda, size_t len, size_t flog2);
+size_t lcpc_log2(size_t v);
+/* LigeroEncodingRho::_n_col_opens (lcpc-ligero-pc/src/lib.rs:61-64) */
+size_t lcpc_ligero_n_col_opens(size_t rho_num, size_t rho_den);
+/* LigeroEncodingRho::_get_dims (lcpc-ligero-pc/src/lib.rs:70-112); LCPC_PROVER_TOO_BIG when
+ * the Rust function returns None */
+lcpc_status lcpc_ligero_get_dims(lcpc_field f, size_t rho_num, size_t rho_den, size_t len,
+                                 size_t *n_rows, size_t *n_per_row, size_t *n_cols);
+
+/* ------------------------------------------------------------------ LcEncoding
+ * Ligero: LigeroEncodingRho::{new, new_ml, new_from_dims} (lcpc-ligero-pc/src/lib.rs:121-148) */
+lcpc_status lcpc_ligero_new(lcpc_field f, size_t rho_num, size_t rho_den, size_t len,
+                            lcpc_encoding **out);
+lcpc_status lcpc_ligero_new_ml(lcpc_field f, size_t rho_num, size_t rho_den, size_t n_vars,
+                               lcpc_encoding **out);
+lcpc_status lcpc_ligero_new_from_dims(lcpc_field f, size_t rho_num, size_t rho_den,
+                                      size_t n_per_row, size_t n_cols, lcpc_encoding **out);
+/* An R-S (fft_io) encoding with explicit soundness parameters, as the lcpc-2d test encoding
+ * (lcpc-2d/src/tests.rs:23-121: N_COL_OPENS = 128, 2 degree tests). */
+lcpc_status lcpc_rs_encoding_new(lcpc_field f, size_t n_per_row, size_t n_cols,
+                                 size_t n_col_opens, size_t n_degree_tests, lcpc_encoding **out);
+void lcpc_encoding_free(lcpc_encoding *e);
+lcpc_field lcpc_encoding_field(const lcpc_encoding *e);
+/* LcEncoding::get_dims / dims_ok / get_n_col_opens / get_n_degree_tests (lib.rs:94-104) */
+void lcpc_encoding_get_dims(const lcpc_encoding *e, size_t len, size_t *n_rows, size_t *n_per_row,
+                            size_t *n_cols);
+int lcpc_encoding_dims_ok(const lcpc_encoding *e, size_t n_per_row, size_t n_cols);
+size_t lcpc_encoding_n_col_opens(const lcpc_encoding *e);
+size_t lcpc_encoding_n_degree_tests(const lcpc_encoding *e);
+size_t lcpc_encoding_n_per_row(const lcpc_encoding *e);
+size_t lcpc_encoding_n_cols(const lcpc_encoding *e);
+/* LcEncoding::encode (lcpc-2d/src/lib.rs:92; Ligero: fft_io_pc, lcpc-ligero-pc/src/lib.rs:
+ * 162-164): in place on `len` elements (must equal n_cols) of host memory. */
+lcpc_status lcpc_encode(const lcpc_encoding *e, uint64_t *inp, size_t len);
+/* Batched encode of n_rows host rows (row r at rows + r * row_stride limbs-elements). */
+lcpc_status lcpc_encode_rows(const lcpc_encoding *e, uint64_t *rows, size_t n_rows,
+                             size_t row_stride);
+/* Device batched encode: row r reads n_valid <= n_per_row... coefficients at
+ * d_src + r * src_stride (elements), the rest of the row zero, and writes n_cols encoded
+ * elements at d_dst + r * dst_stride.  Asynchronous on `stream` (NULL: the handle stream). */
+lcpc_status lcpc_encode_rows_device(const lcpc_encoding *e, const void *d_src, size_t src_stride,
+                                    size_t n_valid, void *d_dst, size_t dst_stride,
+                                    size_t n_rows, void *stream);
+
+/* ------------------------------------------------------------------ LcCommit
+ * LcCommit::commit (lcpc-2d/src/lib.rs:314-316 -> commit :651-700).  The commitment (coeffs,
+ * encoded matrix, Merkle hashes) stays resident in HBM; `len` elements. */
+lcpc_status lcpc_commit_new(const lcpc_encoding *e, const uint64_t *coeffs, size_t len,
+                            lcpc_commit **out);
+/* Same with the coefficients already in device memory (no PCIe transfer). */
+lcpc_status lcpc_commit_new_device(const lcpc_encoding *e, const void *d_coeffs, size_t len,
+                                   lcpc_commit **out);
+void lcpc_commit_free(lcpc_commit *c);
+/* LcCommit::get_root (:291-296) */
+lcpc_status lcpc_commit_get_root(const lcpc_commit *c, uint8_t root[32]);
+size_t lcpc_commit_n_rows(const lcpc_commit *c);      /* get_n_rows   :309-311 */
+size_t lcpc_commit_n_cols(const lcpc_commit *c);      /* get_n_cols   :304-306 */
+size_t lcpc_commit_n_per_row(const lcpc_commit *c);   /* get_n_per_row :299-301 */
+size_t lcpc_commit_n_hashes(const lcpc_commit *c);
+/* copies of the public fields comm / coeffs / hashes (:180-190) to host memory */
+lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out);
+lcpc_status lcpc_commit_copy_coeffs(const lcpc_commit *c, uint64_t *out);
+lcpc_status lcpc_commit_copy_hashes(const lcpc_commit *c, uint8_t *out);
+/* device views (valid while the handle lives) */
+const void *lcpc_commit_device_comm(const lcpc_commit *c);
+const void *lcpc_commit_device_coeffs(const lcpc_commit *c);
+/* check_comm (:703-718) */
+lcpc_status lcpc_check_comm(const lcpc_commit *c, const lcpc_encoding *e);
+/* open_column (:818-855): n_rows elements + log2(n_cols) digests */
+lcpc_status lcpc_open_column(const lcpc_commit *c, size_t column, uint64_t *col_out,
+                             uint8_t *path_out);
+
+/* ------------------------------------------------------------------ merlin::Transcript
+ * (merlin 2.0; used by prove/verify at lcpc-2d/src/lib.rs:901,934,1057,1075-1077,1096-1104) */
+lcpc_transcript *lcpc_transcript_new(const uint8_t *label, size_t label_len);
+lcpc_transcript *lcpc_transcript_clone(const lcpc_transcript *t);
+void lcpc_transcript_free(lcpc_transcript *t);
+void lcpc_transcript_append_message(lcpc_transcript *t, const uint8_t *label, size_t label_len,
+                                    const uint8_t *msg, size_t msg_len);
+void lcpc_transcript_challenge_bytes(lcpc_transcript *t, const uint8_t *label, size_t label_len,
+                                     uint8_t *dest, size_t dest_len);
+
+/* ------------------------------------------------------------------ LcEvalProof
+ * LcCommit::prove (lcpc-2d/src/lib.rs:319-326 -> prove :1034-1123).  outer_tensor: host,
+ * outer_len elements. */
+lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer_tensor, size_t outer_len,
+                       const lcpc_encoding *e, lcpc_transcript *tr, lcpc_proof **out);
+void lcpc_proof_free(lcpc_proof *p);
+size_t lcpc_proof_n_cols(const lcpc_proof *p);          /* LcEvalProof::get_n_cols :537-539 */
+size_t lcpc_proof_n_per_row(const lcpc_proof *p);       /* get_n_per_row :542-544 */
+size_t lcpc_proof_n_rows(const lcpc_proof *p);
+size_t lcpc_proof_n_degree_tests(const lcpc_proof *p);
+size_t lcpc_proof_n_col_opens(const lcpc_proof *p);
+size_t lcpc_proof_path_len(const lcpc_proof *p);
+lcpc_field lcpc_proof_field(const lcpc_proof *p);
+lcpc_status lcpc_proof_copy_p_eval(const lcpc_proof *p, uint64_t *out);
+lcpc_status lcpc_proof_copy_p_random(const lcpc_proof *p, size_t i, uint64_t *out);
+/* k-th opened column (LcColumn, :424-433): values (n_rows) and Merkle path (path_len x 32 B) */
+lcpc_status lcpc_proof_copy_column(const lcpc_proof *p, size_t k, uint64_t *col, uint8_t *path);
+/* Rebuild a proof from its public fields (e.g. after deserialisation, :591-610). */
+lcpc_status lcpc_proof_from_parts(lcpc_field f, size_t n_cols, size_t n_per_row, size_t n_rows,
+                                  size_t n_degree_tests, size_t n_col_opens, size_t path_len,
+                                  const uint64_t *p_eval, const uint64_t *p_random,
+                                  const uint64_t *cols, const uint8_t *paths, lcpc_proof **out);
+/* LcEvalProof::verify (:547-556 -> verify :862-982); *eval_out = the evaluation (limbs). */
+lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer_tensor, size_t outer_len,
+                        const uint64_t *inner_tensor, size_t inner_len, const lcpc_proof *p,
+                        const lcpc_encoding *e, lcpc_transcript *tr, uint64_t *eval_out);
+
+/* ------------------------------------------------------------------ free functions */
+/* collapse_columns (lcpc-2d/src/lib.rs:1126-1154) on host arrays: poly[c] += ... is computed
+ * as poly = sum_r tensor[r] * coeffs[r][c] for c < n_per_row */
+lcpc_status lcpc_collapse_columns(lcpc_field f, const uint64_t *coeffs, const uint64_t *tensor,
+                                  uint64_t *poly, size_t n_rows, size_t n_per_row);
+/* merkle_tree (lcpc-2d/src/lib.rs:777-790): ins has n_ins = 2^k digests, outs n_ins - 1 */
+lcpc_status lcpc_merkle_tree(const uint8_t *ins, size_t n_ins, uint8_t *outs);
+/* verify_column_path (:985-1012) and verify_column_value (:1015-1030): 1 = ok, 0 = fail */
+int lcpc_verify_column_path(lcpc_field f, const uint64_t *col, size_t n_rows,
+                            const uint8_t *path, size_t path_len, size_t col_num,
+                            const uint8_t root[32]);
+int lcpc_verify_column_value(lcpc_field f, const uint64_t *col, const uint64_t *tensor,
+                             size_t n_rows, const uint64_t *poly_eval);
+/* leaf digests of every column of a host matrix (hash_columns, :736-775) */
+lcpc_status lcpc_hash_columns(lcpc_field f, const uint64_t *comm, size_t n_rows, size_t n_cols,
+                              uint8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LCPC_MI_H */

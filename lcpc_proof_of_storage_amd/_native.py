@@ -1,0 +1,121 @@
+"""ctypes binding of liblcpc_mi.so (include/lcpc_mi.h).
+
+The shared library is built in-tree (``make -C lcpc_proof_of_storage_amd``) and loaded from
+this package directory.  There is no fallback: if the library or a HIP device is missing,
+every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "liblcpc_mi.so")
+HEADER_PATH = os.path.join(REPO_DIR, "include", "lcpc_mi.h")
+
+_lib = None
+
+u64p = C.POINTER(C.c_uint64)
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+szp = C.POINTER(C.c_size_t)
+vp = C.c_void_p
+sz = C.c_size_t
+i32 = C.c_int
+
+# name: (restype, argtypes)
+SIGNATURES = {
+    "lcpc_abi_version": (i32, []),
+    "lcpc_last_error": (C.c_char_p, []),
+    "lcpc_set_device": (i32, [i32]),
+    "lcpc_device_count": (i32, []),
+    "lcpc_field_limbs": (i32, [i32]),
+    "lcpc_field_num_bits": (i32, [i32]),
+    "lcpc_n_degree_tests": (sz, [sz, sz, sz]),
+    "lcpc_log2": (sz, [sz]),
+    "lcpc_ligero_n_col_opens": (sz, [sz, sz]),
+    "lcpc_ligero_get_dims": (i32, [i32, sz, sz, sz, szp, szp, szp]),
+    "lcpc_ligero_new": (i32, [i32, sz, sz, sz, C.POINTER(vp)]),
+    "lcpc_ligero_new_ml": (i32, [i32, sz, sz, sz, C.POINTER(vp)]),
+    "lcpc_ligero_new_from_dims": (i32, [i32, sz, sz, sz, sz, C.POINTER(vp)]),
+    "lcpc_rs_encoding_new": (i32, [i32, sz, sz, sz, sz, C.POINTER(vp)]),
+    "lcpc_encoding_free": (None, [vp]),
+    "lcpc_encoding_field": (i32, [vp]),
+    "lcpc_encoding_get_dims": (None, [vp, sz, szp, szp, szp]),
+    "lcpc_encoding_dims_ok": (i32, [vp, sz, sz]),
+    "lcpc_encoding_n_col_opens": (sz, [vp]),
+    "lcpc_encoding_n_degree_tests": (sz, [vp]),
+    "lcpc_encoding_n_per_row": (sz, [vp]),
+    "lcpc_encoding_n_cols": (sz, [vp]),
+    "lcpc_encode": (i32, [vp, u64p, sz]),
+    "lcpc_encode_rows": (i32, [vp, u64p, sz, sz]),
+    "lcpc_encode_rows_device": (i32, [vp, vp, sz, sz, vp, sz, sz, vp]),
+    "lcpc_commit_new": (i32, [vp, u64p, sz, C.POINTER(vp)]),
+    "lcpc_commit_new_device": (i32, [vp, vp, sz, C.POINTER(vp)]),
+    "lcpc_commit_free": (None, [vp]),
+    "lcpc_commit_get_root": (i32, [vp, u8p]),
+    "lcpc_commit_n_rows": (sz, [vp]),
+    "lcpc_commit_n_cols": (sz, [vp]),
+    "lcpc_commit_n_per_row": (sz, [vp]),
+    "lcpc_commit_n_hashes": (sz, [vp]),
+    "lcpc_commit_copy_comm": (i32, [vp, u64p]),
+    "lcpc_commit_copy_coeffs": (i32, [vp, u64p]),
+    "lcpc_commit_copy_hashes": (i32, [vp, u8p]),
+    "lcpc_commit_device_comm": (vp, [vp]),
+    "lcpc_commit_device_coeffs": (vp, [vp]),
+    "lcpc_check_comm": (i32, [vp, vp]),
+    "lcpc_open_column": (i32, [vp, sz, u64p, u8p]),
+    "lcpc_transcript_new": (vp, [u8p, sz]),
+    "lcpc_transcript_clone": (vp, [vp]),
+    "lcpc_transcript_free": (None, [vp]),
+    "lcpc_transcript_append_message": (None, [vp, u8p, sz, u8p, sz]),
+    "lcpc_transcript_challenge_bytes": (None, [vp, u8p, sz, u8p, sz]),
+    "lcpc_prove": (i32, [vp, u64p, sz, vp, vp, C.POINTER(vp)]),
+    "lcpc_proof_free": (None, [vp]),
+    "lcpc_proof_n_cols": (sz, [vp]),
+    "lcpc_proof_n_per_row": (sz, [vp]),
+    "lcpc_proof_n_rows": (sz, [vp]),
+    "lcpc_proof_n_degree_tests": (sz, [vp]),
+    "lcpc_proof_n_col_opens": (sz, [vp]),
+    "lcpc_proof_path_len": (sz, [vp]),
+    "lcpc_proof_field": (i32, [vp]),
+    "lcpc_proof_copy_p_eval": (i32, [vp, u64p]),
+    "lcpc_proof_copy_p_random": (i32, [vp, sz, u64p]),
+    "lcpc_proof_copy_column": (i32, [vp, sz, u64p, u8p]),
+    "lcpc_proof_from_parts": (i32, [i32, sz, sz, sz, sz, sz, sz, u64p, u64p, u64p, u8p, C.POINTER(vp)]),
+    "lcpc_verify": (i32, [u8p, u64p, sz, u64p, sz, vp, vp, vp, u64p]),
+    "lcpc_collapse_columns": (i32, [i32, u64p, u64p, u64p, sz, sz]),
+    "lcpc_merkle_tree": (i32, [u8p, sz, u8p]),
+    "lcpc_verify_column_path": (i32, [i32, u64p, sz, u8p, sz, sz, u8p]),
+    "lcpc_verify_column_value": (i32, [i32, u64p, u64p, sz, u64p]),
+    "lcpc_hash_columns": (i32, [i32, u64p, sz, sz, u8p]),
+}
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Function names declared in include/lcpc_mi.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(lcpc_[a-z0-9_]+)\s*\(", text)))
+
+
+def load(path: str = LIB_PATH):
+    """Load liblcpc_mi.so; raises OSError if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise OSError(f"{path} not built: run `make -C {PKG_DIR}` (or __graft_entry__.build())")
+        lib = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    msg = load().lcpc_last_error()
+    return msg.decode() if msg else ""

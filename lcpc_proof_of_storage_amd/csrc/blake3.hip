@@ -1,0 +1,375 @@
+// blake3.hip -- column leaves and Merkle tree of an lcpc-2d commitment on gfx950.
+//
+// Replaces merkleize -> hash_columns / merkle_tree / merkle_layer (lcpc-2d/src/lib.rs:720-815)
+// with D = blake3::Hasher (blake3 1.5):
+//   leaf[j]  = BLAKE3(32 zero bytes || to_repr(comm[0][j]) || ... || to_repr(comm[n_rows-1][j]))
+//   node     = BLAKE3(left || right)            (a 64-byte message, not a BLAKE3 parent node)
+//   hashes   = [leaves (next_pow2(n_cols), zero-padded) | level 1 | ... | root]
+// plus the opening-side gathers (open_column, :818-855) and the verifier's path check
+// (verify_column_path, :985-1012).
+//
+// Leaves: the leaf message of a column is 32 + n_rows * B bytes (8224 B at 512 x Ft127), i.e.
+// several 1-KiB BLAKE3 chunks.  One thread owns one (column, chunk): a wave is 64 adjacent
+// columns of the same chunk, so every element load is a fully coalesced 1-KiB row segment of
+// the row-major codeword (no transpose).  Chunk chaining values of multi-chunk leaves go to a
+// [chunk][column] scratch (coalesced both ways) and a second kernel folds them with BLAKE3's
+// left-balanced tree (pairwise per level, odd node carried up, ROOT on the last parent).
+#include "field.hpp"
+#include "kernels.hpp"
+
+namespace lcpc {
+
+namespace {
+
+constexpr uint32_t IV0 = 0x6A09E667u, IV1 = 0xBB67AE85u, IV2 = 0x3C6EF372u, IV3 = 0xA54FF53Au,
+                   IV4 = 0x510E527Fu, IV5 = 0x9B05688Cu, IV6 = 0x1F83D9ABu, IV7 = 0x5BE0CD19u;
+enum : uint32_t { CHUNK_START = 1, CHUNK_END = 2, PARENT = 4, ROOT = 8 };
+
+// message schedule: round r uses m[SCHED[r][i]]  (permutation 2,6,3,10,7,0,4,13,1,11,12,5,9,14,15,8)
+__host__ __device__ constexpr int sched(int r, int i) {
+  constexpr int P[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+  int x = i;
+  for (int k = 0; k < r; k++) x = P[x];
+  return x;
+}
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_rotateright32(x, n); }
+
+#define B3G(a, b, c, d, mx, my)          \
+  a = a + b + (mx);                      \
+  d = rotr(d ^ a, 16);                   \
+  c = c + d;                             \
+  b = rotr(b ^ c, 12);                   \
+  a = a + b + (my);                      \
+  d = rotr(d ^ a, 8);                    \
+  c = c + d;                             \
+  b = rotr(b ^ c, 7);
+
+// cv = first half of compress(cv, m, counter, len, flags)
+__device__ __forceinline__ void compress(uint32_t cv[8], const uint32_t m[16], uint64_t counter,
+                                         uint32_t block_len, uint32_t flags) {
+  uint32_t s0 = cv[0], s1 = cv[1], s2 = cv[2], s3 = cv[3], s4 = cv[4], s5 = cv[5], s6 = cv[6],
+           s7 = cv[7];
+  uint32_t s8 = IV0, s9 = IV1, s10 = IV2, s11 = IV3;
+  uint32_t s12 = (uint32_t)counter, s13 = (uint32_t)(counter >> 32), s14 = block_len, s15 = flags;
+#pragma unroll
+  for (int r = 0; r < 7; r++) {
+    B3G(s0, s4, s8, s12, m[sched(r, 0)], m[sched(r, 1)]);
+    B3G(s1, s5, s9, s13, m[sched(r, 2)], m[sched(r, 3)]);
+    B3G(s2, s6, s10, s14, m[sched(r, 4)], m[sched(r, 5)]);
+    B3G(s3, s7, s11, s15, m[sched(r, 6)], m[sched(r, 7)]);
+    B3G(s0, s5, s10, s15, m[sched(r, 8)], m[sched(r, 9)]);
+    B3G(s1, s6, s11, s12, m[sched(r, 10)], m[sched(r, 11)]);
+    B3G(s2, s7, s8, s13, m[sched(r, 12)], m[sched(r, 13)]);
+    B3G(s3, s4, s9, s14, m[sched(r, 14)], m[sched(r, 15)]);
+  }
+  cv[0] = s0 ^ s8;
+  cv[1] = s1 ^ s9;
+  cv[2] = s2 ^ s10;
+  cv[3] = s3 ^ s11;
+  cv[4] = s4 ^ s12;
+  cv[5] = s5 ^ s13;
+  cv[6] = s6 ^ s14;
+  cv[7] = s7 ^ s15;
+}
+
+__device__ __forceinline__ void iv(uint32_t cv[8]) {
+  cv[0] = IV0; cv[1] = IV1; cv[2] = IV2; cv[3] = IV3;
+  cv[4] = IV4; cv[5] = IV5; cv[6] = IV6; cv[7] = IV7;
+}
+
+// BLAKE3 of a 64-byte message (one chunk, one block) = lcpc-2d Merkle node.
+__device__ __forceinline__ void hash64(const uint32_t m[16], uint32_t out[8]) {
+  iv(out);
+  compress(out, m, 0, 64, CHUNK_START | CHUNK_END | ROOT);
+}
+
+__device__ __forceinline__ void parent_cv(const uint32_t l[8], const uint32_t r[8], bool root,
+                                          uint32_t out[8]) {
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    m[i] = l[i];
+    m[8 + i] = r[i];
+  }
+  iv(out);
+  compress(out, m, 0, 64, PARENT | (root ? ROOT : 0u));
+}
+
+__device__ __forceinline__ void load8(const uint32_t *p, uint32_t v[8]) {
+  const uint4 a = reinterpret_cast<const uint4 *>(p)[0], b = reinterpret_cast<const uint4 *>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void store8(uint32_t *p, const uint32_t v[8]) {
+  reinterpret_cast<uint4 *>(p)[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<uint4 *>(p)[1] = make_uint4(v[4], v[5], v[6], v[7]);
+}
+
+// One thread per (column, chunk).  Message word w of a column: w < 8 is the zero prefix,
+// else word (w-8) % N of element row (w-8) / N.  N in {2, 4, 8} divides both 8 and 16, so
+// every 16-word block holds whole elements.
+template <class F>
+__global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict__ m,
+                                                     size_t n_rows, size_t n_cols,
+                                                     size_t row_stride, size_t col_stride,
+                                                     uint32_t *__restrict__ cvs,
+                                                     uint8_t *__restrict__ leaves, int n_chunks) {
+  constexpr int N = F::N;
+  static_assert(16 % N == 0 && 8 % N == 0, "element must tile a BLAKE3 block");
+  const size_t col = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int chunk = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (col >= n_cols || chunk >= n_chunks) return;
+  const size_t total_words = 8 + n_rows * N;
+  const size_t w0 = (size_t)chunk * 256;
+  const size_t cw = total_words - w0 < 256 ? total_words - w0 : 256;
+  const int nb = (int)((cw + 15) / 16);
+  uint32_t cv[8];
+  iv(cv);
+  const uint32_t *colp = m + col * col_stride * N;
+  for (int b = 0; b < nb; b++) {
+    const size_t gw = w0 + 16 * (size_t)b;
+    uint32_t msg[16];
+#pragma unroll
+    for (int k = 0; k < 16 / N; k++) {
+      const long long ew = (long long)gw + k * N - 8;  // element-stream word index
+      uint32_t w[N];
+      if (ew < 0) {
+#pragma unroll
+        for (int i = 0; i < N; i++) w[i] = 0;
+      } else {
+        const size_t row = (size_t)ew / N;
+        if (row < n_rows) {
+          fe_repr_words<F>(fe_load<F>(colp, row * row_stride), w);
+        } else {
+#pragma unroll
+          for (int i = 0; i < N; i++) w[i] = 0;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < N; i++) msg[k * N + i] = w[i];
+    }
+    const size_t left = cw - 16 * (size_t)b;
+    const uint32_t blen = left >= 16 ? 64u : (uint32_t)(4 * left);
+    uint32_t flags = b == 0 ? CHUNK_START : 0u;
+    if (b == nb - 1) flags |= CHUNK_END | (n_chunks == 1 ? ROOT : 0u);
+    compress(cv, msg, (uint64_t)chunk, blen, flags);
+  }
+  if (n_chunks == 1) {
+    store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
+  } else {
+    store8(cvs + ((size_t)chunk * n_cols + col) * 8, cv);
+  }
+}
+
+// Fold n_chunks chaining values of each column into its BLAKE3 root (in place in cvs).
+__global__ __launch_bounds__(256) void k_leaf_merge(uint32_t *__restrict__ cvs, size_t n_cols,
+                                                    int n_chunks, uint8_t *__restrict__ leaves) {
+  const size_t col = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= n_cols) return;
+  int nodes = n_chunks;
+  uint32_t l[8], r[8], o[8];
+  while (nodes > 1) {
+    const int pairs = nodes / 2;
+    for (int i = 0; i < pairs; i++) {
+      load8(cvs + ((size_t)(2 * i) * n_cols + col) * 8, l);
+      load8(cvs + ((size_t)(2 * i + 1) * n_cols + col) * 8, r);
+      parent_cv(l, r, nodes == 2, o);
+      store8(cvs + ((size_t)i * n_cols + col) * 8, o);
+    }
+    if (nodes & 1) {
+      load8(cvs + ((size_t)(nodes - 1) * n_cols + col) * 8, l);
+      store8(cvs + ((size_t)pairs * n_cols + col) * 8, l);
+    }
+    nodes = pairs + (nodes & 1);
+  }
+  load8(cvs + col * 8, o);
+  store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), o);
+}
+
+// Merkle levels: each workgroup folds 2^levels consecutive nodes of level `lvl` (starting at
+// element offset in_off of `hashes`) into one node, writing every intermediate level.
+// node(level l+1, i) = BLAKE3(node(l, 2i) || node(l, 2i+1)).
+__global__ __launch_bounds__(256) void k_merkle(uint8_t *__restrict__ hashes, size_t np2,
+                                                int lvl, int levels) {
+  __shared__ __align__(16) uint32_t buf[2][256 * 8];
+  const int tid = threadIdx.x;
+  size_t n_in = np2 >> lvl;
+  size_t base_in = 2 * np2 - 2 * n_in;  // offset of level lvl
+  const int width = 1 << levels;         // input nodes per workgroup (<= 512)
+  const size_t first = (size_t)blockIdx.x * width;
+  // level lvl -> lvl+1 straight from global
+  int cur = 0;
+  for (int i = tid; i < width / 2; i += 256) {
+    uint32_t msg[16], o[8];
+    load8(reinterpret_cast<const uint32_t *>(hashes + 32 * (base_in + first + 2 * i)), msg);
+    load8(reinterpret_cast<const uint32_t *>(hashes + 32 * (base_in + first + 2 * i + 1)), msg + 8);
+    hash64(msg, o);
+#pragma unroll
+    for (int k = 0; k < 8; k++) buf[cur][i * 8 + k] = o[k];
+    store8(reinterpret_cast<uint32_t *>(hashes + 32 * (base_in + n_in + first / 2 + i)), o);
+  }
+  base_in += n_in;
+  n_in /= 2;
+  size_t f = first / 2;
+  for (int l = 1; l < levels; l++) {
+    __syncthreads();
+    const int cnt = width >> (l + 1);
+    for (int i = tid; i < cnt; i += 256) {
+      uint32_t msg[16], o[8];
+#pragma unroll
+      for (int k = 0; k < 16; k++) msg[k] = buf[cur][2 * i * 8 + k];
+      hash64(msg, o);
+#pragma unroll
+      for (int k = 0; k < 8; k++) buf[cur ^ 1][i * 8 + k] = o[k];
+      store8(reinterpret_cast<uint32_t *>(hashes + 32 * (base_in + n_in + f / 2 + i)), o);
+    }
+    cur ^= 1;
+    base_in += n_in;
+    n_in /= 2;
+    f /= 2;
+  }
+}
+
+template <class F>
+__global__ void k_gather_cols(const uint32_t *__restrict__ m, size_t n_rows, size_t n_cols,
+                              const uint64_t *__restrict__ idx, size_t n_idx,
+                              uint32_t *__restrict__ cols) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_idx * n_rows) return;
+  const size_t k = t / n_rows, r = t % n_rows;
+  fe_store<F>(cols, t, fe_load<F>(m, r * n_cols + idx[k]));
+}
+
+__global__ void k_gather_paths(const uint8_t *__restrict__ hashes, size_t np2,
+                               const uint64_t *__restrict__ idx, size_t n_idx, size_t path_len,
+                               uint8_t *__restrict__ paths) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_idx * path_len) return;
+  const size_t k = t / path_len, i = t % path_len;
+  const size_t base = 2 * np2 - 2 * (np2 >> i);
+  const size_t other = (idx[k] >> i) ^ 1;
+  uint32_t v[8];
+  load8(reinterpret_cast<const uint32_t *>(hashes + 32 * (base + other)), v);
+  store8(reinterpret_cast<uint32_t *>(paths + 32 * t), v);
+}
+
+__global__ void k_path_checks(const uint8_t *__restrict__ leaves, const uint8_t *__restrict__ paths,
+                              size_t n, size_t path_len, const uint64_t *__restrict__ idx,
+                              const uint8_t *__restrict__ root, uint32_t *__restrict__ flags) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  uint32_t h[8], msg[16];
+  load8(reinterpret_cast<const uint32_t *>(leaves + 32 * k), h);
+  size_t col = idx[k];
+  for (size_t i = 0; i < path_len; i++) {
+    uint32_t p[8];
+    load8(reinterpret_cast<const uint32_t *>(paths + 32 * (k * path_len + i)), p);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      msg[q] = (col & 1) ? p[q] : h[q];
+      msg[8 + q] = (col & 1) ? h[q] : p[q];
+    }
+    hash64(msg, h);
+    col >>= 1;
+  }
+  uint32_t rt[8];
+  load8(reinterpret_cast<const uint32_t *>(root), rt);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) diff |= h[q] ^ rt[q];
+  flags[k] = diff == 0;
+}
+
+}  // namespace
+
+size_t leaf_hash_scratch_bytes(int fid, size_t n_rows, size_t n_cols) {
+  const size_t words = 8 + n_rows * (size_t)field_words(fid);
+  const size_t n_chunks = (words + 255) / 256;
+  return n_chunks > 1 ? n_chunks * n_cols * 32 : 0;
+}
+
+static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
+                                      size_t row_stride, size_t col_stride, uint8_t *leaves,
+                                      void *scratch, hipStream_t s) {
+  if (n_cols == 0) return hipSuccess;
+  const size_t words = 8 + n_rows * (size_t)field_words(fid);
+  const int n_chunks = (int)((words + 255) / 256);
+  dim3 grid((unsigned)((n_cols + 63) / 64), (unsigned)((n_chunks + 3) / 4));
+  hipError_t e = dispatch_field(fid, [&]<class F>() {
+    if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
+      hipLaunchKernelGGL((k_leaf_chunks<F>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
+                         col_stride, (uint32_t *)scratch, leaves, n_chunks);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
+  });
+  if (e != hipSuccess || n_chunks == 1) return e;
+  hipLaunchKernelGGL(k_leaf_merge, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, s,
+                     (uint32_t *)scratch, n_cols, n_chunks, leaves);
+  return hipGetLastError();
+}
+
+hipError_t leaf_hashes(int fid, const uint32_t *m, size_t n_rows, size_t n_cols, size_t stride,
+                       uint8_t *leaves, void *scratch, hipStream_t s) {
+  return leaf_hashes_strided(fid, m, n_rows, n_cols, stride, 1, leaves, scratch, s);
+}
+
+hipError_t leaf_hashes_cols(int fid, const uint32_t *cols, size_t n_rows, size_t n_cols,
+                            uint8_t *leaves, void *scratch, hipStream_t s) {
+  // cols laid out [column][row]
+  return leaf_hashes_strided(fid, cols, n_rows, n_cols, 1, n_rows, leaves, scratch, s);
+}
+
+hipError_t merkle_tree(uint8_t *hashes, size_t np2, hipStream_t s) {
+  int lvl = 0;
+  size_t n = np2;
+  while (n > 1) {
+    int levels = 0;
+    while (levels < 9 && ((size_t)1 << (levels + 1)) <= n) levels++;
+    const size_t blocks = n >> levels;
+    hipLaunchKernelGGL(k_merkle, dim3((unsigned)blocks), dim3(256), 0, s, hashes, np2, lvl, levels);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    lvl += levels;
+    n >>= levels;
+  }
+  return hipSuccess;
+}
+
+hipError_t merkle_tree_io(const uint8_t *ins, size_t n_ins, uint8_t *outs, hipStream_t s) {
+  // requires outs to directly follow ins in one buffer (as lcpc-2d's `hashes` split)
+  if (outs != ins + 32 * n_ins) return hipErrorInvalidValue;
+  return merkle_tree(const_cast<uint8_t *>(ins), n_ins, s);
+}
+
+hipError_t gather_columns(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
+                          const uint64_t *idx, size_t n_idx, uint32_t *cols, hipStream_t s) {
+  const size_t n = n_idx * n_rows;
+  if (!n) return hipSuccess;
+  return dispatch_field(fid, [&]<class F>() {
+    hipLaunchKernelGGL((k_gather_cols<F>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, m,
+                       n_rows, n_cols, idx, n_idx, cols);
+    return hipGetLastError();
+  });
+}
+
+hipError_t gather_paths(const uint8_t *hashes, size_t n_hashes, const uint64_t *idx, size_t n_idx,
+                        size_t path_len, uint8_t *paths, hipStream_t s) {
+  const size_t n = n_idx * path_len;
+  if (!n) return hipSuccess;
+  const size_t np2 = (n_hashes + 1) / 2;
+  hipLaunchKernelGGL(k_gather_paths, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hashes,
+                     np2, idx, n_idx, path_len, paths);
+  return hipGetLastError();
+}
+
+hipError_t path_checks(const uint8_t *leaves, const uint8_t *paths, size_t n, size_t path_len,
+                       const uint64_t *idx, const uint8_t *root, uint32_t *flags, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_path_checks, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, leaves, paths,
+                     n, path_len, idx, root, flags);
+  return hipGetLastError();
+}
+
+}  // namespace lcpc

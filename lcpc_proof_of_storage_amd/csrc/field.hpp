@@ -1,0 +1,279 @@
+// field.hpp -- prime-field arithmetic for gfx950 (CDNA4), 32-bit limbs, Montgomery form.
+//
+// Element layout = the reference's ff_derive internal representation (lcpc-test-fields
+// src/lib.rs:13-70: `struct FtX([u64; N])`, value*R mod p with R = 2^(64N), limbs little
+// endian), viewed as 2N little-endian u32 words.  Every result is fully reduced (< p), as
+// ff_derive's, so the words written back are bit-identical to the reference's.
+//
+// Arithmetic: CIOS Montgomery multiplication on 32-bit words with v_mad_u64_u32
+// (32x32+64 -> 64), add/sub with carry chains.  Every prime the reference declares has
+// p = 1 mod 2^32, so -p^-1 mod 2^32 = 0xffffffff and p[0] = 1: the reduction step's quotient
+// is m = -t0 and m*p[0] + t0 contributes only the carry (t0 != 0); the generic path stays for
+// completeness.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "field_params.hpp"
+
+namespace lcpc {
+
+template <class F>
+struct Fe {
+  uint32_t v[F::N];
+};
+
+template <class F>
+__device__ __forceinline__ Fe<F> fe_zero() {
+  Fe<F> r;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = 0;
+  return r;
+}
+
+template <class F>
+__device__ __forceinline__ Fe<F> fe_one() {
+  Fe<F> r;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = F::ONE[i];
+  return r;
+}
+
+template <class F>
+__device__ __forceinline__ bool fe_is_zero(const Fe<F>& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) o |= a.v[i];
+  return o == 0;
+}
+
+template <class F>
+__device__ __forceinline__ bool fe_eq(const Fe<F>& a, const Fe<F>& b) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) o |= a.v[i] ^ b.v[i];
+  return o == 0;
+}
+
+// r = a + b mod p  (a, b < p)
+template <class F>
+__device__ __forceinline__ Fe<F> fe_add(const Fe<F>& a, const Fe<F>& b) {
+  Fe<F> t, u;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) t.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) u.v[i] = __builtin_subc(t.v[i], F::P[i], br, &br);
+  // t >= p  <=>  carry out of the add, or no borrow out of t - p
+  const bool take_u = c | (br ^ 1u);
+  Fe<F> r;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = take_u ? u.v[i] : t.v[i];
+  return r;
+}
+
+// r = a - b mod p
+template <class F>
+__device__ __forceinline__ Fe<F> fe_sub(const Fe<F>& a, const Fe<F>& b) {
+  Fe<F> t, u;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) t.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) u.v[i] = __builtin_addc(t.v[i], F::P[i], c, &c);
+  Fe<F> r;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = br ? u.v[i] : t.v[i];
+  return r;
+}
+
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  return (uint64_t)a * (uint64_t)b + c;
+}
+
+// Montgomery product a*b*R^-1 mod p, R = 2^(32N)  (CIOS, 32-bit words)
+template <class F>
+__device__ __forceinline__ Fe<F> fe_mul(const Fe<F>& a, const Fe<F>& b) {
+  constexpr int N = F::N;
+  uint32_t t[N + 2];
+#pragma unroll
+  for (int i = 0; i < N + 2; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    // t += a * b[i]
+    uint32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      uint64_t s = mad64(a.v[j], b.v[i], (uint64_t)t[j] + carry);
+      t[j] = (uint32_t)s;
+      carry = (uint32_t)(s >> 32);
+    }
+    {
+      uint32_t c2 = 0;
+      t[N] = __builtin_addc(t[N], carry, 0u, &c2);
+      t[N + 1] = c2;
+    }
+    // t = (t + m p) / 2^32
+    uint32_t c;
+    if constexpr (F::NP == 0xffffffffu && F::P[0] == 1u) {
+      // m = -t0; m*p0 + t0 = 2^32 * (t0 != 0)
+      const uint32_t m = 0u - t[0];
+      c = t[0] != 0u;
+#pragma unroll
+      for (int j = 1; j < N; j++) {
+        uint64_t s = mad64(m, F::P[j], (uint64_t)t[j] + c);
+        t[j - 1] = (uint32_t)s;
+        c = (uint32_t)(s >> 32);
+      }
+    } else {
+      const uint32_t m = t[0] * F::NP;
+      uint64_t s0 = mad64(m, F::P[0], (uint64_t)t[0]);
+      c = (uint32_t)(s0 >> 32);
+#pragma unroll
+      for (int j = 1; j < N; j++) {
+        uint64_t s = mad64(m, F::P[j], (uint64_t)t[j] + c);
+        t[j - 1] = (uint32_t)s;
+        c = (uint32_t)(s >> 32);
+      }
+    }
+    uint32_t c3 = 0;
+    t[N - 1] = __builtin_addc(t[N], c, 0u, &c3);
+    t[N] = t[N + 1] + c3;
+  }
+  // conditional final subtraction
+  Fe<F> u, r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) u.v[i] = __builtin_subc(t[i], F::P[i], br, &br);
+  const bool take_u = (t[N] != 0u) | (br ^ 1u);
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = take_u ? u.v[i] : t[i];
+  return r;
+}
+
+template <class F>
+__device__ __forceinline__ Fe<F> fe_sqr(const Fe<F>& a) {
+  return fe_mul<F>(a, a);
+}
+
+// a^e for a small exponent (square-and-multiply, MSB first)
+template <class F>
+__device__ __forceinline__ Fe<F> fe_pow(Fe<F> a, uint64_t e) {
+  Fe<F> acc = fe_one<F>();
+  while (e) {
+    if (e & 1) acc = fe_mul<F>(acc, a);
+    a = fe_sqr<F>(a);
+    e >>= 1;
+  }
+  return acc;
+}
+
+// canonical (non-Montgomery) value of a: a * R^-1 mod p (Montgomery reduction of a
+// single-width value; a < p so the result is < p without a final subtraction)
+template <class F>
+__device__ __forceinline__ Fe<F> fe_from_mont(const Fe<F>& a) {
+  constexpr int N = F::N;
+  uint32_t t[N + 1];
+#pragma unroll
+  for (int i = 0; i < N; i++) t[i] = a.v[i];
+  t[N] = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const uint32_t m = t[0] * F::NP;
+    uint64_t s0 = mad64(m, F::P[0], (uint64_t)t[0]);
+    uint32_t c = (uint32_t)(s0 >> 32);
+#pragma unroll
+    for (int j = 1; j < N; j++) {
+      uint64_t s = mad64(m, F::P[j], (uint64_t)t[j] + c);
+      t[j - 1] = (uint32_t)s;
+      c = (uint32_t)(s >> 32);
+    }
+    t[N - 1] = t[N] + c;
+    t[N] = 0;
+  }
+  Fe<F> r;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = t[i];
+  return r;
+}
+
+// Montgomery form of a canonical value a < p: a * R^2 * R^-1
+template <class F>
+__device__ __forceinline__ Fe<F> fe_to_mont(const Fe<F>& a) {
+  Fe<F> r2;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r2.v[i] = F::R2[i];
+  return fe_mul<F>(a, r2);
+}
+
+// 32-bit words of to_repr(a) as they appear in a byte stream read as little-endian u32:
+// ff_derive's to_repr is the canonical value little endian (big endian for Ft253_192).
+template <class F>
+__device__ __forceinline__ void fe_repr_words(const Fe<F>& a, uint32_t* w) {
+  const Fe<F> c = fe_from_mont<F>(a);
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {
+    if constexpr (F::BE_REPR)
+      w[i] = __builtin_bswap32(c.v[F::N - 1 - i]);
+    else
+      w[i] = c.v[i];
+  }
+}
+
+// ---------------------------------------------------------------- memory
+// Elements are 8/16/24/32 bytes; move them with the widest aligned vector loads.
+template <class F>
+__device__ __forceinline__ Fe<F> fe_load(const uint32_t* __restrict__ base, size_t idx) {
+  Fe<F> r;
+  const uint32_t* p = base + idx * F::N;
+  if constexpr (F::N % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < F::N / 4; k++) {
+      uint4 q = reinterpret_cast<const uint4*>(p)[k];
+      r.v[4 * k] = q.x;
+      r.v[4 * k + 1] = q.y;
+      r.v[4 * k + 2] = q.z;
+      r.v[4 * k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < F::N / 2; k++) {
+      uint2 q = reinterpret_cast<const uint2*>(p)[k];
+      r.v[2 * k] = q.x;
+      r.v[2 * k + 1] = q.y;
+    }
+  }
+  return r;
+}
+
+template <class F>
+__device__ __forceinline__ void fe_store(uint32_t* __restrict__ base, size_t idx, const Fe<F>& x) {
+  uint32_t* p = base + idx * F::N;
+  if constexpr (F::N % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < F::N / 4; k++)
+      reinterpret_cast<uint4*>(p)[k] =
+          make_uint4(x.v[4 * k], x.v[4 * k + 1], x.v[4 * k + 2], x.v[4 * k + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < F::N / 2; k++)
+      reinterpret_cast<uint2*>(p)[k] = make_uint2(x.v[2 * k], x.v[2 * k + 1]);
+  }
+}
+
+// field dispatch helper: calls fn.template operator()<F>()
+template <class Fn>
+inline auto dispatch_field(int fid, Fn&& fn) {
+  switch (fid) {
+    case 0: return fn.template operator()<Ft63>();
+    case 1: return fn.template operator()<Ft127>();
+    case 2: return fn.template operator()<Ft191>();
+    case 3: return fn.template operator()<Ft255>();
+    default: return fn.template operator()<Ft253_192>();
+  }
+}
+
+}  // namespace lcpc

@@ -1,0 +1,79 @@
+// kernels.hpp -- host-side launchers of the gfx950 kernels (internal to liblcpc_mi.so).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace lcpc {
+
+// Bytes per element of field `fid` (8, 16, 24, 32) and 32-bit words per element.
+int field_words(int fid);
+inline int field_bytes(int fid) { return 4 * field_words(fid); }
+bool field_gpu_supported(int fid);
+
+// ------------------------------------------------------------------ NTT (Ligero encode)
+// fffft::fft_io semantics on rows of length n = 2^log_n: out[bitrev(j)] = sum_i in[i] w^(ij),
+// w = ROOT_OF_UNITY^(2^(S - log_n)).  Two passes (four-step):
+//   pass A: 2^l1-point DIF down each of the 2^l2 columns of the row viewed as [2^l1][2^l2],
+//           input zero-padded past n_valid, then the inter-pass twiddle w^(c * bitrev(t'));
+//   pass B: 2^l2-point DIF along each contiguous block.
+struct NttPlan {
+  int fid = -1;
+  int log_n = 0, l1 = 0, l2 = 0;
+  uint32_t *d_tw = nullptr;  // w^e, e in [0, n): n elements (Montgomery)
+};
+hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream_t s);
+void ntt_plan_free(NttPlan &p);
+// rows r in [0, n_rows): in = src + r * src_stride (elements), n_valid leading elements
+// (rest zero); out = dst + r * dst_stride (n elements).  src may alias dst only if
+// src_stride == dst_stride and n_valid == n (in-place full-length transform).
+hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
+                    uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s);
+
+// ------------------------------------------------------------------ BLAKE3 / Merkle
+// leaf[j] = BLAKE3(32 zero bytes || repr(m[0][j]) || ... || repr(m[n_rows-1][j]))
+// for j in [0, n_cols); m is row-major with row stride `stride` elements.
+size_t leaf_hash_scratch_bytes(int fid, size_t n_rows, size_t n_cols);
+hipError_t leaf_hashes(int fid, const uint32_t *m, size_t n_rows, size_t n_cols, size_t stride,
+                       uint8_t *leaves, void *scratch, hipStream_t s);
+// same, for a [column][row] matrix (opened columns of a proof)
+hipError_t leaf_hashes_cols(int fid, const uint32_t *cols, size_t n_rows, size_t n_cols,
+                            uint8_t *leaves, void *scratch, hipStream_t s);
+// hashes = [leaves (np2) | level 1 (np2/2) | ... | root]; fills every level above the leaves
+hipError_t merkle_tree(uint8_t *hashes, size_t np2, hipStream_t s);
+// generic Merkle over ins (n_ins = outs + 1 nodes, power of two) -> outs
+hipError_t merkle_tree_io(const uint8_t *ins, size_t n_ins, uint8_t *outs, hipStream_t s);
+
+// ------------------------------------------------------------------ prover helpers
+// out[t][c] = sum_r tensors[t][r] * coeffs[r][c]   (t < n_tensors, c < n_per_row)
+size_t collapse_scratch_bytes(int fid, size_t n_rows, size_t n_per_row, int n_tensors);
+hipError_t collapse_rows(int fid, const uint32_t *coeffs, size_t n_rows, size_t n_per_row,
+                         const uint32_t *tensors, int n_tensors, uint32_t *out, void *scratch,
+                         hipStream_t s);
+// cols[k][r] = m[r][idx[k]]; paths[k][i] = sibling digests of leaf idx[k]
+hipError_t gather_columns(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
+                          const uint64_t *idx, size_t n_idx, uint32_t *cols, hipStream_t s);
+hipError_t gather_paths(const uint8_t *hashes, size_t n_hashes, const uint64_t *idx,
+                        size_t n_idx, size_t path_len, uint8_t *paths, hipStream_t s);
+
+// ------------------------------------------------------------------ verifier helpers
+// dots[k][t] = sum_r tensors[t][r] * cols[k][r]; ok[k] bit t set iff dots == enc[t][idx[k]]
+hipError_t column_checks(int fid, const uint32_t *cols, size_t n_cols_open, size_t n_rows,
+                         const uint32_t *tensors, int n_tensors, const uint32_t *encs,
+                         size_t enc_len, const uint64_t *idx, uint32_t *flags, hipStream_t s);
+// path[k] check against root: flags[k] = 1 iff the Merkle path of leaf k verifies
+hipError_t path_checks(const uint8_t *leaves, const uint8_t *paths, size_t n, size_t path_len,
+                       const uint64_t *idx, const uint8_t *root, uint32_t *flags,
+                       hipStream_t s);
+// out = sum_i a[i] * b[i]
+hipError_t dot(int fid, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out,
+               void *scratch, hipStream_t s);
+// elementwise Montgomery <-> canonical conversion (device)
+hipError_t convert(int fid, const uint32_t *in, uint32_t *out, size_t n, bool to_mont,
+                   hipStream_t s);
+// chunk-local self-test entry: out = a * b elementwise (Montgomery)
+hipError_t mul_elementwise(int fid, const uint32_t *a, const uint32_t *b, uint32_t *out,
+                           size_t n, hipStream_t s);
+
+}  // namespace lcpc

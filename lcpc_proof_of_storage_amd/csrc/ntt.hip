@@ -1,0 +1,59 @@
+// ntt.hip -- Ligero encode plan / dispatch (kernels: ntt_impl.hpp, one TU per field).
+#include "kernels.hpp"
+#include "field.hpp"
+
+namespace lcpc {
+
+#define DECL(n)                                                                                   \
+  hipError_t ntt_rows_##n(const NttPlan &, const uint32_t *, size_t, size_t, uint32_t *, size_t, \
+                          size_t, hipStream_t);                                                   \
+  hipError_t ntt_tw_table_##n(uint32_t *, int, bool, hipStream_t);
+DECL(ft63)
+DECL(ft127)
+DECL(ft255)
+DECL(ft253)
+#undef DECL
+
+int field_words(int fid) {
+  return dispatch_field(fid, []<class F>() { return F::N; });
+}
+
+bool field_gpu_supported(int fid) { return fid == 0 || fid == 1 || fid == 3 || fid == 4; }
+
+int ntt_max_log_n(int fid) { return fid == 3 || fid == 4 ? 22 : 24; }
+
+hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream_t s) {
+  if (!field_gpu_supported(fid) || log_n < 0 || log_n > ntt_max_log_n(fid))
+    return hipErrorInvalidValue;
+  p.fid = fid;
+  p.log_n = log_n;
+  p.l1 = log_n / 2;
+  p.l2 = log_n - p.l1;
+  const size_t n = (size_t)1 << log_n;
+  hipError_t e = hipMalloc(&p.d_tw, n * field_bytes(fid));
+  if (e != hipSuccess) return e;
+  switch (fid) {
+    case 0: return ntt_tw_table_ft63(p.d_tw, log_n, inverse, s);
+    case 1: return ntt_tw_table_ft127(p.d_tw, log_n, inverse, s);
+    case 3: return ntt_tw_table_ft255(p.d_tw, log_n, inverse, s);
+    default: return ntt_tw_table_ft253(p.d_tw, log_n, inverse, s);
+  }
+}
+
+void ntt_plan_free(NttPlan &p) {
+  if (p.d_tw) (void)hipFree(p.d_tw);
+  p.d_tw = nullptr;
+}
+
+hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
+                    uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s) {
+  switch (p.fid) {
+    case 0: return ntt_rows_ft63(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s);
+    case 1: return ntt_rows_ft127(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s);
+    case 3: return ntt_rows_ft255(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s);
+    case 4: return ntt_rows_ft253(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace lcpc

@@ -1,0 +1,310 @@
+// transcript.cpp -- merlin / STROBE-128 / Keccak-f[1600], ChaCha20Rng, Uniform, Field::random.
+// See transcript.hpp.  Semantics follow the published crates the reference pins
+// (Cargo.toml:25 merlin 2.0, :32-34 rand 0.8 / rand_chacha 0.3 / rand_core 0.6, :15 ff 0.13).
+#include "transcript.hpp"
+
+namespace lcpc {
+
+namespace {
+constexpr uint64_t RC[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808aULL, 0x8000000080008000ULL,
+    0x000000000000808bULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+    0x000000000000008aULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000aULL,
+    0x000000008000808bULL, 0x800000000000008bULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+    0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800aULL, 0x800000008000000aULL,
+    0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+inline uint64_t rol(uint64_t x, int n) { return (x << n) | (x >> ((64 - n) & 63)); }
+constexpr uint8_t STROBE_R = 166;
+enum : uint8_t { FLAG_I = 1, FLAG_A = 2, FLAG_C = 4, FLAG_T = 8, FLAG_M = 16, FLAG_K = 32 };
+}  // namespace
+
+// Keccak-f[1600], lanes in registers, rho/pi folded into one pass per round.
+void keccak_f1600(uint64_t s[25]) {
+  uint64_t a00 = s[0], a01 = s[1], a02 = s[2], a03 = s[3], a04 = s[4];
+  uint64_t a05 = s[5], a06 = s[6], a07 = s[7], a08 = s[8], a09 = s[9];
+  uint64_t a10 = s[10], a11 = s[11], a12 = s[12], a13 = s[13], a14 = s[14];
+  uint64_t a15 = s[15], a16 = s[16], a17 = s[17], a18 = s[18], a19 = s[19];
+  uint64_t a20 = s[20], a21 = s[21], a22 = s[22], a23 = s[23], a24 = s[24];
+  for (int r = 0; r < 24; r++) {
+    const uint64_t c0 = a00 ^ a05 ^ a10 ^ a15 ^ a20, c1 = a01 ^ a06 ^ a11 ^ a16 ^ a21,
+                   c2 = a02 ^ a07 ^ a12 ^ a17 ^ a22, c3 = a03 ^ a08 ^ a13 ^ a18 ^ a23,
+                   c4 = a04 ^ a09 ^ a14 ^ a19 ^ a24;
+    const uint64_t d0 = c4 ^ rol(c1, 1), d1 = c0 ^ rol(c2, 1), d2 = c1 ^ rol(c3, 1),
+                   d3 = c2 ^ rol(c4, 1), d4 = c3 ^ rol(c0, 1);
+    // theta + rho + pi: b[y][2x+3y] = rot(a[x][y] ^ d[x], r[x][y])
+    const uint64_t b00 = a00 ^ d0;
+    const uint64_t b10 = rol(a01 ^ d1, 1);
+    const uint64_t b20 = rol(a02 ^ d2, 62);
+    const uint64_t b05 = rol(a03 ^ d3, 28);
+    const uint64_t b15 = rol(a04 ^ d4, 27);
+    const uint64_t b16 = rol(a05 ^ d0, 36);
+    const uint64_t b01 = rol(a06 ^ d1, 44);
+    const uint64_t b11 = rol(a07 ^ d2, 6);
+    const uint64_t b21 = rol(a08 ^ d3, 55);
+    const uint64_t b06 = rol(a09 ^ d4, 20);
+    const uint64_t b07 = rol(a10 ^ d0, 3);
+    const uint64_t b17 = rol(a11 ^ d1, 10);
+    const uint64_t b02 = rol(a12 ^ d2, 43);
+    const uint64_t b12 = rol(a13 ^ d3, 25);
+    const uint64_t b22 = rol(a14 ^ d4, 39);
+    const uint64_t b23 = rol(a15 ^ d0, 41);
+    const uint64_t b08 = rol(a16 ^ d1, 45);
+    const uint64_t b18 = rol(a17 ^ d2, 15);
+    const uint64_t b03 = rol(a18 ^ d3, 21);
+    const uint64_t b13 = rol(a19 ^ d4, 8);
+    const uint64_t b14 = rol(a20 ^ d0, 18);
+    const uint64_t b24 = rol(a21 ^ d1, 2);
+    const uint64_t b09 = rol(a22 ^ d2, 61);
+    const uint64_t b19 = rol(a23 ^ d3, 56);
+    const uint64_t b04 = rol(a24 ^ d4, 14);
+    // chi + iota (lane index x + 5y)
+    a00 = b00 ^ (~b01 & b02) ^ RC[r];
+    a01 = b01 ^ (~b02 & b03);
+    a02 = b02 ^ (~b03 & b04);
+    a03 = b03 ^ (~b04 & b00);
+    a04 = b04 ^ (~b00 & b01);
+    a05 = b05 ^ (~b06 & b07);
+    a06 = b06 ^ (~b07 & b08);
+    a07 = b07 ^ (~b08 & b09);
+    a08 = b08 ^ (~b09 & b05);
+    a09 = b09 ^ (~b05 & b06);
+    a10 = b10 ^ (~b11 & b12);
+    a11 = b11 ^ (~b12 & b13);
+    a12 = b12 ^ (~b13 & b14);
+    a13 = b13 ^ (~b14 & b10);
+    a14 = b14 ^ (~b10 & b11);
+    a15 = b15 ^ (~b16 & b17);
+    a16 = b16 ^ (~b17 & b18);
+    a17 = b17 ^ (~b18 & b19);
+    a18 = b18 ^ (~b19 & b15);
+    a19 = b19 ^ (~b15 & b16);
+    a20 = b20 ^ (~b21 & b22);
+    a21 = b21 ^ (~b22 & b23);
+    a22 = b22 ^ (~b23 & b24);
+    a23 = b23 ^ (~b24 & b20);
+    a24 = b24 ^ (~b20 & b21);
+  }
+  s[0] = a00; s[1] = a01; s[2] = a02; s[3] = a03; s[4] = a04;
+  s[5] = a05; s[6] = a06; s[7] = a07; s[8] = a08; s[9] = a09;
+  s[10] = a10; s[11] = a11; s[12] = a12; s[13] = a13; s[14] = a14;
+  s[15] = a15; s[16] = a16; s[17] = a17; s[18] = a18; s[19] = a19;
+  s[20] = a20; s[21] = a21; s[22] = a22; s[23] = a23; s[24] = a24;
+}
+
+// ------------------------------------------------------------------ STROBE-128 (merlin strobe.rs)
+Strobe128::Strobe128(const uint8_t *proto, size_t n) {
+  std::memset(st_, 0, sizeof(st_));
+  const uint8_t init[18] = {1, STROBE_R + 2, 1, 0, 1, 96, 'S', 'T', 'R', 'O', 'B', 'E',
+                            'v', '1', '.', '0', '.', '2'};
+  std::memcpy(bytes(), init, sizeof(init));
+  keccak_f1600(st_);
+  meta_ad(proto, n, false);
+}
+
+void Strobe128::run_f() {
+  uint8_t *b = bytes();
+  b[pos_] ^= pos_begin_;
+  b[pos_ + 1] ^= 0x04;
+  b[STROBE_R + 1] ^= 0x80;
+  keccak_f1600(st_);
+  pos_ = 0;
+  pos_begin_ = 0;
+}
+
+void Strobe128::absorb(const uint8_t *d, size_t n) {
+  uint8_t *b = bytes();
+  while (n) {
+    size_t take = STROBE_R - pos_;
+    if (take > n) take = n;
+    for (size_t i = 0; i < take; i++) b[pos_ + i] ^= d[i];
+    pos_ = (uint8_t)(pos_ + take);
+    d += take;
+    n -= take;
+    if (pos_ == STROBE_R) run_f();
+  }
+}
+
+void Strobe128::squeeze(uint8_t *d, size_t n) {
+  uint8_t *b = bytes();
+  for (size_t i = 0; i < n; i++) {
+    d[i] = b[pos_];
+    b[pos_] = 0;
+    pos_++;
+    if (pos_ == STROBE_R) run_f();
+  }
+}
+
+void Strobe128::begin_op(uint8_t flags, bool more) {
+  if (more) return;  // continuing the same operation (merlin asserts the flags match)
+  const uint8_t old_begin = pos_begin_;
+  pos_begin_ = (uint8_t)(pos_ + 1);
+  cur_flags_ = flags;
+  const uint8_t hdr[2] = {old_begin, flags};
+  absorb(hdr, 2);
+  if ((flags & (FLAG_C | FLAG_K)) && pos_ != 0) run_f();
+}
+
+void Strobe128::meta_ad(const uint8_t *d, size_t n, bool more) {
+  begin_op(FLAG_M | FLAG_A, more);
+  absorb(d, n);
+}
+void Strobe128::ad(const uint8_t *d, size_t n, bool more) {
+  begin_op(FLAG_A, more);
+  absorb(d, n);
+}
+void Strobe128::prf(uint8_t *d, size_t n, bool more) {
+  begin_op(FLAG_I | FLAG_A | FLAG_C, more);
+  squeeze(d, n);
+}
+
+// ------------------------------------------------------------------ merlin Transcript
+static const uint8_t MERLIN_LABEL[] = "Merlin v1.0";
+
+Transcript::Transcript(const uint8_t *label, size_t n) : s_(MERLIN_LABEL, 11) {
+  append_message(reinterpret_cast<const uint8_t *>("dom-sep"), 7, label, n);
+}
+
+void Transcript::append_message(const uint8_t *label, size_t ln, const uint8_t *msg, size_t mn) {
+  const uint8_t len4[4] = {(uint8_t)mn, (uint8_t)(mn >> 8), (uint8_t)(mn >> 16), (uint8_t)(mn >> 24)};
+  s_.meta_ad(label, ln, false);
+  s_.meta_ad(len4, 4, true);
+  s_.ad(msg, mn, false);
+}
+
+void Transcript::append_messages(const uint8_t *label, size_t ln, const uint8_t *msgs,
+                                 size_t msg_len, size_t n_msgs) {
+  for (size_t i = 0; i < n_msgs; i++) append_message(label, ln, msgs + i * msg_len, msg_len);
+}
+
+void Transcript::challenge_bytes(const uint8_t *label, size_t ln, uint8_t *dst, size_t n) {
+  const uint8_t len4[4] = {(uint8_t)n, (uint8_t)(n >> 8), (uint8_t)(n >> 16), (uint8_t)(n >> 24)};
+  s_.meta_ad(label, ln, false);
+  s_.meta_ad(len4, 4, true);
+  s_.prf(dst, n, false);
+}
+
+// ------------------------------------------------------------------ ChaCha20Rng
+namespace {
+inline uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+inline void qr(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+  a += b; d ^= a; d = rotl32(d, 16);
+  c += d; b ^= c; b = rotl32(b, 12);
+  a += b; d ^= a; d = rotl32(d, 8);
+  c += d; b ^= c; b = rotl32(b, 7);
+}
+}  // namespace
+
+ChaCha20Rng::ChaCha20Rng(const uint8_t seed[32], int rounds) : rounds_(rounds) {
+  for (int i = 0; i < 8; i++)
+    key_[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) |
+              ((uint32_t)seed[4 * i + 2] << 16) | ((uint32_t)seed[4 * i + 3] << 24);
+}
+
+ChaCha20Rng ChaCha20Rng::seed_from_u64(uint64_t state, int rounds) {
+  uint8_t seed[32];
+  for (int i = 0; i < 8; i++) {  // rand_core 0.6 SeedableRng::seed_from_u64 (PCG32)
+    state = state * 6364136223846793005ULL + 11634580027462260723ULL;
+    const uint32_t xorshifted = (uint32_t)(((state >> 18) ^ state) >> 27);
+    const uint32_t rot = (uint32_t)(state >> 59);
+    const uint32_t x = (xorshifted >> rot) | (xorshifted << ((32 - rot) & 31));
+    for (int k = 0; k < 4; k++) seed[4 * i + k] = (uint8_t)(x >> (8 * k));
+  }
+  return ChaCha20Rng(seed, rounds);
+}
+
+void ChaCha20Rng::refill() {
+  for (int blk = 0; blk < 4; blk++) {
+    const uint64_t ctr = counter_ + (uint64_t)blk;
+    uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key_[0], key_[1],
+                       key_[2], key_[3], key_[4], key_[5], key_[6], key_[7], (uint32_t)ctr,
+                       (uint32_t)(ctr >> 32), (uint32_t)stream_, (uint32_t)(stream_ >> 32)};
+    uint32_t x[16];
+    std::memcpy(x, in, sizeof(x));
+    for (int i = 0; i < rounds_; i += 2) {
+      qr(x[0], x[4], x[8], x[12]);
+      qr(x[1], x[5], x[9], x[13]);
+      qr(x[2], x[6], x[10], x[14]);
+      qr(x[3], x[7], x[11], x[15]);
+      qr(x[0], x[5], x[10], x[15]);
+      qr(x[1], x[6], x[11], x[12]);
+      qr(x[2], x[7], x[8], x[13]);
+      qr(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; i++) buf_[16 * blk + i] = x[i] + in[i];
+  }
+  counter_ += 4;
+}
+
+uint32_t ChaCha20Rng::next_u32() {
+  if (index_ >= 64) {
+    refill();
+    index_ = 0;
+  }
+  return buf_[index_++];
+}
+
+uint64_t ChaCha20Rng::next_u64() {  // rand_core BlockRng::next_u64
+  if (index_ < 63) {
+    const uint64_t v = (uint64_t)buf_[index_] | ((uint64_t)buf_[index_ + 1] << 32);
+    index_ += 2;
+    return v;
+  }
+  if (index_ >= 64) {
+    refill();
+    index_ = 2;
+    return (uint64_t)buf_[0] | ((uint64_t)buf_[1] << 32);
+  }
+  const uint64_t x = buf_[63];
+  refill();
+  index_ = 1;
+  return ((uint64_t)buf_[0] << 32) | x;
+}
+
+void ChaCha20Rng::set_stream(uint64_t stream) {  // rand_chacha set_stream: keep word position
+  if (index_ < 64) {
+    const uint64_t word = (counter_ - 4) * 16 + (uint64_t)index_;
+    stream_ = stream;
+    counter_ = word / 16;
+    index_ = 64;
+    if (word % 16) {
+      refill();
+      index_ = (int)(word % 16);
+    }
+  } else {
+    stream_ = stream;
+  }
+}
+
+uint64_t uniform_usize(ChaCha20Rng &rng, uint64_t low, uint64_t high) {
+  const uint64_t range = high - low;
+  if (range == 0) return rng.next_u64();
+  const uint64_t reject = (UINT64_MAX - range + 1) % range;
+  const uint64_t zone = UINT64_MAX - reject;
+  for (;;) {
+    const unsigned __int128 m = (unsigned __int128)rng.next_u64() * range;
+    if ((uint64_t)m <= zone) return low + (uint64_t)(m >> 64);
+  }
+}
+
+void field_random(ChaCha20Rng &rng, int limbs, int num_bits, const uint64_t *p, uint64_t *out,
+                  size_t n) {
+  const int shave = 64 * limbs - num_bits;
+  const uint64_t mask = shave >= 64 ? 0 : (UINT64_MAX >> shave);
+  for (size_t i = 0; i < n; i++) {
+    uint64_t *e = out + i * limbs;
+    for (;;) {
+      for (int k = 0; k < limbs; k++) e[k] = rng.next_u64();
+      e[limbs - 1] &= mask;
+      bool lt = false;
+      for (int k = limbs - 1; k >= 0; k--) {
+        if (e[k] != p[k]) {
+          lt = e[k] < p[k];
+          break;
+        }
+      }
+      if (lt) break;
+    }
+  }
+}
+
+}  // namespace lcpc

@@ -1,0 +1,465 @@
+"""Python mirror of the reference's lcpc-2d / lcpc-ligero-pc API over liblcpc_mi.so.
+
+Reference interface (TrevorGKann/lcpc_proof_of_storage):
+  LcEncoding trait              lcpc-2d/src/lib.rs:75-105
+  LigeroEncodingRho             lcpc-ligero-pc/src/lib.rs:32-186 (LigeroEncoding = rho 1/2)
+  LcCommit::{commit, prove, get_root, get_n_rows, get_n_cols, get_n_per_row}   :285-327
+  LcEvalProof::{verify, get_n_cols, get_n_per_row}                             :531-557
+  LcColumn {col, path}                                                         :424-433
+  ProverError / VerifierError                                                  :113-167
+  free functions open_column, merkle_tree, verify_column_path/value,
+  collapse_columns, n_degree_tests, log2                                       :642-1154
+
+Field elements are numpy uint64 arrays of shape (n, limbs) in ff_derive's Montgomery form
+(bit-identical to the reference's ``struct FtX([u64; N])``).  All compute runs on the GPU
+through the C ABI; nothing here does field arithmetic.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field as dc_field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _native as N
+
+FT63, FT127, FT191, FT255, FT253_192 = 0, 1, 2, 3, 4
+FIELD_NAMES = {FT63: "Ft63", FT127: "Ft127", FT191: "Ft191", FT255: "Ft255", FT253_192: "Ft253_192"}
+
+# status codes (include/lcpc_mi.h)
+PROVER = {1: "TooBig", 2: "Encode", 3: "Commit", 4: "ColumnNumber", 5: "OuterTensor"}
+VERIFIER = {10: "NumColOpens", 11: "ColumnPath", 12: "ColumnEval", 13: "ColumnDegree", 14: "OuterTensor",
+            15: "InnerTensor", 16: "EncodingDims", 17: "Encode"}
+FFT = {20: "NotPowerOfTwo", 21: "TooBig", 22: "WrongSizePrecomp"}
+
+
+class LcpcError(Exception):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"{self.kind} ({code}): {msg}")
+
+    @property
+    def kind(self) -> str:
+        return {**PROVER, **VERIFIER, **FFT}.get(self.code, "Error")
+
+
+class ProverError(LcpcError):
+    pass
+
+
+class VerifierError(LcpcError):
+    pass
+
+
+class FFTError(LcpcError):
+    pass
+
+
+class DeviceError(LcpcError):
+    pass
+
+
+def _raise(code: int, cls=None):
+    if code == 0:
+        return
+    msg = N.last_error()
+    if cls is None:
+        if code in PROVER:
+            cls = ProverError
+        elif code in VERIFIER:
+            cls = VerifierError
+        elif code in FFT:
+            cls = FFTError
+        else:
+            cls = DeviceError
+    raise cls(code, msg)
+
+
+def _p64(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(N.u64p)
+
+
+def _bytes_ptr(b: bytes):
+    buf = (C.c_uint8 * max(len(b), 1)).from_buffer_copy(bytes(b) if len(b) else b"\0")
+    return C.cast(buf, N.u8p), buf
+
+
+def limbs(field: int) -> int:
+    return N.load().lcpc_field_limbs(field)
+
+
+def num_bits(field: int) -> int:
+    return N.load().lcpc_field_num_bits(field)
+
+
+def _elems(a, field: int) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    return a.reshape(-1, limbs(field))
+
+
+def set_device(device: int):
+    _raise(N.load().lcpc_set_device(device), DeviceError)
+
+
+def device_count() -> int:
+    return N.load().lcpc_device_count()
+
+
+# ---------------------------------------------------------------- parameters
+def n_degree_tests(lam: int, length: int, flog2: int) -> int:
+    """lcpc-2d/src/lib.rs:642-645"""
+    return N.load().lcpc_n_degree_tests(lam, length, flog2)
+
+
+def log2(v: int) -> int:
+    """lcpc-2d/src/lib.rs:857-859"""
+    return N.load().lcpc_log2(v)
+
+
+# ---------------------------------------------------------------- transcript
+class Transcript:
+    """merlin::Transcript (merlin 2.0)."""
+
+    def __init__(self, label: bytes = b"", _h=None):
+        L = N.load()
+        if _h is None:
+            p, keep = _bytes_ptr(label)
+            _h = L.lcpc_transcript_new(p, len(label))
+        self._h = _h
+
+    def clone(self) -> "Transcript":
+        return Transcript(_h=N.load().lcpc_transcript_clone(self._h))
+
+    def append_message(self, label: bytes, message: bytes):
+        lp, k1 = _bytes_ptr(label)
+        mp, k2 = _bytes_ptr(message)
+        N.load().lcpc_transcript_append_message(self._h, lp, len(label), mp, len(message))
+
+    def challenge_bytes(self, label: bytes, n: int) -> bytes:
+        lp, k1 = _bytes_ptr(label)
+        out = (C.c_uint8 * max(n, 1))()
+        N.load().lcpc_transcript_challenge_bytes(self._h, lp, len(label), C.cast(out, N.u8p), n)
+        return bytes(out)[:n]
+
+    def __del__(self):
+        try:
+            N.load().lcpc_transcript_free(self._h)
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- encodings
+class LcEncoding:
+    """Handle to a GPU-resident encoding (LcEncoding trait, lcpc-2d/src/lib.rs:75-105)."""
+
+    LABEL_DT = b"$l//DT"  # def_labels! (lcpc-2d/src/macros.rs:29-36) never substitutes $l
+    LABEL_PR = b"$l//PR"
+    LABEL_PE = b"$l//PE"
+    LABEL_CO = b"$l//CO"
+
+    def __init__(self, handle):
+        self._h = handle
+        L = N.load()
+        self.field = L.lcpc_encoding_field(handle)
+
+    def __del__(self):
+        try:
+            N.load().lcpc_encoding_free(self._h)
+        except Exception:
+            pass
+
+    @property
+    def n_per_row(self) -> int:
+        return N.load().lcpc_encoding_n_per_row(self._h)
+
+    @property
+    def n_cols(self) -> int:
+        return N.load().lcpc_encoding_n_cols(self._h)
+
+    def get_dims(self, length: int):
+        a, b, c = C.c_size_t(), C.c_size_t(), C.c_size_t()
+        N.load().lcpc_encoding_get_dims(self._h, length, C.byref(a), C.byref(b), C.byref(c))
+        return a.value, b.value, c.value
+
+    def dims_ok(self, n_per_row: int, n_cols: int) -> bool:
+        return bool(N.load().lcpc_encoding_dims_ok(self._h, n_per_row, n_cols))
+
+    def get_n_col_opens(self) -> int:
+        return N.load().lcpc_encoding_n_col_opens(self._h)
+
+    def get_n_degree_tests(self) -> int:
+        return N.load().lcpc_encoding_n_degree_tests(self._h)
+
+    def encode(self, inp: np.ndarray) -> np.ndarray:
+        """LcEncoding::encode: in place on one row of n_cols elements (uint64, C-contiguous)."""
+        a = np.asarray(inp)
+        if a.dtype != np.uint64 or not a.flags["C_CONTIGUOUS"]:
+            raise TypeError("encode needs a C-contiguous uint64 array (modified in place)")
+        _raise(N.load().lcpc_encode(self._h, _p64(a.reshape(-1)), a.size // limbs(self.field)))
+        return a
+
+    def encode_rows(self, rows: np.ndarray) -> np.ndarray:
+        """Batched in-place encode of a (n_rows, n_cols, limbs) array."""
+        a = np.ascontiguousarray(rows, dtype=np.uint64)
+        nl = limbs(self.field)
+        a = a.reshape(-1, self.n_cols * nl)
+        _raise(N.load().lcpc_encode_rows(self._h, _p64(a), a.shape[0], self.n_cols))
+        return a.reshape(-1, self.n_cols, nl)
+
+    def encode_rows_device(self, src_ptr: int, src_stride: int, n_valid: int, dst_ptr: int,
+                           dst_stride: int, n_rows: int, stream: int = 0):
+        _raise(N.load().lcpc_encode_rows_device(self._h, src_ptr, src_stride, n_valid, dst_ptr,
+                                                 dst_stride, n_rows, stream or None))
+
+
+class LigeroEncoding(LcEncoding):
+    """LigeroEncodingRho<F, Rn, Rd> (lcpc-ligero-pc/src/lib.rs:32-186); default rate 1/2."""
+
+    LAMBDA = 128
+
+    @staticmethod
+    def _new(fn, *args) -> "LigeroEncoding":
+        h = C.c_void_p()
+        _raise(fn(*args, C.byref(h)))
+        return LigeroEncoding(h.value)
+
+    @classmethod
+    def new(cls, field: int, length: int, rho=(1, 2)) -> "LigeroEncoding":
+        return cls._new(N.load().lcpc_ligero_new, field, rho[0], rho[1], length)
+
+    @classmethod
+    def new_ml(cls, field: int, n_vars: int, rho=(1, 2)) -> "LigeroEncoding":
+        return cls._new(N.load().lcpc_ligero_new_ml, field, rho[0], rho[1], n_vars)
+
+    @classmethod
+    def new_from_dims(cls, field: int, n_per_row: int, n_cols: int, rho=(1, 2)) -> "LigeroEncoding":
+        return cls._new(N.load().lcpc_ligero_new_from_dims, field, rho[0], rho[1], n_per_row, n_cols)
+
+    @staticmethod
+    def n_col_opens(rho=(1, 2)) -> int:
+        return N.load().lcpc_ligero_n_col_opens(*rho)
+
+    @staticmethod
+    def get_dims_for(field: int, length: int, rho=(1, 2)):
+        """LigeroEncodingRho::_get_dims (lib.rs:70-112)."""
+        a, b, c = C.c_size_t(), C.c_size_t(), C.c_size_t()
+        _raise(N.load().lcpc_ligero_get_dims(field, rho[0], rho[1], length, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
+
+class RsEncoding(LcEncoding):
+    """fft_io encoding with explicit soundness counts (lcpc-2d/src/tests.rs:23-121)."""
+
+    @classmethod
+    def new(cls, field: int, n_per_row: int, n_cols: int, n_col_opens: int, n_degree_tests: int):
+        h = C.c_void_p()
+        _raise(N.load().lcpc_rs_encoding_new(field, n_per_row, n_cols, n_col_opens, n_degree_tests, C.byref(h)))
+        return cls(h.value)
+
+
+# ---------------------------------------------------------------- commitment / proof
+@dataclass
+class LcColumn:
+    col: np.ndarray          # (n_rows, limbs)
+    path: List[bytes]        # log2(n_cols) digests
+
+
+class LcCommit:
+    """LcCommit<Blake3, E> resident in HBM (lcpc-2d/src/lib.rs:174-191, 285-327)."""
+
+    def __init__(self, handle, field: int):
+        self._h = handle
+        self.field = field
+
+    def __del__(self):
+        try:
+            N.load().lcpc_commit_free(self._h)
+        except Exception:
+            pass
+
+    @classmethod
+    def commit(cls, coeffs: np.ndarray, enc: LcEncoding) -> "LcCommit":
+        a = _elems(coeffs, enc.field)
+        h = C.c_void_p()
+        _raise(N.load().lcpc_commit_new(enc._h, _p64(a), a.shape[0], C.byref(h)))
+        return cls(h.value, enc.field)
+
+    @classmethod
+    def commit_device(cls, d_coeffs: int, length: int, enc: LcEncoding) -> "LcCommit":
+        h = C.c_void_p()
+        _raise(N.load().lcpc_commit_new_device(enc._h, d_coeffs, length, C.byref(h)))
+        return cls(h.value, enc.field)
+
+    def get_root(self) -> bytes:
+        out = (C.c_uint8 * 32)()
+        _raise(N.load().lcpc_commit_get_root(self._h, C.cast(out, N.u8p)))
+        return bytes(out)
+
+    def get_n_rows(self) -> int:
+        return N.load().lcpc_commit_n_rows(self._h)
+
+    def get_n_cols(self) -> int:
+        return N.load().lcpc_commit_n_cols(self._h)
+
+    def get_n_per_row(self) -> int:
+        return N.load().lcpc_commit_n_per_row(self._h)
+
+    @property
+    def comm(self) -> np.ndarray:
+        out = np.zeros((self.get_n_rows() * self.get_n_cols(), limbs(self.field)), np.uint64)
+        _raise(N.load().lcpc_commit_copy_comm(self._h, _p64(out)))
+        return out
+
+    @property
+    def coeffs(self) -> np.ndarray:
+        out = np.zeros((self.get_n_rows() * self.get_n_per_row(), limbs(self.field)), np.uint64)
+        _raise(N.load().lcpc_commit_copy_coeffs(self._h, _p64(out)))
+        return out
+
+    @property
+    def hashes(self) -> bytes:
+        n = N.load().lcpc_commit_n_hashes(self._h)
+        out = (C.c_uint8 * (32 * n))()
+        _raise(N.load().lcpc_commit_copy_hashes(self._h, C.cast(out, N.u8p)))
+        return bytes(out)
+
+    def device_comm_ptr(self) -> int:
+        return N.load().lcpc_commit_device_comm(self._h)
+
+    def check(self, enc: LcEncoding):
+        _raise(N.load().lcpc_check_comm(self._h, enc._h))
+
+    def open_column(self, column: int) -> LcColumn:
+        nr, nl = self.get_n_rows(), limbs(self.field)
+        pl = log2(self.get_n_cols())
+        col = np.zeros((nr, nl), np.uint64)
+        path = (C.c_uint8 * max(32 * pl, 1))()
+        _raise(N.load().lcpc_open_column(self._h, column, _p64(col), C.cast(path, N.u8p)))
+        pb = bytes(path)
+        return LcColumn(col, [pb[32 * i:32 * i + 32] for i in range(pl)])
+
+    def prove(self, outer_tensor: np.ndarray, enc: LcEncoding, tr: Transcript) -> "LcEvalProof":
+        o = _elems(outer_tensor, self.field)
+        h = C.c_void_p()
+        _raise(N.load().lcpc_prove(self._h, _p64(o), o.shape[0], enc._h, tr._h, C.byref(h)))
+        return LcEvalProof(h.value)
+
+
+class LcEvalProof:
+    """LcEvalProof<Blake3, E> (lcpc-2d/src/lib.rs:516-557)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        L = N.load()
+        self.field = L.lcpc_proof_field(handle)
+        self.n_cols = L.lcpc_proof_n_cols(handle)
+        self.n_per_row = L.lcpc_proof_n_per_row(handle)
+        self.n_rows = L.lcpc_proof_n_rows(handle)
+        self.n_degree_tests = L.lcpc_proof_n_degree_tests(handle)
+        self.n_col_opens = L.lcpc_proof_n_col_opens(handle)
+        self.path_len = L.lcpc_proof_path_len(handle)
+
+    def __del__(self):
+        try:
+            N.load().lcpc_proof_free(self._h)
+        except Exception:
+            pass
+
+    def get_n_cols(self) -> int:
+        return self.n_cols
+
+    def get_n_per_row(self) -> int:
+        return self.n_per_row
+
+    @property
+    def p_eval(self) -> np.ndarray:
+        out = np.zeros((self.n_per_row, limbs(self.field)), np.uint64)
+        _raise(N.load().lcpc_proof_copy_p_eval(self._h, _p64(out)))
+        return out
+
+    @property
+    def p_random_vec(self) -> List[np.ndarray]:
+        res = []
+        for i in range(self.n_degree_tests):
+            out = np.zeros((self.n_per_row, limbs(self.field)), np.uint64)
+            _raise(N.load().lcpc_proof_copy_p_random(self._h, i, _p64(out)))
+            res.append(out)
+        return res
+
+    @property
+    def columns(self) -> List[LcColumn]:
+        res = []
+        nl = limbs(self.field)
+        for k in range(self.n_col_opens):
+            col = np.zeros((self.n_rows, nl), np.uint64)
+            path = (C.c_uint8 * max(32 * self.path_len, 1))()
+            _raise(N.load().lcpc_proof_copy_column(self._h, k, _p64(col), C.cast(path, N.u8p)))
+            pb = bytes(path)
+            res.append(LcColumn(col, [pb[32 * i:32 * i + 32] for i in range(self.path_len)]))
+        return res
+
+    @classmethod
+    def from_parts(cls, field: int, n_cols: int, p_eval, p_random_vec, columns: List[LcColumn]):
+        nl = limbs(field)
+        pe = _elems(p_eval, field)
+        pr = np.ascontiguousarray(np.concatenate([_elems(x, field) for x in p_random_vec]) if p_random_vec
+                                  else np.zeros((1, nl), np.uint64))
+        n_rows = columns[0].col.shape[0] if columns else 0
+        path_len = len(columns[0].path) if columns else 0
+        cols = np.ascontiguousarray(np.concatenate([_elems(c.col, field) for c in columns]) if columns
+                                    else np.zeros((1, nl), np.uint64))
+        paths = b"".join(b"".join(c.path) for c in columns)
+        pp, keep = _bytes_ptr(paths)
+        h = C.c_void_p()
+        _raise(N.load().lcpc_proof_from_parts(field, n_cols, pe.shape[0], n_rows, len(p_random_vec), len(columns),
+                                              path_len, _p64(pe), _p64(pr), _p64(cols), pp, C.byref(h)))
+        return cls(h.value)
+
+    def verify(self, root: bytes, outer_tensor, inner_tensor, enc: LcEncoding, tr: Transcript) -> np.ndarray:
+        o = _elems(outer_tensor, self.field)
+        i = _elems(inner_tensor, self.field)
+        rp, keep = _bytes_ptr(root)
+        out = np.zeros(limbs(self.field), np.uint64)
+        _raise(N.load().lcpc_verify(rp, _p64(o), o.shape[0], _p64(i), i.shape[0], self._h, enc._h, tr._h, _p64(out)))
+        return out
+
+
+# ---------------------------------------------------------------- free functions
+def collapse_columns(field: int, coeffs, tensor, n_rows: int, n_per_row: int) -> np.ndarray:
+    c = _elems(coeffs, field)
+    t = _elems(tensor, field)
+    out = np.zeros((n_per_row, limbs(field)), np.uint64)
+    _raise(N.load().lcpc_collapse_columns(field, _p64(c), _p64(t), _p64(out), n_rows, n_per_row))
+    return out
+
+
+def merkle_tree(ins: bytes) -> bytes:
+    n = len(ins) // 32
+    ip, keep = _bytes_ptr(ins)
+    out = (C.c_uint8 * max(32 * (n - 1), 1))()
+    _raise(N.load().lcpc_merkle_tree(ip, n, C.cast(out, N.u8p)))
+    return bytes(out)[:32 * (n - 1)]
+
+
+def hash_columns(field: int, comm, n_rows: int, n_cols: int) -> bytes:
+    c = _elems(comm, field)
+    out = (C.c_uint8 * (32 * n_cols))()
+    _raise(N.load().lcpc_hash_columns(field, _p64(c), n_rows, n_cols, C.cast(out, N.u8p)))
+    return bytes(out)
+
+
+def verify_column_path(field: int, column: LcColumn, col_num: int, root: bytes) -> bool:
+    c = _elems(column.col, field)
+    pb = b"".join(column.path)
+    pp, k1 = _bytes_ptr(pb)
+    rp, k2 = _bytes_ptr(root)
+    return bool(N.load().lcpc_verify_column_path(field, _p64(c), c.shape[0], pp, len(column.path), col_num, rp))
+
+
+def verify_column_value(field: int, column: LcColumn, tensor, poly_eval) -> bool:
+    c = _elems(column.col, field)
+    t = _elems(tensor, field)
+    e = _elems(poly_eval, field)
+    return bool(N.load().lcpc_verify_column_value(field, _p64(c), _p64(t), c.shape[0], _p64(e)))

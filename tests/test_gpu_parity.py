@@ -1,0 +1,220 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit for bit.
+
+Every test here runs the product library liblcpc_mi.so on the MI355X and compares with
+oracle/ (the CPU restatement of the reference path).  Sizes are ones the oracle finishes in
+seconds; full-size (2^24) behaviour is covered by size-independent properties in
+test_gpu_properties.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [0, 1, 3, 4]  # Ft63, Ft127, Ft255, Ft253_192 (Ft191 has no GPU kernels)
+
+
+def rand_elems(oracle, fid, n, seed):
+    return oracle.ChaCha(seed_u64=seed).field_random(fid, n)
+
+
+@pytest.mark.parametrize("fid", FIELDS)
+@pytest.mark.parametrize("log_n", [1, 2, 3, 5, 8, 11, 12, 13, 14, 15, 16])
+def test_encode_matches_fffft(gpu, oracle, fid, log_n):
+    """LcEncoding::encode (fft_io) on one row, zero-padded half (rho = 1/2)."""
+    n = 1 << log_n
+    np_ = n // 2
+    nl = oracle.limbs(fid)
+    enc = gpu.RsEncoding.new(fid, np_, n, 4, 1)
+    row = np.zeros(n * nl, np.uint64)
+    row[:np_ * nl] = rand_elems(oracle, fid, np_, 100 + log_n)
+    want = oracle.fft_io(fid, row)
+    got = row.copy()
+    enc.encode(got)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("fid", [0, 1])
+@pytest.mark.parametrize("log_n", [13, 14, 16])
+def test_encode_full_rows(gpu, oracle, fid, log_n):
+    """Full-length (no zero padding) batched rows."""
+    n = 1 << log_n
+    nl = oracle.limbs(fid)
+    enc = gpu.RsEncoding.new(fid, 1, n, 4, 1)
+    rows = rand_elems(oracle, fid, 3 * n, 7 + log_n).reshape(3, n * nl)
+    got = enc.encode_rows(rows.copy()).reshape(3, n * nl)
+    for r in range(3):
+        assert np.array_equal(got[r], oracle.fft_io(fid, rows[r]))
+
+
+def test_encode_errors(gpu):
+    enc = gpu.RsEncoding.new(1, 8, 16, 4, 1)
+    bad = np.zeros(12 * 2, np.uint64)
+    with pytest.raises(gpu.FFTError) as e:
+        enc.encode(bad)
+    assert e.value.kind == "NotPowerOfTwo"
+    with pytest.raises(gpu.FFTError) as e:
+        enc.encode(np.zeros(32 * 2, np.uint64))
+    assert e.value.kind == "WrongSizePrecomp"
+
+
+def _commit_both(gpu, oracle, fid, n_per_row, n_cols, length, seed, nco=16, ndt=2):
+    coeffs = rand_elems(oracle, fid, length, seed)
+    g_enc = gpu.RsEncoding.new(fid, n_per_row, n_cols, nco, ndt)
+    o_enc = oracle.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
+    g = gpu.LcCommit.commit(coeffs, g_enc)
+    o = oracle.Commit(o_enc, coeffs)
+    return coeffs, g_enc, o_enc, g, o
+
+
+@pytest.mark.parametrize("fid,n_per_row,n_cols,length", [
+    (1, 2048, 4096, 1 << 16),      # cfg1 shape
+    (0, 100, 256, 3000),           # ragged: last row partial
+    (1, 1, 2, 5),                  # smallest R-S code
+    (0, 700, 1024, 700),           # one row
+    (3, 512, 1024, 4096),
+    (4, 300, 512, 2000),           # big-endian repr field
+    (1, 8192, 16384, 128 * 8192),  # cfg2 shape: 128 x 8192 -> 16384
+])
+def test_commit_matches_oracle(gpu, oracle, fid, n_per_row, n_cols, length):
+    coeffs, g_enc, o_enc, g, o = _commit_both(gpu, oracle, fid, n_per_row, n_cols, length, 11)
+    assert g.get_n_rows() == o.n_rows and g.get_n_cols() == o.n_cols
+    assert np.array_equal(g.comm.reshape(-1), o.comm)
+    assert np.array_equal(g.coeffs.reshape(-1), o.coeffs)
+    assert g.hashes == o.hashes
+    assert g.get_root() == o.root()
+
+
+@pytest.mark.parametrize("fid,n_per_row,n_cols,length,nco,ndt", [
+    (1, 2048, 4096, 1 << 16, 309, 2),
+    (0, 100, 256, 3000, 128, 3),
+    (3, 256, 512, 1000, 40, 1),
+    (4, 64, 128, 1000, 20, 2),
+])
+def test_prove_verify_matches_oracle(gpu, oracle, fid, n_per_row, n_cols, length, nco, ndt):
+    coeffs, g_enc, o_enc, g, o = _commit_both(gpu, oracle, fid, n_per_row, n_cols, length, 5, nco, ndt)
+    root = g.get_root()
+    x = rand_elems(oracle, fid, 1, 77)
+    inner, outer = oracle.eval_tensors(fid, x, n_per_row, g.get_n_rows())
+    g_tr = gpu.Transcript(b"test transcript")
+    g_tr.append_message(b"polycommit", root)
+    g_tr.append_message(b"ncols", nco.to_bytes(8, "big"))
+    o_tr = oracle.standard_transcript(nco, root)
+    gp = g.prove(outer, g_enc, g_tr)
+    op = o.prove(o_enc, outer, o_tr)
+    assert np.array_equal(gp.p_eval.reshape(-1), op.p_eval)
+    pr = np.concatenate([v.reshape(-1) for v in gp.p_random_vec]) if ndt else np.zeros(0, np.uint64)
+    assert np.array_equal(pr, op.p_random)
+    cols = gp.columns
+    nl = oracle.limbs(fid)
+    o_cols = op.cols.reshape(nco, -1)
+    o_paths = op.paths.tobytes()
+    for k, c in enumerate(cols):
+        assert np.array_equal(c.col.reshape(-1), o_cols[k])
+        assert b"".join(c.path) == o_paths[k * 32 * op.path_len:(k + 1) * 32 * op.path_len]
+    # transcripts stay in lock step after the proof
+    assert g_tr.challenge_bytes(b"after", 32) == o_tr.challenge_bytes(b"after", 32)
+    # verify on the GPU and on the oracle; the evaluation equals p(x)
+    v_tr = gpu.Transcript(b"test transcript")
+    v_tr.append_message(b"polycommit", root)
+    v_tr.append_message(b"ncols", nco.to_bytes(8, "big"))
+    ev = gp.verify(root, outer, inner, g_enc, v_tr)
+    rc, o_ev = op.verify(root, outer, inner, o_enc, oracle.standard_transcript(nco, root))
+    assert rc == 0
+    assert np.array_equal(ev.reshape(-1), o_ev)
+    want = oracle.from_mont(fid, np.zeros(nl, np.uint64))[0]
+    acc = 0
+    p = oracle.modulus(fid)
+    xs = oracle.from_mont(fid, x)[0]
+    cs = oracle.from_mont(fid, coeffs)
+    for c in reversed(cs):
+        acc = (acc * xs + c) % p
+    assert oracle.from_mont(fid, ev.reshape(-1))[0] == acc
+
+
+def test_verify_rejects_tampering(gpu, oracle):
+    fid, n_per_row, n_cols, nco = 1, 512, 1024, 64
+    coeffs, g_enc, o_enc, g, o = _commit_both(gpu, oracle, fid, n_per_row, n_cols, 40 * 512, 9, nco, 2)
+    root = g.get_root()
+    x = rand_elems(oracle, fid, 1, 3)
+    inner, outer = oracle.eval_tensors(fid, x, n_per_row, g.get_n_rows())
+
+    def tr():
+        t = gpu.Transcript(b"test transcript")
+        t.append_message(b"polycommit", root)
+        return t
+
+    pf = g.prove(outer, g_enc, tr())
+    pf.verify(root, outer, inner, g_enc, tr())
+    cols = pf.columns
+
+    def rebuilt(p_eval=None, p_random=None, columns=None):
+        return gpu.LcEvalProof.from_parts(fid, n_cols, pf.p_eval if p_eval is None else p_eval,
+                                          pf.p_random_vec if p_random is None else p_random,
+                                          cols if columns is None else columns)
+
+    # untouched rebuild verifies
+    rebuilt().verify(root, outer, inner, g_enc, tr())
+    # flip one opened value -> degree test fails first (ColumnDegree precedes ColumnEval/Path)
+    bad_cols = [gpu.LcColumn(c.col.copy(), list(c.path)) for c in cols]
+    bad_cols[3].col[5, 0] ^= 1
+    with pytest.raises(gpu.VerifierError) as e:
+        rebuilt(columns=bad_cols).verify(root, outer, inner, g_enc, tr())
+    assert e.value.kind in ("ColumnDegree", "ColumnEval", "ColumnPath")
+    # corrupt one Merkle path digest -> ColumnPath
+    bad_cols = [gpu.LcColumn(c.col.copy(), list(c.path)) for c in cols]
+    p0 = bytearray(bad_cols[0].path[2]); p0[0] ^= 0xff
+    bad_cols[0].path[2] = bytes(p0)
+    with pytest.raises(gpu.VerifierError) as e:
+        rebuilt(columns=bad_cols).verify(root, outer, inner, g_enc, tr())
+    assert e.value.kind == "ColumnPath"
+    # wrong root -> ColumnPath
+    with pytest.raises(gpu.VerifierError) as e:
+        pf.verify(bytes(32), outer, inner, g_enc, tr())
+    # wrong tensor sizes
+    with pytest.raises(gpu.VerifierError) as e:
+        pf.verify(root, outer[:-2], inner, g_enc, tr())
+    assert e.value.kind == "OuterTensor"
+    with pytest.raises(gpu.VerifierError) as e:
+        pf.verify(root, outer, inner[:-2], g_enc, tr())
+    assert e.value.kind == "InnerTensor"
+    with pytest.raises(gpu.ProverError) as e:
+        g.prove(outer[:-2], g_enc, tr())
+    assert e.value.kind == "OuterTensor"
+
+
+def test_open_column_and_free_functions(gpu, oracle):
+    fid = 0
+    coeffs, g_enc, o_enc, g, o = _commit_both(gpu, oracle, fid, 200, 512, 5000, 21)
+    root = g.get_root()
+    nl = oracle.limbs(fid)
+    for col in [0, 1, 255, 511, 300]:
+        c = g.open_column(col)
+        assert gpu.verify_column_path(fid, c, col, root)
+        assert not gpu.verify_column_path(fid, c, col ^ 1, root)
+        ocol = np.zeros(o.n_rows * nl, np.uint64)
+        opath = np.zeros(32 * 9, np.uint8)
+        oracle.lib().of_open_column(o.ptr, col, oracle.p64(ocol), opath.ctypes.data_as(oracle.u8p))
+        assert np.array_equal(c.col.reshape(-1), ocol)
+        assert b"".join(c.path) == opath.tobytes()
+    with pytest.raises(gpu.ProverError) as e:
+        g.open_column(512)
+    assert e.value.kind == "ColumnNumber"
+    # collapse_columns / verify_column_value against the oracle
+    t = rand_elems(oracle, fid, g.get_n_rows(), 4)
+    got = gpu.collapse_columns(fid, g.coeffs, t, g.get_n_rows(), 200)
+    want = np.zeros(200 * nl, np.uint64)
+    oracle.lib().of_collapse_columns(fid, oracle.p64(o.coeffs), oracle.p64(t), oracle.p64(want),
+                                     o.n_rows, 200)
+    assert np.array_equal(got.reshape(-1), want)
+    # merkle_tree / hash_columns
+    leaves = o.hashes[:32 * 512]
+    assert gpu.merkle_tree(leaves) == o.hashes[32 * 512:]
+    assert gpu.hash_columns(fid, g.comm, o.n_rows, 512) == leaves
+    comm = g.comm.reshape(o.n_rows, 512, nl)
+    col7 = gpu.LcColumn(np.ascontiguousarray(comm[:, 7, :]), [])
+    # linearity: sum_r t[r] * comm[r][j] == encode(collapse(coeffs, t))[j]
+    row = np.zeros((512, nl), np.uint64)
+    row[:200] = got
+    g_enc.encode(row)
+    assert gpu.verify_column_value(fid, col7, t, row[7])
+    assert not gpu.verify_column_value(fid, col7, t, row[8])
