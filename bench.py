@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""bench.py -- committed field-elements/s (commit + open) of a 2^24-coefficient Ligero
+commitment over Ft127 on MI355X (BASELINE.json metric, config 3 at N = 1).
+
+One step = LcCommit::commit of 2^24 Ft127 coefficients already resident in HBM (encode every
+row with the R-S NTT, hash every column with BLAKE3, build the Merkle tree) followed by
+LcCommit::prove (2 degree tests + evaluation row combination, Merlin transcript over every
+row-combination coefficient, 309 column openings with Merkle paths): lcpc-2d/src/lib.rs:651-700
+and :1034-1123, dims 512 x 32768 -> 65536 (rho = 1/2, lcpc-ligero-pc/src/lib.rs:70-112).
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
+committing and opening its own 2^24-coefficient polynomial (independent commitments, e.g. the
+proof-of-storage server's files): no data-path collective, "scaling": "weak".  The barrier and
+the max-over-ranks reduction of the timed region use torch.distributed.
+
+Printed JSON line: the metric, a "roofline" object for the dominant kernel (HIP-event timed live
+on the library's stream) and a "cpu_baseline" object (the C restatement under oracle/, run on
+the host cores of rank 0 at N = 1, which doubles as the bit-exactness check of the root).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+SEED = 0x1CDC2024       # coefficients = F::random(ChaCha20Rng::seed_from_u64(SEED))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-len", type=int, default=24)
+    ap.add_argument("--field", default="Ft127")
+    ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the cores available (max 16)")
+    ap.add_argument("--no-prof", action="store_true", help="disable HIP-event kernel timing")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+
+    import lcpc_proof_of_storage_amd as L
+    from lcpc_proof_of_storage_amd import _native
+
+    L.set_device(local_rank)
+    fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
+    nl = L.limbs(fid)
+    n = 1 << args.log_len
+    enc = L.LigeroEncoding.new(fid, n)
+    n_rows, n_per_row, n_cols = enc.get_dims(n)
+    nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
+
+    # synthetic inputs (host RNG of the product library), then resident in HBM
+    coeffs = L.field_random(fid, n, SEED + rank)
+    outer = L.field_random(fid, n_rows, 7)  # prove accepts any outer tensor of n_rows elements
+    d_coeffs = torch.from_numpy(coeffs.view(np.int64)).to(f"cuda:{local_rank}")
+    torch.cuda.synchronize()
+
+    def step():
+        c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+        root = c.get_root()
+        tr = L.Transcript(b"test transcript")
+        tr.append_message(b"polycommit", root)
+        tr.append_message(b"ncols", nco.to_bytes(8, "big"))
+        pf = c.prove(outer, enc, tr)
+        return c, pf, root
+
+    for _ in range(args.warmup):
+        step()
+    prof = not args.no_prof
+    L.prof_enable(prof)
+    L.prof_reset()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    root = None
+    for _ in range(args.steps):
+        c, pf, root = step()
+        del c, pf
+    barrier()
+    elapsed = time.perf_counter() - t0
+    L.prof_enable(False)
+    stats = L.prof_stats() if prof else {}
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_elems = n * args.steps * world
+    value = total_elems / elapsed
+    B = 8 * nl
+    out = {
+        "metric": "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU",
+        "value": value,
+        "unit": "field-elements/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": f"u64x{nl} ({args.field} Montgomery limbs)",
+        "data": f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), resident in HBM",
+        "config": {
+            "workload": f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho=1/2, "
+                        f"{n_rows}x{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, BLAKE3 Merkle",
+            "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
+            "n_col_opens": nco, "n_degree_tests": ndt,
+            "parallelism": f"replicas x{world} (one independent commitment per GPU)",
+        },
+        "mb_per_s": value * B / 1e6,
+    }
+
+    # ---- roofline of the dominant kernel (encode = pass A + pass B, HIP events on the lib stream)
+    if stats:
+        kern = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]} for k, v in stats.items()}
+        out["kernels"] = kern
+        enc_ms = sum(kern[k]["avg_ms"] for k in ("ntt_pass_a", "ntt_pass_b") if k in kern)
+        algo = n_rows * n_per_row * B + n_rows * n_cols * B  # encode bytes per commit
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tpath):
+            try:
+                tj = json.load(open(tpath))
+                if tj.get("config_len") == n and tj.get("field") == args.field:
+                    traffic = tj.get("ntt_encode_bytes_per_launch")
+            except Exception:
+                traffic = None
+        achieved = algo / (enc_ms * 1e-3) / 1e9 if enc_ms else None
+        out["roofline"] = {
+            "kernel": "ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit)",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None,
+            "traffic": traffic,
+            "algorithmic_bytes": algo,
+            "avg_ms": enc_ms,
+        }
+
+    # ---- CPU baseline: the oracle (C restatement) on the same workload, rank 0 at N = 1
+    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    if rank == 0 and want_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ffi as O  # checker / CPU baseline only
+
+        cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        O.lib().of_set_threads(cores)
+        o_enc = O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
+        t1 = time.perf_counter()
+        oc = O.Commit(o_enc, coeffs.reshape(-1))
+        otr = O.standard_transcript(nco, oc.root())
+        op = oc.prove(o_enc, outer.reshape(-1), otr)
+        cpu_s = time.perf_counter() - t1
+        out["cpu_baseline"] = {
+            "value": n / cpu_s,
+            "unit": "field-elements/s",
+            "cores": cores,
+            "kind": "port",
+            "sample": f"one full commit+open of the same 2^{args.log_len} {args.field} workload "
+                      f"({cpu_s:.2f} s on {cores} threads)",
+        }
+        out["parity_root_vs_oracle"] = oc.root() == root if root is not None else None
+        del op, oc
+
+    if rank == 0:
+        print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -82,6 +82,10 @@ int lcpc_device_count(void);
 int lcpc_field_limbs(lcpc_field f);
 /* NUM_BITS of the field (SizedField::CLOG2, lcpc-2d/src/lib.rs:69-72) */
 int lcpc_field_num_bits(lcpc_field f);
+/* n draws of Field::random(&mut ChaCha20Rng::seed_from_u64(seed)) (ff_derive / rand_chacha):
+ * the synthetic-input generator of the tests and benches (lcpc-test-fields random_coeffs,
+ * lcpc-test-fields/src/lib.rs:86-108, with a seeded instead of a thread RNG). Host only. */
+lcpc_status lcpc_field_random(lcpc_field f, uint64_t seed, uint64_t *out, size_t n);
 
 /* ------------------------------------------------------------------ parameters
  * n_degree_tests (lcpc-2d/src/lib.rs:642-645), log2 (:857-859) */
@@ -210,6 +214,15 @@ int lcpc_verify_column_value(lcpc_field f, const uint64_t *col, const uint64_t *
 /* leaf digests of every column of a host matrix (hash_columns, :736-775) */
 lcpc_status lcpc_hash_columns(lcpc_field f, const uint64_t *comm, size_t n_rows, size_t n_cols,
                               uint8_t *out);
+
+/* ------------------------------------------------------------------ kernel timing
+ * HIP-event timing of every kernel launch on the handle streams (off by default). */
+void lcpc_prof_enable(int enable);
+void lcpc_prof_reset(void);
+/* accumulated milliseconds and launch count for a kernel name (0 if never launched) */
+int lcpc_prof_get(const char *name, double *total_ms, uint64_t *count);
+/* newline-separated kernel names seen so far; returns the full length */
+size_t lcpc_prof_names(char *buf, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -9,5 +9,6 @@ from .lcpc2d import (  # noqa: F401
     LcpcError, ProverError, VerifierError, FFTError, DeviceError,
     Transcript, LcEncoding, LigeroEncoding, RsEncoding, LcCommit, LcEvalProof, LcColumn,
     collapse_columns, merkle_tree, hash_columns, verify_column_path, verify_column_value,
-    n_degree_tests, log2, limbs, num_bits, set_device, device_count,
+    n_degree_tests, log2, limbs, num_bits, set_device, device_count, field_random,
+    prof_enable, prof_reset, prof_stats,
 )

@@ -33,6 +33,7 @@ SIGNATURES = {
     "lcpc_device_count": (i32, []),
     "lcpc_field_limbs": (i32, [i32]),
     "lcpc_field_num_bits": (i32, [i32]),
+    "lcpc_field_random": (i32, [i32, C.c_uint64, u64p, sz]),
     "lcpc_n_degree_tests": (sz, [sz, sz, sz]),
     "lcpc_log2": (sz, [sz]),
     "lcpc_ligero_n_col_opens": (sz, [sz, sz]),
@@ -91,6 +92,10 @@ SIGNATURES = {
     "lcpc_verify_column_path": (i32, [i32, u64p, sz, u8p, sz, sz, u8p]),
     "lcpc_verify_column_value": (i32, [i32, u64p, u64p, sz, u64p]),
     "lcpc_hash_columns": (i32, [i32, u64p, sz, sz, u8p]),
+    "lcpc_prof_enable": (None, [i32]),
+    "lcpc_prof_reset": (None, []),
+    "lcpc_prof_get": (i32, [C.c_char_p, C.POINTER(C.c_double), u64p]),
+    "lcpc_prof_names": (sz, [C.c_char_p, sz]),
 }
 
 

@@ -16,6 +16,7 @@
 // left-balanced tree (pairwise per level, odd node carried up, ROOT on the last parent).
 #include "field.hpp"
 #include "kernels.hpp"
+#include "prof.hpp"
 
 namespace lcpc {
 
@@ -297,6 +298,7 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
   dim3 grid((unsigned)((n_cols + 63) / 64), (unsigned)((n_chunks + 3) / 4));
   hipError_t e = dispatch_field(fid, [&]<class F>() {
     if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
+      prof::Scope ps("leaf_chunks", s);
       hipLaunchKernelGGL((k_leaf_chunks<F>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
                          col_stride, (uint32_t *)scratch, leaves, n_chunks);
       return hipGetLastError();
@@ -305,6 +307,7 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
     }
   });
   if (e != hipSuccess || n_chunks == 1) return e;
+  prof::Scope ps("leaf_merge", s);
   hipLaunchKernelGGL(k_leaf_merge, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, s,
                      (uint32_t *)scratch, n_cols, n_chunks, leaves);
   return hipGetLastError();
@@ -328,6 +331,7 @@ hipError_t merkle_tree(uint8_t *hashes, size_t np2, hipStream_t s) {
     int levels = 0;
     while (levels < 9 && ((size_t)1 << (levels + 1)) <= n) levels++;
     const size_t blocks = n >> levels;
+    prof::Scope ps("merkle", s);
     hipLaunchKernelGGL(k_merkle, dim3((unsigned)blocks), dim3(256), 0, s, hashes, np2, lvl, levels);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -348,6 +352,7 @@ hipError_t gather_columns(int fid, const uint32_t *m, size_t n_rows, size_t n_co
   const size_t n = n_idx * n_rows;
   if (!n) return hipSuccess;
   return dispatch_field(fid, [&]<class F>() {
+    prof::Scope ps("gather_cols", s);
     hipLaunchKernelGGL((k_gather_cols<F>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, m,
                        n_rows, n_cols, idx, n_idx, cols);
     return hipGetLastError();

@@ -13,6 +13,7 @@
 // per-split partials are folded by a second kernel.
 #include "field.hpp"
 #include "kernels.hpp"
+#include "prof.hpp"
 
 namespace lcpc {
 
@@ -124,10 +125,12 @@ hipError_t collapse_t(const uint32_t *coeffs, size_t n_rows, size_t n_per_row,
   const size_t splits = n_splits_for(n_rows, n_per_row);
   const size_t rps = (n_rows + splits - 1) / splits;
   dim3 grid((unsigned)((n_per_row + 255) / 256), (unsigned)splits);
+  prof::Scope ps("collapse_partial", s);
   hipLaunchKernelGGL((k_collapse_partial<F, T>), grid, dim3(256), 0, s, coeffs, n_rows, n_per_row,
                      tensors, (uint32_t *)scratch, rps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  prof::Scope ps2("collapse_fold", s);
   hipLaunchKernelGGL((k_collapse_fold<F, T>), dim3((unsigned)((n_per_row + 255) / 256)), dim3(256),
                      0, s, (const uint32_t *)scratch, splits, n_per_row, out);
   return hipGetLastError();

@@ -368,6 +368,15 @@ int lcpc_device_count(void) {
   return n;
 }
 
+lcpc_status lcpc_field_random(lcpc_field f, uint64_t seed, uint64_t *out, size_t n) {
+  // F::random(&mut ChaCha20Rng::seed_from_u64(seed)) x n (ff_derive; rand_core 0.6)
+  if (!valid_field(f) || (!out && n)) return fail(LCPC_ERR_INVALID_ARG, "field / out");
+  ChaCha20Rng rng = ChaCha20Rng::seed_from_u64(seed);
+  const FieldInfo fi = field_info(f);
+  field_random(rng, fi.limbs, fi.num_bits, fi.p, out, n);
+  return LCPC_OK;
+}
+
 int lcpc_field_limbs(lcpc_field f) { return valid_field(f) ? field_info(f).limbs : 0; }
 int lcpc_field_num_bits(lcpc_field f) { return valid_field(f) ? field_info(f).num_bits : 0; }
 

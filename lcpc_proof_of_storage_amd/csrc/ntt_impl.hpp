@@ -22,6 +22,7 @@
 #pragma once
 #include "field.hpp"
 #include "kernels.hpp"
+#include "prof.hpp"
 
 namespace lcpc {
 namespace ntt_detail {
@@ -207,6 +208,7 @@ hipError_t launch_a(const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, si
                     const uint32_t *tw, int log_n, size_t n_rows, hipStream_t s) {
   constexpr int LE = log_elems<F>();
   const size_t groups = (size_t)1 << (log_n - LOG_S - (LE - LOG_S));
+  prof::Scope ps("ntt_pass_a", s);
   hipLaunchKernelGGL((k_ntt_pass_a<F, LOG_S, LE>), dim3(n_rows * groups), dim3(NTHREADS), 0, s,
                      src, ss, nv, dst, ds, tw, log_n);
   return hipGetLastError();
@@ -217,6 +219,7 @@ hipError_t launch_b(uint32_t *dst, size_t ds, const uint32_t *tw, int log_n, siz
                     hipStream_t s) {
   constexpr int LE = log_elems<F>();
   const size_t groups = (size_t)1 << (log_n - LOG_S - (LE - LOG_S));
+  prof::Scope ps("ntt_pass_b", s);
   hipLaunchKernelGGL((k_ntt_pass_b<F, LOG_S, LE>), dim3(n_rows * groups), dim3(NTHREADS), 0, s,
                      dst, ds, tw, log_n);
   return hipGetLastError();
@@ -241,6 +244,7 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
                             hipMemcpyDeviceToDevice, s);
   }
   if (p.log_n <= 12) {
+    prof::Scope ps("ntt_small", s);
     hipLaunchKernelGGL((k_ntt_small<F>), dim3(n_rows), dim3(NTHREADS), 0, s, src, ss, nv, dst, ds,
                        p.d_tw, p.log_n);
     return hipGetLastError();

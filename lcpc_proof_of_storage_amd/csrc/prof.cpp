@@ -1,0 +1,116 @@
+// prof.cpp -- see prof.hpp.
+#include "prof.hpp"
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/lcpc_mi.h"
+
+namespace lcpc {
+namespace prof {
+
+namespace {
+struct Rec {
+  const char *name;
+  hipEvent_t a, b;
+};
+std::mutex mu;
+bool on = false;
+std::vector<Rec> pending;
+std::vector<hipEvent_t> spare;
+std::map<std::string, std::pair<double, uint64_t>> totals;
+
+hipEvent_t get_event() {
+  if (!spare.empty()) {
+    hipEvent_t e = spare.back();
+    spare.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void resolve() {  // caller holds mu
+  for (auto &r : pending) {
+    (void)hipEventSynchronize(r.b);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+      auto &t = totals[r.name];
+      t.first += ms;
+      t.second += 1;
+    }
+    spare.push_back(r.a);
+    spare.push_back(r.b);
+  }
+  pending.clear();
+}
+}  // namespace
+
+bool enabled() { return on; }
+
+Scope::Scope(const char *name, hipStream_t s) : s_(s) {
+  if (!on) return;
+  std::lock_guard<std::mutex> lk(mu);
+  Rec r{name, get_event(), get_event()};
+  (void)hipEventRecord(r.a, s);
+  pending.push_back(r);
+  slot_ = (int)pending.size() - 1;
+}
+
+Scope::~Scope() {
+  if (slot_ < 0) return;
+  std::lock_guard<std::mutex> lk(mu);
+  (void)hipEventRecord(pending[slot_].b, s_);
+}
+
+}  // namespace prof
+}  // namespace lcpc
+
+extern "C" {
+
+void lcpc_prof_enable(int enable) {
+  std::lock_guard<std::mutex> lk(lcpc::prof::mu);
+  lcpc::prof::on = enable != 0;
+}
+
+void lcpc_prof_reset(void) {
+  std::lock_guard<std::mutex> lk(lcpc::prof::mu);
+  lcpc::prof::resolve();
+  lcpc::prof::totals.clear();
+}
+
+int lcpc_prof_get(const char *name, double *total_ms, uint64_t *count) {
+  std::lock_guard<std::mutex> lk(lcpc::prof::mu);
+  lcpc::prof::resolve();
+  auto it = lcpc::prof::totals.find(name);
+  if (it == lcpc::prof::totals.end()) {
+    *total_ms = 0;
+    *count = 0;
+    return 0;
+  }
+  *total_ms = it->second.first;
+  *count = it->second.second;
+  return 1;
+}
+
+size_t lcpc_prof_names(char *buf, size_t cap) {
+  std::lock_guard<std::mutex> lk(lcpc::prof::mu);
+  lcpc::prof::resolve();
+  std::string all;
+  for (auto &kv : lcpc::prof::totals) {
+    all += kv.first;
+    all += '\n';
+  }
+  if (buf && cap) {
+    const size_t n = all.size() < cap - 1 ? all.size() : cap - 1;
+    std::memcpy(buf, all.data(), n);
+    buf[n] = 0;
+  }
+  return all.size();
+}
+
+}  // extern "C"

@@ -99,6 +99,37 @@ def _elems(a, field: int) -> np.ndarray:
     return a.reshape(-1, limbs(field))
 
 
+def field_random(field: int, n: int, seed: int) -> np.ndarray:
+    """n draws of F::random(ChaCha20Rng::seed_from_u64(seed)), shape (n, limbs)."""
+    out = np.zeros((n, limbs(field)), np.uint64)
+    _raise(N.load().lcpc_field_random(field, seed, _p64(out), n))
+    return out
+
+
+def prof_enable(on: bool = True):
+    N.load().lcpc_prof_enable(1 if on else 0)
+
+
+def prof_reset():
+    N.load().lcpc_prof_reset()
+
+
+def prof_stats() -> dict:
+    """{kernel name: (total ms, launches)} recorded with HIP events since the last reset."""
+    L = N.load()
+    n = L.lcpc_prof_names(None, 0)
+    buf = C.create_string_buffer(n + 1)
+    L.lcpc_prof_names(buf, n + 1)
+    out = {}
+    for name in buf.value.decode().split("\n"):
+        if not name:
+            continue
+        ms, cnt = C.c_double(), C.c_uint64()
+        L.lcpc_prof_get(name.encode(), C.byref(ms), C.byref(cnt))
+        out[name] = (ms.value, cnt.value)
+    return out
+
+
 def set_device(device: int):
     _raise(N.load().lcpc_set_device(device), DeviceError)
 

@@ -34,6 +34,7 @@ static const uint8_t LABEL_CO[] = "$l//CO";
 /* ---------------- thread pool-less parallel for ---------------- */
 static int g_threads = 1;
 void of_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+int of_get_threads(void) { return g_threads; }
 
 typedef struct {
   of_range_fn fn;
@@ -56,14 +57,21 @@ void of_parallel_for(size_t n, size_t min_chunk, of_range_fn fn, void *ctx) {
   pthread_t th[256];
   pf_arg args[256];
   if (nt > 256) nt = 256;
+  int started[256];
   for (int t = 0; t < nt; t++) {
     args[t].fn = fn;
     args[t].ctx = ctx;
     args[t].lo = n * (size_t)t / (size_t)nt;
     args[t].hi = n * (size_t)(t + 1) / (size_t)nt;
-    pthread_create(&th[t], NULL, pf_tramp, &args[t]);
+    started[t] = t > 0 && pthread_create(&th[t], NULL, pf_tramp, &args[t]) == 0;
   }
-  for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+  fn(ctx, args[0].lo, args[0].hi); /* the calling thread takes the first range */
+  for (int t = 1; t < nt; t++) {
+    if (started[t])
+      pthread_join(th[t], NULL);
+    else
+      fn(ctx, args[t].lo, args[t].hi); /* could not spawn: run inline */
+  }
 }
 
 /* ---------------- parameters ---------------- */
