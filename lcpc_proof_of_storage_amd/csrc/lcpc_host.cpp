@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -20,6 +21,7 @@
 #include "../../include/lcpc_mi.h"
 #include "field.hpp"
 #include "kernels.hpp"
+#include "prof.hpp"
 #include "transcript.hpp"
 
 using namespace lcpc;
@@ -67,23 +69,57 @@ FieldInfo field_info(int fid) {
 bool valid_field(int f) { return f >= 0 && f <= 4; }
 
 // ---------------------------------------------------------------- per-device context
-// One stream + one caching allocator per device; calls on a device are serialized.
+// A pool of HIP streams and a caching allocator per device.  Every API call leases its own
+// stream, so independent commitments run concurrently (their CPU-side Fiat-Shamir work
+// overlaps another commitment's kernels); only pool bookkeeping is locked.
 struct Device {
   int id = 0;
-  hipStream_t stream = nullptr;
-  std::recursive_mutex mu;
-  std::multimap<size_t, void *> free_blocks;  // size -> block
   bool ok = false;
   std::string init_err;
+  std::mutex mu;  // guards the pools below
+  std::vector<hipStream_t> idle_streams[2];  // [0] bulk (commit / encode), [1] high priority
+  std::multimap<size_t, void *> free_blocks;  // size -> block
+  std::map<void *, size_t> sizes;
 
+  // high-priority streams carry the prover's short latency-critical kernels (row
+  // combinations, conversions, gathers) ahead of other commitments' bulk encode work
+  hipStream_t acquire_stream(bool high) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto &pool = idle_streams[high ? 1 : 0];
+      if (!pool.empty()) {
+        hipStream_t s = pool.back();
+        pool.pop_back();
+        return s;
+      }
+    }
+    hipStream_t s = nullptr;
+    (void)hipSetDevice(id);
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = lo = 0;
+    static const bool prio = [] {
+      const char *v = getenv("LCPC_PRIORITY_STREAMS");
+      return !(v && v[0] == '0');
+    }();
+    if (!prio) hi = lo;
+    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? hi : lo) != hipSuccess) return nullptr;
+    return s;
+  }
+  void release_stream(hipStream_t s, bool high) {
+    std::lock_guard<std::mutex> lk(mu);
+    idle_streams[high ? 1 : 0].push_back(s);
+  }
   hipError_t alloc(void **p, size_t bytes) {
     if (bytes == 0) bytes = 16;
     bytes = (bytes + 255) & ~(size_t)255;
-    auto it = free_blocks.find(bytes);
-    if (it != free_blocks.end()) {
-      *p = it->second;
-      free_blocks.erase(it);
-      return hipSuccess;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = free_blocks.find(bytes);
+      if (it != free_blocks.end()) {
+        *p = it->second;
+        free_blocks.erase(it);
+        return hipSuccess;
+      }
     }
     hipError_t e = hipMalloc(p, bytes);
     if (e == hipErrorOutOfMemory) {
@@ -91,24 +127,29 @@ struct Device {
       trim();
       e = hipMalloc(p, bytes);
     }
-    if (e == hipSuccess) sizes[*p] = bytes;
+    if (e == hipSuccess) {
+      std::lock_guard<std::mutex> lk(mu);
+      sizes[*p] = bytes;
+    }
     return e;
   }
+  // the caller guarantees no queued work still uses p
   void release(void *p) {
     if (!p) return;
+    std::lock_guard<std::mutex> lk(mu);
     auto it = sizes.find(p);
     if (it == sizes.end()) return;
     free_blocks.emplace(it->second, p);
   }
   void trim() {
-    (void)hipStreamSynchronize(stream);
+    (void)hipDeviceSynchronize();
+    std::lock_guard<std::mutex> lk(mu);
     for (auto &kv : free_blocks) {
       sizes.erase(kv.second);
       (void)hipFree(kv.second);
     }
     free_blocks.clear();
   }
-  std::map<void *, size_t> sizes;
 };
 
 std::mutex g_devices_mu;
@@ -124,8 +165,7 @@ Device *get_device(int id, lcpc_status *st) {
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= id) {
       slot->init_err = "no HIP device available (liblcpc_mi has no CPU fallback)";
-    } else if ((e = hipSetDevice(id)) != hipSuccess ||
-               (e = hipStreamCreateWithFlags(&slot->stream, hipStreamNonBlocking)) != hipSuccess) {
+    } else if ((e = hipSetDevice(id)) != hipSuccess) {
       slot->init_err = std::string("HIP init failed: ") + hipGetErrorString(e);
     } else {
       slot->ok = true;
@@ -139,34 +179,91 @@ Device *get_device(int id, lcpc_status *st) {
   return slot.get();
 }
 
-// RAII device buffer from the pool
+thread_local hipStream_t t_stream = nullptr;  // stream of the innermost live Lease
+
+// A stream leased for the duration of one API call (also makes the device current).
+struct Lease {
+  Device *d;
+  hipStream_t s;
+  hipStream_t prev;
+  bool high;
+  explicit Lease(Device *dev, bool high_priority = false)
+      : d(dev), s(nullptr), prev(t_stream), high(high_priority) {
+    (void)hipSetDevice(dev->id);
+    s = dev->acquire_stream(high);
+    t_stream = s;
+  }
+  ~Lease() {
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      d->release_stream(s, high);
+    }
+    t_stream = prev;
+  }
+  Lease(const Lease &) = delete;
+  Lease &operator=(const Lease &) = delete;
+};
+
+// RAII device buffer from the pool.  It remembers the stream it was allocated for and
+// drains that stream before returning the block (error paths leave work queued).
 struct DBuf {
   Device *d = nullptr;
   void *p = nullptr;
   size_t n = 0;
+  hipStream_t s = nullptr;
   DBuf() = default;
   DBuf(const DBuf &) = delete;
   DBuf &operator=(const DBuf &) = delete;
-  DBuf(DBuf &&o) noexcept : d(o.d), p(o.p), n(o.n) { o.p = nullptr; }
+  DBuf(DBuf &&o) noexcept : d(o.d), p(o.p), n(o.n), s(o.s) { o.p = nullptr; }
   DBuf &operator=(DBuf &&o) noexcept {
     reset();
-    d = o.d; p = o.p; n = o.n; o.p = nullptr;
+    d = o.d; p = o.p; n = o.n; s = o.s; o.p = nullptr;
     return *this;
   }
   ~DBuf() { reset(); }
   void reset() {
-    if (p && d) d->release(p);
+    if (p && d) {
+      if (s) (void)hipStreamSynchronize(s);
+      d->release(p);
+    }
     p = nullptr;
   }
+  // the queued work using this buffer has completed (no drain needed at release)
+  void settle() { s = nullptr; }
   hipError_t alloc(Device *dev, size_t bytes) {
     reset();
     d = dev;
     n = bytes;
+    s = t_stream;
     return dev->alloc(&p, bytes);
   }
   template <class T>
   T *as() const { return reinterpret_cast<T *>(p); }
 };
+
+// Thread-local pinned (page-locked) host staging buffers: device<->host copies of proof-sized
+// vectors go through these so they are true async DMA (pageable copies are staged and
+// serialize concurrent commitments).  Slots are grown on demand and reused across calls.
+struct PinnedSlot {
+  void *p = nullptr;
+  size_t cap = 0;
+  ~PinnedSlot() {
+    if (p) (void)hipHostFree(p);
+  }
+  void *get(size_t n) {
+    if (n > cap) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+      size_t want = n < 4096 ? 4096 : n + n / 4;
+      if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+      cap = want;
+    }
+    return p;
+  }
+};
+enum { PIN_REPR = 0, PIN_PRANDOM, PIN_PEVAL, PIN_COLS, PIN_PATHS, PIN_TENSOR, PIN_OUTER, PIN_N };
+thread_local PinnedSlot t_pin[PIN_N];
 
 size_t next_pow2(size_t v) {
   size_t p = 1;
@@ -190,9 +287,9 @@ struct lcpc_encoding {
   NttPlan plan;
   ~lcpc_encoding() {
     if (dev) {
-      std::lock_guard<std::recursive_mutex> lk(dev->mu);
+      Lease lease(dev);
       (void)hipSetDevice(dev->id);
-      (void)hipStreamSynchronize(dev->stream);
+      (void)hipStreamSynchronize(lease.s);
       ntt_plan_free(plan);
     }
   }
@@ -248,12 +345,12 @@ lcpc_status make_rs_encoding(int fid, size_t n_per_row, size_t n_cols, size_t nc
   e->n_cols = n_cols;
   e->n_col_opens = nco;
   e->n_degree_tests = ndt;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
-  hipError_t he = ntt_plan_init(e->plan, fid, log_n, false, dev->stream);
+  hipError_t he = ntt_plan_init(e->plan, fid, log_n, false, lease.s);
   if (he == hipErrorInvalidValue) return fail(LCPC_ERR_UNSUPPORTED, "n_cols beyond the supported NTT range");
   HIP_TRY(he);
-  HIP_TRY(hipStreamSynchronize(dev->stream));
+  HIP_TRY(hipStreamSynchronize(lease.s));
   e->dev = dev;
   *out = e.release();
   return LCPC_OK;
@@ -262,23 +359,26 @@ lcpc_status make_rs_encoding(int fid, size_t n_per_row, size_t n_cols, size_t nc
 // upload host -> device (pool buffer)
 lcpc_status upload(Device *dev, DBuf &b, const void *h, size_t bytes) {
   HIP_TRY(b.alloc(dev, bytes));
-  if (bytes) HIP_TRY(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, dev->stream));
+  if (bytes) HIP_TRY(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, t_stream));
   return LCPC_OK;
 }
 
-// field elements -> canonical repr bytes (device convert, then host byte order)
+// field elements -> canonical repr bytes (device convert, D2H into a pinned slot, host byte
+// order); *out points into thread-local pinned memory valid until the next call.
 lcpc_status to_repr_host(Device *dev, int fid, const uint32_t *d_elems, size_t n,
-                         std::vector<uint8_t> &out) {
+                         const uint8_t **out) {
   const int wb = field_bytes(fid);
   DBuf canon;
   HIP_TRY(canon.alloc(dev, n * wb));
-  HIP_TRY(convert(fid, d_elems, canon.as<uint32_t>(), n, false, dev->stream));
-  out.resize(n * wb);
-  if (n) HIP_TRY(hipMemcpyAsync(out.data(), canon.p, n * wb, hipMemcpyDeviceToHost, dev->stream));
-  HIP_TRY(hipStreamSynchronize(dev->stream));
+  HIP_TRY(convert(fid, d_elems, canon.as<uint32_t>(), n, false, t_stream));
+  uint8_t *h = (uint8_t *)t_pin[PIN_REPR].get(n * wb);
+  if (!h) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  if (n) HIP_TRY(hipMemcpyAsync(h, canon.p, n * wb, hipMemcpyDeviceToHost, t_stream));
+  HIP_TRY(hipStreamSynchronize(t_stream));
   if (fid == LCPC_FT253_192) {  // PrimeFieldReprEndianness = "big" (ft253_192.rs:9)
-    for (size_t i = 0; i < n; i++) std::reverse(out.begin() + i * wb, out.begin() + (i + 1) * wb);
+    for (size_t i = 0; i < n; i++) std::reverse(h + i * wb, h + (i + 1) * wb);
   }
+  *out = h;
   return LCPC_OK;
 }
 
@@ -303,6 +403,7 @@ void challenge_columns(Transcript &tr, size_t n_cols, size_t nco, std::vector<ui
 
 lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is_host, size_t len,
                           lcpc_commit **out) {
+  prof::HostScope hs_total("host_commit_total");
   if (!e || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   const size_t np = e->n_per_row, nc = e->n_cols;
   const size_t n_rows = (len + np - 1) / np;  // LcEncoding::get_dims
@@ -313,9 +414,9 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   const size_t np2 = next_pow2(nc);
   if (np2 == 0) return fail(LCPC_PROVER_TOO_BIG, "n_cols too large");
   Device *dev = e->dev;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
-  hipStream_t s = dev->stream;
+  hipStream_t s = lease.s;
   const int fid = e->fid, wb = field_bytes(fid);
   auto c = std::make_unique<lcpc_commit>();
   c->fid = fid;
@@ -343,6 +444,9 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   HIP_TRY(hipMemcpyAsync(c->root, c->hashes.as<uint8_t>() + (c->n_hashes - 1) * 32, 32,
                          hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  c->coeffs.settle();
+  c->comm.settle();
+  c->hashes.settle();
   *out = c.release();
   return LCPC_OK;
 }
@@ -479,18 +583,18 @@ lcpc_status lcpc_encode_rows(const lcpc_encoding *e, uint64_t *rows, size_t n_ro
   if (stride < e->n_cols) return fail(LCPC_ERR_INVALID_ARG, "row stride < n_cols");
   if (n_rows == 0) return LCPC_OK;
   Device *dev = e->dev;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   const int wb = field_bytes(e->fid);
   DBuf d;
   HIP_TRY(d.alloc(dev, n_rows * e->n_cols * wb));
   HIP_TRY(hipMemcpy2DAsync(d.p, e->n_cols * wb, rows, stride * wb, e->n_cols * wb, n_rows,
-                           hipMemcpyHostToDevice, dev->stream));
+                           hipMemcpyHostToDevice, lease.s));
   HIP_TRY(ntt_rows(e->plan, d.as<uint32_t>(), e->n_cols, e->n_cols, d.as<uint32_t>(), e->n_cols,
-                   n_rows, dev->stream));
+                   n_rows, lease.s));
   HIP_TRY(hipMemcpy2DAsync(rows, stride * wb, d.p, e->n_cols * wb, e->n_cols * wb, n_rows,
-                           hipMemcpyDeviceToHost, dev->stream));
-  HIP_TRY(hipStreamSynchronize(dev->stream));
+                           hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
 
@@ -512,9 +616,9 @@ lcpc_status lcpc_encode_rows_device(const lcpc_encoding *e, const void *d_src, s
   if (n_valid > e->n_cols || dst_stride < e->n_cols)
     return fail(LCPC_ERR_INVALID_ARG, "encode_rows_device: bad lengths");
   Device *dev = e->dev;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
-  hipStream_t s = stream ? (hipStream_t)stream : dev->stream;
+  hipStream_t s = stream ? (hipStream_t)stream : lease.s;
   HIP_TRY(ntt_rows(e->plan, (const uint32_t *)d_src, src_stride, n_valid, (uint32_t *)d_dst,
                    dst_stride, n_rows, s));
   if (!stream) HIP_TRY(hipStreamSynchronize(s));
@@ -537,9 +641,9 @@ lcpc_status lcpc_commit_new_device(const lcpc_encoding *e, const void *d_coeffs,
 void lcpc_commit_free(lcpc_commit *c) {
   if (!c) return;
   Device *dev = c->dev;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   (void)hipSetDevice(dev->id);
-  (void)hipStreamSynchronize(dev->stream);
+  (void)hipStreamSynchronize(lease.s);
   delete c;
 }
 
@@ -555,10 +659,10 @@ const void *lcpc_commit_device_comm(const lcpc_commit *c) { return c->comm.p; }
 const void *lcpc_commit_device_coeffs(const lcpc_commit *c) { return c->coeffs.p; }
 
 static lcpc_status copy_out(const lcpc_commit *c, void *dst, const void *src, size_t bytes) {
-  std::lock_guard<std::recursive_mutex> lk(c->dev->mu);
+  Lease lease(c->dev);
   HIP_TRY(hipSetDevice(c->dev->id));
-  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->dev->stream));
-  HIP_TRY(hipStreamSynchronize(c->dev->stream));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
 lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out) {
@@ -586,7 +690,7 @@ lcpc_status lcpc_open_column(const lcpc_commit *c, size_t column, uint64_t *col_
   if (!c) return fail(LCPC_ERR_INVALID_ARG, "null commit");
   if (column >= c->n_cols) return fail(LCPC_PROVER_COLUMN_NUMBER, "ProverError::ColumnNumber");
   Device *dev = c->dev;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   const uint64_t idx = column;
   const size_t path_len = log2_np2(c->n_cols);
@@ -597,13 +701,13 @@ lcpc_status lcpc_open_column(const lcpc_commit *c, size_t column, uint64_t *col_
   HIP_TRY(dcol.alloc(dev, c->n_rows * wb));
   HIP_TRY(dpath.alloc(dev, path_len * 32));
   HIP_TRY(gather_columns(c->fid, c->comm.as<uint32_t>(), c->n_rows, c->n_cols, didx.as<uint64_t>(), 1,
-                         dcol.as<uint32_t>(), dev->stream));
+                         dcol.as<uint32_t>(), lease.s));
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), 1, path_len,
-                       dpath.as<uint8_t>(), dev->stream));
-  if (col_out) HIP_TRY(hipMemcpyAsync(col_out, dcol.p, c->n_rows * wb, hipMemcpyDeviceToHost, dev->stream));
+                       dpath.as<uint8_t>(), lease.s));
+  if (col_out) HIP_TRY(hipMemcpyAsync(col_out, dcol.p, c->n_rows * wb, hipMemcpyDeviceToHost, lease.s));
   if (path_out && path_len)
-    HIP_TRY(hipMemcpyAsync(path_out, dpath.p, path_len * 32, hipMemcpyDeviceToHost, dev->stream));
-  HIP_TRY(hipStreamSynchronize(dev->stream));
+    HIP_TRY(hipMemcpyAsync(path_out, dpath.p, path_len * 32, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
 
@@ -626,15 +730,16 @@ void lcpc_transcript_challenge_bytes(lcpc_transcript *t, const uint8_t *l, size_
 lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer_len,
                        const lcpc_encoding *e, lcpc_transcript *tr, lcpc_proof **out) {
   // prove (lcpc-2d/src/lib.rs:1034-1123)
+  prof::HostScope hs_total("host_prove_total");
   if (!c || !e || !tr || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   lcpc_status st = lcpc_check_comm(c, e);
   if (st) return st;
   if (outer_len != c->n_rows || (!outer && outer_len))
     return fail(LCPC_PROVER_OUTER_TENSOR, "ProverError::OuterTensor");
   Device *dev = c->dev;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev, true);
   HIP_TRY(hipSetDevice(dev->id));
-  hipStream_t s = dev->stream;
+  hipStream_t s = lease.s;
   const int fid = c->fid, wb = field_bytes(fid), limbs = wb / 8;
   const size_t nr = c->n_rows, np = c->n_per_row, ndt = e->n_degree_tests, nco = e->n_col_opens;
   auto p = std::make_unique<lcpc_proof>();
@@ -645,8 +750,14 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   p->ndt = ndt;
   p->nco = nco;
   p->path_len = log2_np2(c->n_cols);
-  p->p_random.resize(ndt * np * limbs);
-  p->p_eval.resize(np * limbs);
+
+  // pinned staging for everything that crosses PCIe
+  uint8_t *h_prand = (uint8_t *)t_pin[PIN_PRANDOM].get(std::max<size_t>(1, ndt) * np * wb);
+  uint8_t *h_peval = (uint8_t *)t_pin[PIN_PEVAL].get(np * wb);
+  uint8_t *h_tens = (uint8_t *)t_pin[PIN_TENSOR].get(nr * wb);
+  uint8_t *h_outer = (uint8_t *)t_pin[PIN_OUTER].get(nr * wb);
+  if (!h_prand || !h_peval || !h_tens || !h_outer) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  std::memcpy(h_outer, outer, nr * wb);
 
   // tensors on device: [t_i | outer] -- the evaluation tensor rides along with the first
   // degree test so the coefficient matrix is read once for both (results are independent).
@@ -654,57 +765,75 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   HIP_TRY(dtens.alloc(dev, 2 * nr * wb));
   HIP_TRY(dres.alloc(dev, 2 * np * wb));
   HIP_TRY(scratch.alloc(dev, collapse_scratch_bytes(fid, nr, np, 2)));
-  HIP_TRY(hipMemcpyAsync(dtens.as<uint8_t>() + nr * wb, outer, nr * wb, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(dtens.as<uint8_t>() + nr * wb, h_outer, nr * wb, hipMemcpyHostToDevice, s));
   std::vector<uint64_t> tensor;
-  std::vector<uint8_t> repr;
+  const uint8_t *repr = nullptr;
   bool eval_done = false;
   for (size_t i = 0; i < ndt; i++) {
     challenge_tensor(tr->t, fid, nr, tensor);
-    HIP_TRY(hipMemcpyAsync(dtens.p, tensor.data(), nr * wb, hipMemcpyHostToDevice, s));
+    std::memcpy(h_tens, tensor.data(), nr * wb);
+    HIP_TRY(hipMemcpyAsync(dtens.p, h_tens, nr * wb, hipMemcpyHostToDevice, s));
     const int nt = eval_done ? 1 : 2;
     HIP_TRY(collapse_rows(fid, c->coeffs.as<uint32_t>(), nr, np, dtens.as<uint32_t>(), nt,
                           dres.as<uint32_t>(), scratch.p, s));
-    HIP_TRY(hipMemcpyAsync(p->p_random.data() + i * np * limbs, dres.p, np * wb,
-                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_prand + i * np * wb, dres.p, np * wb, hipMemcpyDeviceToHost, s));
     if (!eval_done) {
-      HIP_TRY(hipMemcpyAsync(p->p_eval.data(), dres.as<uint8_t>() + np * wb, np * wb,
-                             hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(h_peval, dres.as<uint8_t>() + np * wb, np * wb, hipMemcpyDeviceToHost, s));
       eval_done = true;
     }
-    st = to_repr_host(dev, fid, dres.as<uint32_t>(), np, repr);  // syncs the stream
+    {
+      prof::HostScope hs("host_prove_gpu_wait");
+      st = to_repr_host(dev, fid, dres.as<uint32_t>(), np, &repr);  // syncs the stream
+    }
     if (st) return st;
-    tr->t.append_messages(LABEL_PR, 6, repr.data(), wb, np);
+    {
+      prof::HostScope hs("host_prove_transcript");
+      tr->t.append_messages(LABEL_PR, 6, repr, wb, np);
+    }
   }
   const uint32_t *d_eval = dres.as<uint32_t>() + np * limbs * 2;  // second collapse output
   if (!eval_done) {
     HIP_TRY(collapse_rows(fid, c->coeffs.as<uint32_t>(), nr, np, dtens.as<uint32_t>() + nr * limbs * 2, 1,
                           dres.as<uint32_t>(), scratch.p, s));
-    HIP_TRY(hipMemcpyAsync(p->p_eval.data(), dres.p, np * wb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_peval, dres.p, np * wb, hipMemcpyDeviceToHost, s));
     d_eval = dres.as<uint32_t>();
   }
-  st = to_repr_host(dev, fid, d_eval, np, repr);
+  {
+    prof::HostScope hs("host_prove_gpu_wait");
+    st = to_repr_host(dev, fid, d_eval, np, &repr);
+  }
   if (st) return st;
-  tr->t.append_messages(LABEL_PE, 6, repr.data(), wb, np);
+  {
+    prof::HostScope hs("host_prove_transcript");
+    tr->t.append_messages(LABEL_PE, 6, repr, wb, np);
+  }
 
   // columns (:1101-1115)
   challenge_columns(tr->t, c->n_cols, nco, p->col_idx);
+  uint8_t *h_cols = (uint8_t *)t_pin[PIN_COLS].get(std::max<size_t>(1, nco * nr * wb));
+  uint8_t *h_paths = (uint8_t *)t_pin[PIN_PATHS].get(std::max<size_t>(1, nco * p->path_len * 32 + nco * 8));
+  if (!h_cols || !h_paths) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  uint8_t *h_idx = h_paths + nco * p->path_len * 32;
+  std::memcpy(h_idx, p->col_idx.data(), nco * 8);
   DBuf didx, dcols, dpaths;
-  st = upload(dev, didx, p->col_idx.data(), nco * 8);
-  if (st) return st;
+  HIP_TRY(didx.alloc(dev, nco * 8));
+  if (nco) HIP_TRY(hipMemcpyAsync(didx.p, h_idx, nco * 8, hipMemcpyHostToDevice, s));
   HIP_TRY(dcols.alloc(dev, nco * nr * wb));
   HIP_TRY(dpaths.alloc(dev, nco * p->path_len * 32));
   HIP_TRY(gather_columns(fid, c->comm.as<uint32_t>(), nr, c->n_cols, didx.as<uint64_t>(), nco,
                          dcols.as<uint32_t>(), s));
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), nco, p->path_len,
                        dpaths.as<uint8_t>(), s));
-  p->cols.resize(nco * nr * limbs);
-  p->paths.resize(nco * p->path_len * 32);
   if (nco) {
-    HIP_TRY(hipMemcpyAsync(p->cols.data(), dcols.p, nco * nr * wb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_cols, dcols.p, nco * nr * wb, hipMemcpyDeviceToHost, s));
     if (p->path_len)
-      HIP_TRY(hipMemcpyAsync(p->paths.data(), dpaths.p, p->paths.size(), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(h_paths, dpaths.p, nco * p->path_len * 32, hipMemcpyDeviceToHost, s));
   }
   HIP_TRY(hipStreamSynchronize(s));
+  p->p_random.assign((const uint64_t *)h_prand, (const uint64_t *)(h_prand + ndt * np * wb));
+  p->p_eval.assign((const uint64_t *)h_peval, (const uint64_t *)(h_peval + np * wb));
+  p->cols.assign((const uint64_t *)h_cols, (const uint64_t *)(h_cols + nco * nr * wb));
+  p->paths.assign(h_paths, h_paths + nco * p->path_len * 32);
   *out = p.release();
   return LCPC_OK;
 }
@@ -775,9 +904,9 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
   if (p->ndt != ndt) return fail(LCPC_VERIFIER_ENCODING_DIMS, "proof has a different number of degree tests");
   const int fid = e->fid, wb = field_bytes(fid), limbs = wb / 8;
   Device *dev = e->dev;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev, true);
   HIP_TRY(hipSetDevice(dev->id));
-  hipStream_t s = dev->stream;
+  hipStream_t s = lease.s;
 
   // device copies: tensors [ndt | outer] (n_rows each), encodings [ndt + 1][n_cols]
   DBuf dtens, denc, dvec, didx, dcols, dpaths, dleaves, dflags, dpflags, scratch, dinner, dout, droot;
@@ -785,7 +914,7 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
   HIP_TRY(denc.alloc(dev, (ndt + 1) * nc * wb));
   HIP_TRY(hipMemcpyAsync(dtens.as<uint8_t>() + ndt * nr * wb, outer, nr * wb, hipMemcpyHostToDevice, s));
   std::vector<uint64_t> tensor;
-  std::vector<uint8_t> repr;
+  const uint8_t *repr = nullptr;
   lcpc_status st;
   for (size_t i = 0; i < ndt; i++) {
     challenge_tensor(tr->t, fid, nr, tensor);
@@ -794,15 +923,15 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
     st = upload(dev, dvec, p->p_random.data() + i * np * limbs, np * wb);
     if (st) return st;
     HIP_TRY(ntt_rows(e->plan, dvec.as<uint32_t>(), np, np, denc.as<uint32_t>() + i * nc * limbs * 2, nc, 1, s));
-    st = to_repr_host(dev, fid, dvec.as<uint32_t>(), np, repr);
+    st = to_repr_host(dev, fid, dvec.as<uint32_t>(), np, &repr);
     if (st) return st;
-    tr->t.append_messages(LABEL_PR, 6, repr.data(), wb, np);
+    tr->t.append_messages(LABEL_PR, 6, repr, wb, np);
   }
   st = upload(dev, dvec, p->p_eval.data(), np * wb);
   if (st) return st;
-  st = to_repr_host(dev, fid, dvec.as<uint32_t>(), np, repr);
+  st = to_repr_host(dev, fid, dvec.as<uint32_t>(), np, &repr);
   if (st) return st;
-  tr->t.append_messages(LABEL_PE, 6, repr.data(), wb, np);
+  tr->t.append_messages(LABEL_PE, 6, repr, wb, np);
   std::vector<uint64_t> idx;
   challenge_columns(tr->t, nc, nco, idx);
   HIP_TRY(ntt_rows(e->plan, dvec.as<uint32_t>(), np, np, denc.as<uint32_t>() + ndt * nc * limbs * 2, nc, 1, s));
@@ -857,7 +986,7 @@ lcpc_status lcpc_collapse_columns(lcpc_field f, const uint64_t *coeffs, const ui
   lcpc_status st;
   Device *dev = current_device(&st);
   if (!dev) return st;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   const int wb = field_bytes(f);
   DBuf dc, dt, dp, scratch;
@@ -866,9 +995,9 @@ lcpc_status lcpc_collapse_columns(lcpc_field f, const uint64_t *coeffs, const ui
   HIP_TRY(dp.alloc(dev, n_per_row * wb));
   HIP_TRY(scratch.alloc(dev, collapse_scratch_bytes(f, n_rows, n_per_row, 1)));
   HIP_TRY(collapse_rows(f, dc.as<uint32_t>(), n_rows, n_per_row, dt.as<uint32_t>(), 1, dp.as<uint32_t>(),
-                        scratch.p, dev->stream));
-  HIP_TRY(hipMemcpyAsync(poly, dp.p, n_per_row * wb, hipMemcpyDeviceToHost, dev->stream));
-  HIP_TRY(hipStreamSynchronize(dev->stream));
+                        scratch.p, lease.s));
+  HIP_TRY(hipMemcpyAsync(poly, dp.p, n_per_row * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
 
@@ -877,16 +1006,16 @@ lcpc_status lcpc_merkle_tree(const uint8_t *ins, size_t n_ins, uint8_t *outs) {
   lcpc_status st;
   Device *dev = current_device(&st);
   if (!dev) return st;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   DBuf d;
   HIP_TRY(d.alloc(dev, (2 * n_ins - 1) * 32));
-  HIP_TRY(hipMemcpyAsync(d.p, ins, n_ins * 32, hipMemcpyHostToDevice, dev->stream));
-  HIP_TRY(merkle_tree(d.as<uint8_t>(), n_ins, dev->stream));
+  HIP_TRY(hipMemcpyAsync(d.p, ins, n_ins * 32, hipMemcpyHostToDevice, lease.s));
+  HIP_TRY(merkle_tree(d.as<uint8_t>(), n_ins, lease.s));
   if (n_ins > 1)
     HIP_TRY(hipMemcpyAsync(outs, d.as<uint8_t>() + n_ins * 32, (n_ins - 1) * 32, hipMemcpyDeviceToHost,
-                           dev->stream));
-  HIP_TRY(hipStreamSynchronize(dev->stream));
+                           lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
 
@@ -896,16 +1025,16 @@ lcpc_status lcpc_hash_columns(lcpc_field f, const uint64_t *comm, size_t n_rows,
   lcpc_status st;
   Device *dev = current_device(&st);
   if (!dev) return st;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   const int wb = field_bytes(f);
   DBuf dm, dl, scratch;
   if ((st = upload(dev, dm, comm, n_rows * n_cols * wb))) return st;
   HIP_TRY(dl.alloc(dev, n_cols * 32));
   HIP_TRY(scratch.alloc(dev, leaf_hash_scratch_bytes(f, n_rows, n_cols)));
-  HIP_TRY(leaf_hashes(f, dm.as<uint32_t>(), n_rows, n_cols, n_cols, dl.as<uint8_t>(), scratch.p, dev->stream));
-  HIP_TRY(hipMemcpyAsync(out, dl.p, n_cols * 32, hipMemcpyDeviceToHost, dev->stream));
-  HIP_TRY(hipStreamSynchronize(dev->stream));
+  HIP_TRY(leaf_hashes(f, dm.as<uint32_t>(), n_rows, n_cols, n_cols, dl.as<uint8_t>(), scratch.p, lease.s));
+  HIP_TRY(hipMemcpyAsync(out, dl.p, n_cols * 32, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
 
@@ -915,7 +1044,7 @@ int lcpc_verify_column_path(lcpc_field f, const uint64_t *col, size_t n_rows, co
   lcpc_status st;
   Device *dev = current_device(&st);
   if (!dev) return 0;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   if (hipSetDevice(dev->id) != hipSuccess) return 0;
   const int wb = field_bytes(f);
   DBuf dc, dp, di, dr, dl, dfl, scratch;
@@ -925,13 +1054,13 @@ int lcpc_verify_column_path(lcpc_field f, const uint64_t *col, size_t n_rows, co
     return 0;
   if (dl.alloc(dev, 32) || dfl.alloc(dev, 4) || scratch.alloc(dev, leaf_hash_scratch_bytes(f, n_rows, 1)))
     return 0;
-  if (leaf_hashes_cols(f, dc.as<uint32_t>(), n_rows, 1, dl.as<uint8_t>(), scratch.p, dev->stream) ||
+  if (leaf_hashes_cols(f, dc.as<uint32_t>(), n_rows, 1, dl.as<uint8_t>(), scratch.p, lease.s) ||
       path_checks(dl.as<uint8_t>(), dp.as<uint8_t>(), 1, path_len, di.as<uint64_t>(), dr.as<uint8_t>(),
-                  dfl.as<uint32_t>(), dev->stream))
+                  dfl.as<uint32_t>(), lease.s))
     return 0;
   uint32_t flag = 0;
-  if (hipMemcpyAsync(&flag, dfl.p, 4, hipMemcpyDeviceToHost, dev->stream) ||
-      hipStreamSynchronize(dev->stream))
+  if (hipMemcpyAsync(&flag, dfl.p, 4, hipMemcpyDeviceToHost, lease.s) ||
+      hipStreamSynchronize(lease.s))
     return 0;
   return flag != 0;
 }
@@ -942,7 +1071,7 @@ int lcpc_verify_column_value(lcpc_field f, const uint64_t *col, const uint64_t *
   lcpc_status st;
   Device *dev = current_device(&st);
   if (!dev) return 0;
-  std::lock_guard<std::recursive_mutex> lk(dev->mu);
+  Lease lease(dev);
   if (hipSetDevice(dev->id) != hipSuccess) return 0;
   const int wb = field_bytes(f);
   DBuf dc, dt, de, di, dfl;
@@ -951,11 +1080,11 @@ int lcpc_verify_column_value(lcpc_field f, const uint64_t *col, const uint64_t *
       upload(dev, de, poly_eval, wb) || upload(dev, di, &zero, 8) || dfl.alloc(dev, 4))
     return 0;
   if (column_checks(f, dc.as<uint32_t>(), 1, n_rows, dt.as<uint32_t>(), 1, de.as<uint32_t>(), 1,
-                    di.as<uint64_t>(), dfl.as<uint32_t>(), dev->stream))
+                    di.as<uint64_t>(), dfl.as<uint32_t>(), lease.s))
     return 0;
   uint32_t flag = 0;
-  if (hipMemcpyAsync(&flag, dfl.p, 4, hipMemcpyDeviceToHost, dev->stream) ||
-      hipStreamSynchronize(dev->stream))
+  if (hipMemcpyAsync(&flag, dfl.p, 4, hipMemcpyDeviceToHost, lease.s) ||
+      hipStreamSynchronize(lease.s))
     return 0;
   return flag != 0;
 }

@@ -14,14 +14,15 @@
 // Position t' M + c' then holds X_{j1 + 2^l1 j2} with j1 = bitrev(t'), j2 = bitrev(c'), which
 // is exactly out[bitrev_log_n(j)].
 //
-// Each workgroup (256 threads) stages a tile of 2^LOG_E elements in LDS laid out [t][v] with
-// one element of row padding (conflict-free 16-B columns), runs the sub-FFTs as radix-2^R
-// register rounds (R stages per LDS round trip, twiddles from an LDS table), and streams
-// coalesced rows of HBM in and out.  The last DIF stage of every sub-FFT has twiddle 1 and
+// Passes (ntt_v2.hpp): each workgroup owns a tile of CW sub-FFT vectors; the first radix-2^R
+// round reads HBM directly, rounds exchange through one padded LDS tile, and pass A's last round
+// applies the inter-pass twiddle and writes HBM directly.  Rows of length <= 2^12 use a single
+// whole-row-in-LDS kernel (k_ntt_small).  The last DIF stage of every sub-FFT has twiddle 1 and
 // is multiplication-free at compile time.
 #pragma once
 #include "field.hpp"
 #include "kernels.hpp"
+#include "ntt_v2.hpp"
 #include "prof.hpp"
 
 namespace lcpc {
@@ -43,127 +44,6 @@ __global__ void k_tw_table(uint32_t *__restrict__ tw, int log_n, int inverse) {
 
 __device__ __forceinline__ int bitrev(int x, int bits) {
   return bits ? (int)(__builtin_bitreverse32((uint32_t)x) >> (32 - bits)) : 0;
-}
-
-// One radix-2^RR round of the S-point DIF (stages S0 .. S0+RR-1) on CW vectors in LDS.
-template <class F, int LOG_S, int LOG_CW, int S0, int RR>
-__device__ __forceinline__ void dif_round(Fe<F> *tile, const Fe<F> *tw, int tid) {
-  constexpr int CW = 1 << LOG_CW, LD = CW + 1;
-  constexpr int LOG_GL = LOG_S - S0 - RR;  // log2 of the smallest gap in this round
-  constexpr int GL = 1 << LOG_GL;
-  constexpr int K = 1 << RR;
-  constexpr int ITEMS = (1 << (LOG_S - RR)) * CW;
-  for (int item = tid; item < ITEMS; item += NTHREADS) {
-    const int v = item & (CW - 1);
-    const int q = item >> LOG_CW;
-    const int b_lo = q & (GL - 1);
-    const int b = b_lo + ((q >> LOG_GL) << (LOG_GL + RR));
-    Fe<F> x[K];
-#pragma unroll
-    for (int j = 0; j < K; j++) x[j] = tile[(b + j * GL) * LD + v];
-#pragma unroll
-    for (int qq = 0; qq < RR; qq++) {
-      const int s = S0 + qq;
-      const int h = 1 << (RR - 1 - qq);
-#pragma unroll
-      for (int j = 0; j < K; j++) {
-        if (j & h) continue;
-        const Fe<F> a = x[j], c = x[j + h];
-        x[j] = fe_add<F>(a, c);
-        const Fe<F> d = fe_sub<F>(a, c);
-        const int jm = j & (h - 1);
-        if (LOG_GL == 0 && jm == 0) {
-          x[j + h] = d;  // twiddle w^0
-        } else {
-          const int e = (b_lo + jm * GL) << s;
-          x[j + h] = fe_mul<F>(d, tw[e]);
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < K; j++) tile[(b + j * GL) * LD + v] = x[j];
-  }
-}
-
-template <class F, int LOG_S, int LOG_CW, int R, int S0>
-__device__ __forceinline__ void dif_all(Fe<F> *tile, const Fe<F> *tw, int tid) {
-  if constexpr (S0 < LOG_S) {
-    constexpr int RR = (LOG_S - S0) < R ? (LOG_S - S0) : R;
-    dif_round<F, LOG_S, LOG_CW, S0, RR>(tile, tw, tid);
-    __syncthreads();
-    dif_all<F, LOG_S, LOG_CW, R, S0 + RR>(tile, tw, tid);
-  }
-}
-
-template <class F, int LOG_S, int LOG_E>
-__global__ __launch_bounds__(NTHREADS) void k_ntt_pass_a(const uint32_t *__restrict__ src,
-                                                         size_t src_stride, size_t n_valid,
-                                                         uint32_t *__restrict__ dst,
-                                                         size_t dst_stride,
-                                                         const uint32_t *__restrict__ twn,
-                                                         int log_n) {
-  constexpr int LOG_CW = LOG_E - LOG_S;
-  constexpr int S = 1 << LOG_S, CW = 1 << LOG_CW, LD = CW + 1;
-  constexpr int R = LOG_E - 8;
-  __shared__ __align__(16) uint32_t smem[(S * LD + S / 2) * F::N];
-  Fe<F> *tile = reinterpret_cast<Fe<F> *>(smem);
-  Fe<F> *tw = tile + S * LD;
-  const int tid = threadIdx.x;
-  const int log_m = log_n - LOG_S;
-  const int groups = 1 << (log_m - LOG_CW);
-  const size_t row = blockIdx.x / groups;
-  const size_t c0 = (size_t)(blockIdx.x % groups) << LOG_CW;
-
-  for (int e = tid; e < S / 2; e += NTHREADS) tw[e] = fe_load<F>(twn, (size_t)e << log_m);
-  const uint32_t *in = src + row * src_stride * F::N;
-  for (int idx = tid; idx < S * CW; idx += NTHREADS) {
-    const int t = idx >> LOG_CW, v = idx & (CW - 1);
-    const size_t pos = c0 + v + ((size_t)t << log_m);
-    tile[t * LD + v] = pos < n_valid ? fe_load<F>(in, pos) : fe_zero<F>();
-  }
-  __syncthreads();
-  dif_all<F, LOG_S, LOG_CW, R, 0>(tile, tw, tid);
-
-  uint32_t *out = dst + row * dst_stride * F::N;
-  for (int idx = tid; idx < S * CW; idx += NTHREADS) {
-    const int t = idx >> LOG_CW, v = idx & (CW - 1);
-    const size_t c = c0 + v;
-    const size_t e = c * (size_t)bitrev(t, LOG_S);
-    Fe<F> x = tile[t * LD + v];
-    if (e) x = fe_mul<F>(x, fe_load<F>(twn, e));
-    fe_store<F>(out, c + ((size_t)t << log_m), x);
-  }
-}
-
-template <class F, int LOG_S, int LOG_E>
-__global__ __launch_bounds__(NTHREADS) void k_ntt_pass_b(uint32_t *__restrict__ data,
-                                                         size_t stride,
-                                                         const uint32_t *__restrict__ twn,
-                                                         int log_n) {
-  constexpr int LOG_CW = LOG_E - LOG_S;
-  constexpr int S = 1 << LOG_S, CW = 1 << LOG_CW, LD = CW + 1;
-  constexpr int R = LOG_E - 8;
-  __shared__ __align__(16) uint32_t smem[(S * LD + S / 2) * F::N];
-  Fe<F> *tile = reinterpret_cast<Fe<F> *>(smem);
-  Fe<F> *tw = tile + S * LD;
-  const int tid = threadIdx.x;
-  const int log_blocks = log_n - LOG_S;  // contiguous S-blocks per row
-  const int groups = 1 << (log_blocks - LOG_CW);
-  const size_t row = blockIdx.x / groups;
-  const size_t b0 = (size_t)(blockIdx.x % groups) << LOG_CW;
-
-  for (int e = tid; e < S / 2; e += NTHREADS) tw[e] = fe_load<F>(twn, (size_t)e << log_blocks);
-  uint32_t *io = data + (row * stride + b0 * S) * F::N;
-  for (int idx = tid; idx < S * CW; idx += NTHREADS) {
-    const int v = idx >> LOG_S, t = idx & (S - 1);
-    tile[t * LD + v] = fe_load<F>(io, idx);
-  }
-  __syncthreads();
-  dif_all<F, LOG_S, LOG_CW, R, 0>(tile, tw, tid);
-  for (int idx = tid; idx < S * CW; idx += NTHREADS) {
-    const int v = idx >> LOG_S, t = idx & (S - 1);
-    fe_store<F>(io, idx, tile[t * LD + v]);
-  }
 }
 
 // Whole row in LDS (log_n <= 12): plain radix-2 DIF stages.
@@ -198,31 +78,34 @@ __global__ __launch_bounds__(NTHREADS) void k_ntt_small(const uint32_t *__restri
   for (int i = threadIdx.x; i < n; i += NTHREADS) fe_store<F>(out, i, buf[i]);
 }
 
+// Per-field tile shapes for the v2 passes (tools/microbench/nttbench.hip sweep on MI355X):
+// R = log2(elements per thread per round), E = log2(tile elements per workgroup).
 template <class F>
-constexpr int log_elems() {
-  return F::N >= 8 ? 11 : 12;  // 64 KiB-class tiles; 32-byte fields use 2^11
-}
+struct Shape;
+template <>
+struct Shape<Ft63> {
+  static constexpr int R = 3, E = 12;
+};
+template <>
+struct Shape<Ft127> {
+  static constexpr int R = 3, E = 11;
+};
+template <>
+struct Shape<Ft255> {
+  static constexpr int R = 2, E = 10;
+};
+template <>
+struct Shape<Ft253_192> {
+  static constexpr int R = 2, E = 10;
+};
+template <>
+struct Shape<Ft191> {
+  static constexpr int R = 2, E = 10;
+};
 
-template <class F, int LOG_S>
-hipError_t launch_a(const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
-                    const uint32_t *tw, int log_n, size_t n_rows, hipStream_t s) {
-  constexpr int LE = log_elems<F>();
-  const size_t groups = (size_t)1 << (log_n - LOG_S - (LE - LOG_S));
-  prof::Scope ps("ntt_pass_a", s);
-  hipLaunchKernelGGL((k_ntt_pass_a<F, LOG_S, LE>), dim3(n_rows * groups), dim3(NTHREADS), 0, s,
-                     src, ss, nv, dst, ds, tw, log_n);
-  return hipGetLastError();
-}
-
-template <class F, int LOG_S>
-hipError_t launch_b(uint32_t *dst, size_t ds, const uint32_t *tw, int log_n, size_t n_rows,
-                    hipStream_t s) {
-  constexpr int LE = log_elems<F>();
-  const size_t groups = (size_t)1 << (log_n - LOG_S - (LE - LOG_S));
-  prof::Scope ps("ntt_pass_b", s);
-  hipLaunchKernelGGL((k_ntt_pass_b<F, LOG_S, LE>), dim3(n_rows * groups), dim3(NTHREADS), 0, s,
-                     dst, ds, tw, log_n);
-  return hipGetLastError();
+template <int LOG_S, int E>
+constexpr int log_cw() {
+  return E > LOG_S ? E - LOG_S : 0;
 }
 
 template <class F, int LO, int HI, class Fn>
@@ -249,13 +132,21 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
                        p.d_tw, p.log_n);
     return hipGetLastError();
   }
-  constexpr int LE = log_elems<F>();
-  hipError_t e = dispatch_logs<F, 6, LE>(p.l1, [&]<int L>() {
-    return launch_a<F, L>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s);
+  constexpr int R = Shape<F>::R, E = Shape<F>::E;
+  const bool halfz = 2 * nv <= ((size_t)1 << p.log_n);
+  constexpr int HI = F::N >= 8 ? 11 : 12;  // LDS budget of 32-byte fields
+  hipError_t e = dispatch_logs<F, 6, HI>(p.l1, [&]<int L>() {
+    constexpr int CW = log_cw<L, E>();
+    constexpr int T = L + CW - R;
+    if (halfz)
+      return ntt_v2::launch_a<F, L, CW, T, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s);
+    return ntt_v2::launch_a<F, L, CW, T, false>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s);
   });
   if (e != hipSuccess) return e;
-  return dispatch_logs<F, 6, LE>(p.l2, [&]<int L>() {
-    return launch_b<F, L>(dst, ds, p.d_tw, p.log_n, n_rows, s);
+  return dispatch_logs<F, 7, HI>(p.l2, [&]<int L>() {
+    constexpr int CW = log_cw<L, E>();
+    constexpr int T = L + CW - R;
+    return ntt_v2::launch_b<F, L, CW, T>(dst, ds, p.d_tw, p.log_n, n_rows, s);
   });
 }
 

@@ -1,6 +1,7 @@
 // prof.cpp -- see prof.hpp.
 #include "prof.hpp"
 
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -52,19 +53,38 @@ void resolve() {  // caller holds mu
 
 bool enabled() { return on; }
 
-Scope::Scope(const char *name, hipStream_t s) : s_(s) {
+Scope::Scope(const char *name, hipStream_t s) : name_(name), s_(s) {
   if (!on) return;
-  std::lock_guard<std::mutex> lk(mu);
-  Rec r{name, get_event(), get_event()};
-  (void)hipEventRecord(r.a, s);
-  pending.push_back(r);
-  slot_ = (int)pending.size() - 1;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    a_ = get_event();
+    b_ = get_event();
+  }
+  (void)hipEventRecord(a_, s);
 }
 
 Scope::~Scope() {
-  if (slot_ < 0) return;
+  if (!a_) return;
+  (void)hipEventRecord(b_, s_);
   std::lock_guard<std::mutex> lk(mu);
-  (void)hipEventRecord(pending[slot_].b, s_);
+  pending.push_back(Rec{name_, a_, b_});
+}
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+HostScope::HostScope(const char *name) : name_(name) {
+  if (on) t0_ = now_ms();
+}
+
+HostScope::~HostScope() {
+  if (t0_ < 0) return;
+  const double dt = now_ms() - t0_;
+  std::lock_guard<std::mutex> lk(mu);
+  auto &t = totals[name_];
+  t.first += dt;
+  t.second += 1;
 }
 
 }  // namespace prof

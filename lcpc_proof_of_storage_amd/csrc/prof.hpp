@@ -15,8 +15,20 @@ class Scope {
   ~Scope();
 
  private:
-  int slot_ = -1;
+  const char *name_;
+  hipEvent_t a_ = nullptr, b_ = nullptr;
   hipStream_t s_;
+};
+
+// wall time of a host-side phase (accumulated under `name`, same table as the kernels)
+class HostScope {
+ public:
+  explicit HostScope(const char *name);
+  ~HostScope();
+
+ private:
+  const char *name_;
+  double t0_ = -1.0;
 };
 
 }  // namespace prof

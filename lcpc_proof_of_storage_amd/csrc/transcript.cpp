@@ -173,7 +173,43 @@ void Transcript::append_message(const uint8_t *label, size_t ln, const uint8_t *
 
 void Transcript::append_messages(const uint8_t *label, size_t ln, const uint8_t *msgs,
                                  size_t msg_len, size_t n_msgs) {
-  for (size_t i = 0; i < n_msgs; i++) append_message(label, ln, msgs + i * msg_len, msg_len);
+  // One append absorbs the record  [pos_begin, M|A] label LE32(len) [pos_begin', A] msg
+  // (meta_AD(label); meta_AD(len, more); AD(msg)).  When the whole record fits before the
+  // rate boundary its header bytes are known up front, so it is XORed in one pass; records
+  // that straddle a permutation take the byte-exact generic path.
+  const size_t rec = 2 + ln + 4 + 2 + msg_len;
+  if (ln > 64 || msg_len > 64 || msg_len > 0xffffffffu) {
+    for (size_t i = 0; i < n_msgs; i++) append_message(label, ln, msgs + i * msg_len, msg_len);
+    return;
+  }
+  uint8_t r[2 + 64 + 4 + 2 + 64];
+  std::memcpy(r + 2, label, ln);
+  r[1] = FLAG_M | FLAG_A;
+  r[2 + ln + 0] = (uint8_t)msg_len;
+  r[2 + ln + 1] = (uint8_t)(msg_len >> 8);
+  r[2 + ln + 2] = (uint8_t)(msg_len >> 16);
+  r[2 + ln + 3] = (uint8_t)(msg_len >> 24);
+  r[2 + ln + 5] = FLAG_A;
+  for (size_t i = 0; i < n_msgs; i++) {
+    const uint8_t *m = msgs + i * msg_len;
+    if (!s_.append_record_fast(r, rec, ln, m, msg_len)) append_message(label, ln, m, msg_len);
+  }
+}
+
+bool Strobe128::append_record_fast(uint8_t *r, size_t rec, size_t ln, const uint8_t *msg,
+                                   size_t msg_len) {
+  if ((size_t)pos_ + rec > STROBE_R) return false;
+  const uint8_t p0 = pos_;
+  r[0] = pos_begin_;                 // meta_AD(label): [old pos_begin, flags]
+  r[2 + ln + 4] = (uint8_t)(p0 + 1);  // AD(msg): old pos_begin = the one meta_AD set
+  std::memcpy(r + 2 + ln + 6, msg, msg_len);
+  uint8_t *b = bytes() + p0;
+  for (size_t i = 0; i < rec; i++) b[i] ^= r[i];
+  pos_ = (uint8_t)(p0 + rec);
+  pos_begin_ = (uint8_t)(p0 + 2 + ln + 4 + 1);  // AD begin_op: pos + 1 at its header
+  cur_flags_ = FLAG_A;
+  if (pos_ == STROBE_R) run_f();
+  return true;
 }
 
 void Transcript::challenge_bytes(const uint8_t *label, size_t ln, uint8_t *dst, size_t n) {

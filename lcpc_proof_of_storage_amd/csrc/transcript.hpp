@@ -22,6 +22,9 @@ class Strobe128 {
   void meta_ad(const uint8_t *d, size_t n, bool more);
   void ad(const uint8_t *d, size_t n, bool more);
   void prf(uint8_t *d, size_t n, bool more);
+  // meta_AD(label); meta_AD(len, more); AD(msg) in one XOR pass when the record fits before the
+  // rate boundary (r = prepared record with label/len/flag bytes filled in); false otherwise
+  bool append_record_fast(uint8_t *r, size_t rec, size_t ln, const uint8_t *msg, size_t msg_len);
 
  private:
   void run_f();

@@ -1,0 +1,142 @@
+// nttbench.hip -- A/B harness for NTT pass variants on gfx950 (one process, interleaved
+// rounds; outputs checked bit-for-bit against the v1 kernels, which the GPU parity tests pin
+// to the CPU oracle).  Usage: ./nttbench [log_n] [rows]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "ntt_v1.hpp"
+
+using namespace lcpc;
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t e = (x);                                                       \
+    if (e != hipSuccess) {                                                    \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+template <class F>
+__global__ void k_fill(uint32_t *p, size_t n, uint32_t seed) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t x = (uint32_t)i * 0x9E3779B9u ^ seed;
+  x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
+  p[i] = ((i % F::N) == F::N - 1) ? (x & 0x0fffffffu) : x;  // < p for every field
+}
+
+struct Variant {
+  std::string name;
+  std::function<void(const uint32_t *, uint32_t *, hipStream_t)> run;
+};
+
+template <class F>
+void bench(const char *fname, int log_n, size_t rows) {
+  const size_t n = (size_t)1 << log_n, np = n / 2;
+  const size_t W = F::N;
+  uint32_t *coeffs, *ref, *out, *tw;
+  CK(hipMalloc(&coeffs, rows * np * W * 4));
+  CK(hipMalloc(&ref, rows * n * W * 4));
+  CK(hipMalloc(&out, rows * n * W * 4));
+  CK(hipMalloc(&tw, n * W * 4));
+  hipLaunchKernelGGL(k_fill<F>, dim3((rows * np * W + 255) / 256), dim3(256), 0, 0, coeffs, rows * np * W, 12345u);
+  hipLaunchKernelGGL((ntt_detail::k_tw_table<F>), dim3((n + 255) / 256), dim3(256), 0, 0, tw, log_n, 0);
+  CK(hipDeviceSynchronize());
+  NttPlan plan;
+  plan.fid = F::ID; plan.log_n = log_n; plan.l1 = log_n / 2; plan.l2 = log_n - plan.l1; plan.d_tw = tw;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  CK(ntt_v1::ntt_rows_v1<F>(plan, coeffs, np, np, ref, n, rows, s));
+  CK(hipStreamSynchronize(s));
+
+  std::vector<Variant> vs;
+  vs.push_back({"product (ntt_rows_t)", [&](const uint32_t *c, uint32_t *o, hipStream_t st) {
+                  CK(ntt_detail::ntt_rows_t<F>(plan, c, np, np, o, n, rows, st));
+                }});
+  vs.push_back({"v1 (256thr, 3 LDS trips)", [&](const uint32_t *c, uint32_t *o, hipStream_t st) {
+                  CK(ntt_v1::ntt_rows_v1<F>(plan, c, np, np, o, n, rows, st));
+                }});
+#define V2(LA, CWA, TA, LB, CWB, TB)                                                           \
+  vs.push_back({"v2 A(S=2^" #LA ",CW=2^" #CWA ",T=2^" #TA ") B(S=2^" #LB ",CW=2^" #CWB ",T=2^" #TB ")", \
+                [&](const uint32_t *c, uint32_t *o, hipStream_t st) {                          \
+                  CK((ntt_v2::launch_a<F, LA, CWA, TA, true>(c, np, np, o, n, tw, log_n, rows, st))); \
+                  CK((ntt_v2::launch_b<F, LB, CWB, TB>(o, n, tw, log_n, rows, st)));           \
+                }});
+  if constexpr (F::ID == 1) {
+    if (log_n == 16) {
+      V2(8, 3, 8, 8, 3, 8)
+      V2(8, 2, 7, 8, 2, 7)
+      V2(8, 2, 8, 8, 2, 8)
+      V2(8, 3, 9, 8, 3, 9)
+      V2(8, 1, 7, 8, 1, 7)
+      V2(8, 4, 9, 8, 3, 8)
+      V2(8, 3, 8, 8, 4, 9)
+      V2(7, 3, 7, 9, 2, 8)
+      V2(7, 4, 8, 9, 2, 8)
+      V2(6, 4, 7, 10, 1, 8)
+    } else if (log_n == 14) {
+      V2(7, 3, 7, 7, 3, 7)
+      V2(7, 4, 8, 7, 4, 8)
+      V2(7, 2, 6, 7, 2, 6)
+    }
+  } else if constexpr (F::ID == 0) {
+    V2(8, 4, 8, 8, 4, 8)
+    V2(8, 3, 8, 8, 3, 8)
+    V2(8, 4, 9, 8, 4, 9)
+    V2(8, 5, 9, 8, 5, 9)
+    V2(8, 3, 7, 8, 3, 7)
+  } else {
+    V2(8, 2, 8, 9, 1, 8)
+    V2(8, 3, 8, 9, 2, 8)
+    V2(8, 2, 7, 9, 1, 7)
+    V2(8, 1, 7, 9, 1, 8)
+    V2(8, 3, 9, 9, 2, 9)
+  }
+  std::vector<uint32_t> h_ref(rows * n * W), h_out(rows * n * W);
+  CK(hipMemcpy(h_ref.data(), ref, h_ref.size() * 4, hipMemcpyDeviceToHost));
+  std::vector<std::vector<float>> times(vs.size());
+  std::vector<bool> ok(vs.size(), true);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (size_t i = 0; i < vs.size(); i++) {  // correctness
+    CK(hipMemset(out, 0, rows * n * W * 4));
+    vs[i].run(coeffs, out, s);
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(h_out.data(), out, h_out.size() * 4, hipMemcpyDeviceToHost));
+    ok[i] = h_out == h_ref;
+  }
+  for (int round = 0; round < 7; round++)
+    for (size_t i = 0; i < vs.size(); i++) {
+      CK(hipEventRecord(a, s));
+      vs[i].run(coeffs, out, s);
+      CK(hipEventRecord(b, s));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      if (round > 0) times[i].push_back(ms);
+    }
+  const double bytes = (double)rows * (np + n) * W * 4;
+  printf("%s log_n=%d rows=%zu  algorithmic bytes %.1f MiB\n", fname, log_n, rows, bytes / 1048576);
+  for (size_t i = 0; i < vs.size(); i++) {
+    auto t = times[i];
+    std::sort(t.begin(), t.end());
+    printf("%-52s %s  median %.3f ms  min %.3f ms  (%.0f GB/s algorithmic)\n", vs[i].name.c_str(),
+           ok[i] ? "OK " : "BAD", t[t.size() / 2], t[0], bytes / (t[t.size() / 2] * 1e-3) / 1e9);
+  }
+}
+
+int main(int argc, char **argv) {
+  const int which = argc > 1 ? atoi(argv[1]) : 1;
+  if (which == 1) { bench<Ft127>("Ft127", 16, 512); bench<Ft127>("Ft127", 14, 128); }
+  if (which == 0) bench<Ft63>("Ft63", 16, 512);
+  if (which == 3) bench<Ft255>("Ft255", 17, 256);
+  return 0;
+}
