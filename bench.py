@@ -49,17 +49,60 @@ def parse():
     return ap.parse_args()
 
 
+# ---------------------------------------------------------------- multi-process plumbing
+def dist_env():
+    """(rank, local_rank, world) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def init_dist(world, local_rank, backend="nccl"):
+    """One process per GPU; returns torch.distributed or None at N = 1 (RCCL is "nccl")."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    if backend == "nccl":
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        dist.init_process_group(backend=backend)
+    return dist
+
+
+def sync_barrier(dist, device_sync=None):
+    """barrier over ranks, then drain this rank's device (both sides of the timed region)."""
+    if dist is not None:
+        dist.barrier()
+    if device_sync is not None:
+        device_sync()
+
+
+def max_over_ranks(dist, x, device="cpu"):
+    """The job's wall time is its slowest rank's."""
+    if dist is None:
+        return float(x)
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def replica_seed(rank):
+    """Each replica commits its own polynomial (independent objects, no data-path collective)."""
+    return SEED + rank
+
+
+def job_throughput(n_per_step, steps, world, elapsed):
+    """Whole-job rate: the units all ranks processed / the max-over-ranks time."""
+    return n_per_step * steps * world / elapsed
+
+
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank, local_rank, world = dist_env()
     import torch
 
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+    dist = init_dist(world, local_rank)
     torch.cuda.set_device(local_rank)
 
     import lcpc_proof_of_storage_amd as L
@@ -74,7 +117,7 @@ def main():
     nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
 
     # synthetic inputs (host RNG of the product library), then resident in HBM
-    coeffs = L.field_random(fid, n, SEED + rank)
+    coeffs = L.field_random(fid, n, replica_seed(rank))
     outer = L.field_random(fid, n_rows, 7)  # prove accepts any outer tensor of n_rows elements
     d_coeffs = torch.from_numpy(coeffs.view(np.int64)).to(f"cuda:{local_rank}")
     torch.cuda.synchronize()
@@ -94,9 +137,7 @@ def main():
     warmup_done = warm_each * n_workers                # staging and pool blocks first
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
+        sync_barrier(dist, torch.cuda.synchronize)
 
     lock = threading.Lock()
     todo = [args.steps]
@@ -156,13 +197,8 @@ def main():
             step()
         L.prof_enable(False)
         iso = L.prof_stats()
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    total_elems = n * args.steps * world
-    value = total_elems / elapsed
+    elapsed = max_over_ranks(dist, elapsed, f"cuda:{local_rank}")
+    value = job_throughput(n, args.steps, world, elapsed)
     B = 8 * nl
     out = {
         "metric": "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU",

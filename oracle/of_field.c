@@ -240,7 +240,13 @@ void of_inv(int fid, const uint64_t *a, uint64_t *out) {
   const of_field *f = of_get_field(fid);
   uint64_t e[OF_MAXL];
   memcpy(e, f->p, sizeof(e));
-  e[0] -= 2; /* p - 2, p odd and > 2 */
+  /* p - 2 with borrow: Ft253_192's low limb is exactly 1 */
+  uint64_t borrow = 2;
+  for (int i = 0; i < f->nl && borrow; i++) {
+    const uint64_t prev = e[i];
+    e[i] = prev - borrow;
+    borrow = prev < borrow ? 1 : 0;
+  }
   of_mont_pow_big(f, a, e, f->nl, out);
 }
 

@@ -111,7 +111,7 @@ def test_field_constants_and_arith(oracle, fid):
     m = oracle.to_mont(fid, vals)
     assert oracle.ints_from_limbs(m, f.nl) == [f.to_mont(v) for v in vals]
     assert oracle.from_mont(fid, m) == vals
-    prod = oracle.mul(fid, m, m[::-1].reshape(-1, f.nl)[::-1].reshape(-1).copy())
+    prod = oracle.mul(fid, m, m.copy())
     assert oracle.from_mont(fid, prod) == [v * v % f.p for v in vals]
 
 
