@@ -14,8 +14,9 @@
  *     lcpc_last_error() returns a thread-local message;
  *   - "host" pointers are caller-owned CPU memory; "device" pointers are HIP device memory
  *     of the current device; handles own their device buffers;
- *   - a handle may be used from several threads; calls on one handle are serialized
- *     internally (one HIP stream per handle).
+ *   - handles may be used from several threads: each call leases a HIP stream from a
+ *     per-device pool (prove/verify from a high-priority pool), so independent calls, e.g.
+ *     commitments of different objects, overlap on the device.
  * No torch / HIP types appear in the signatures; `void *stream` is an optional hipStream_t.
  */
 #ifndef LCPC_MI_H
@@ -126,9 +127,10 @@ lcpc_status lcpc_encode(const lcpc_encoding *e, uint64_t *inp, size_t len);
 /* Batched encode of n_rows host rows (row r at rows + r * row_stride limbs-elements). */
 lcpc_status lcpc_encode_rows(const lcpc_encoding *e, uint64_t *rows, size_t n_rows,
                              size_t row_stride);
-/* Device batched encode: row r reads n_valid <= n_per_row... coefficients at
- * d_src + r * src_stride (elements), the rest of the row zero, and writes n_cols encoded
- * elements at d_dst + r * dst_stride.  Asynchronous on `stream` (NULL: the handle stream). */
+/* Device batched encode: row r reads n_valid (<= n_cols) coefficients at
+ * d_src + r * src_stride (elements), treats the rest of the row as zero, and writes n_cols
+ * encoded elements at d_dst + r * dst_stride (>= n_cols).  Asynchronous on `stream`; with
+ * stream == NULL it runs on a pooled stream and returns when the rows are written. */
 lcpc_status lcpc_encode_rows_device(const lcpc_encoding *e, const void *d_src, size_t src_stride,
                                     size_t n_valid, void *d_dst, size_t dst_stride,
                                     size_t n_rows, void *stream);

@@ -28,8 +28,12 @@ void ntt_plan_free(NttPlan &p);
 // rows r in [0, n_rows): in = src + r * src_stride (elements), n_valid leading elements
 // (rest zero); out = dst + r * dst_stride (n elements).  src may alias dst only if
 // src_stride == dst_stride and n_valid == n (in-place full-length transform).
+// copy (optional): the n_valid input coefficients of row r are also written to
+// copy + r * copy_stride by the first pass, which reads them anyway (commit keeps its own
+// coefficient matrix without a separate device-to-device copy).
 hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
-                    uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s);
+                    uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s,
+                    uint32_t *copy = nullptr, size_t copy_stride = 0);
 
 // ------------------------------------------------------------------ BLAKE3 / Merkle
 // leaf[j] = BLAKE3(32 zero bytes || repr(m[0][j]) || ... || repr(m[n_rows-1][j]))

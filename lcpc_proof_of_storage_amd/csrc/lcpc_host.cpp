@@ -83,7 +83,26 @@ struct Device {
 
   // high-priority streams carry the prover's short latency-critical kernels (row
   // combinations, conversions, gathers) ahead of other commitments' bulk encode work
+  hipStream_t shared_stream = nullptr;  // LCPC_STREAM_MODE=serial: every call on one stream
+
+  static bool serial_mode() {
+    static const bool v = [] {
+      const char *m = getenv("LCPC_STREAM_MODE");
+      return m && std::string(m) == "serial";
+    }();
+    return v;
+  }
+
   hipStream_t acquire_stream(bool high) {
+    if (serial_mode()) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!shared_stream) {
+        (void)hipSetDevice(id);
+        if (hipStreamCreateWithFlags(&shared_stream, hipStreamNonBlocking) != hipSuccess)
+          shared_stream = nullptr;
+      }
+      return shared_stream;
+    }
     {
       std::lock_guard<std::mutex> lk(mu);
       auto &pool = idle_streams[high ? 1 : 0];
@@ -106,6 +125,7 @@ struct Device {
     return s;
   }
   void release_stream(hipStream_t s, bool high) {
+    if (serial_mode()) return;
     std::lock_guard<std::mutex> lk(mu);
     idle_streams[high ? 1 : 0].push_back(s);
   }
@@ -425,15 +445,31 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   c->n_cols = nc;
   c->n_per_row = np;
   c->n_hashes = 2 * np2 - 1;
-  // coeffs, zero padded to n_rows * n_per_row (:665, :669-674)
+  // coeffs, zero padded to n_rows * n_per_row (:665, :669-674); comm row r = fft_io(coeffs
+  // row r || zeros) (:677-682)
   HIP_TRY(c->coeffs.alloc(dev, n_rows * np * wb));
-  HIP_TRY(hipMemcpyAsync(c->coeffs.p, d_src, len * wb,
-                         src_is_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
-  if (n_rows * np > len)
-    HIP_TRY(hipMemsetAsync(c->coeffs.as<uint8_t>() + len * wb, 0, (n_rows * np - len) * wb, s));
-  // encode every row (:677-682): row r of comm = fft_io(coeffs row r || zeros)
   HIP_TRY(c->comm.alloc(dev, n_rows * nc * wb));
-  HIP_TRY(ntt_rows(e->plan, c->coeffs.as<uint32_t>(), np, np, c->comm.as<uint32_t>(), nc, n_rows, s));
+  uint8_t *cf = c->coeffs.as<uint8_t>();
+  uint8_t *cm = c->comm.as<uint8_t>();
+  if (src_is_host) {
+    HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb, hipMemcpyHostToDevice, s));
+    if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
+    HIP_TRY(ntt_rows(e->plan, (const uint32_t *)cf, np, np, (uint32_t *)cm, nc, n_rows, s));
+  } else {
+    // full rows are encoded straight from the caller's buffer; the first NTT pass writes the
+    // commitment's own coefficient copy as it reads them (no separate D2D copy)
+    const size_t full = len / np, tail = len - full * np;
+    HIP_TRY(ntt_rows(e->plan, (const uint32_t *)d_src, np, np, (uint32_t *)cm, nc, full, s,
+                     (uint32_t *)cf, np));
+    if (tail) {
+      uint8_t *last = cf + full * np * wb;
+      HIP_TRY(hipMemcpyAsync(last, (const uint8_t *)d_src + full * np * wb, tail * wb,
+                             hipMemcpyDeviceToDevice, s));
+      HIP_TRY(hipMemsetAsync(last + tail * wb, 0, (np - tail) * wb, s));
+      HIP_TRY(ntt_rows(e->plan, (const uint32_t *)last, np, np, (uint32_t *)(cm + full * nc * wb),
+                       nc, 1, s));
+    }
+  }
   // Merkle tree (:685-697, merkleize :720-734); leaves past n_cols stay zero digests
   HIP_TRY(c->hashes.alloc(dev, c->n_hashes * 32));
   if (np2 > nc) HIP_TRY(hipMemsetAsync(c->hashes.as<uint8_t>() + nc * 32, 0, (np2 - nc) * 32, s));

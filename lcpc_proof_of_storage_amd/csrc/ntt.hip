@@ -6,7 +6,7 @@ namespace lcpc {
 
 #define DECL(n)                                                                                   \
   hipError_t ntt_rows_##n(const NttPlan &, const uint32_t *, size_t, size_t, uint32_t *, size_t, \
-                          size_t, hipStream_t);                                                   \
+                          size_t, hipStream_t, uint32_t *, size_t);                               \
   hipError_t ntt_tw_table_##n(uint32_t *, int, bool, hipStream_t);
 DECL(ft63)
 DECL(ft127)
@@ -46,12 +46,13 @@ void ntt_plan_free(NttPlan &p) {
 }
 
 hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
-                    uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s) {
+                    uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s, uint32_t *copy,
+                    size_t copy_stride) {
   switch (p.fid) {
-    case 0: return ntt_rows_ft63(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s);
-    case 1: return ntt_rows_ft127(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s);
-    case 3: return ntt_rows_ft255(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s);
-    case 4: return ntt_rows_ft253(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s);
+    case 0: return ntt_rows_ft63(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride);
+    case 1: return ntt_rows_ft127(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride);
+    case 3: return ntt_rows_ft255(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride);
+    case 4: return ntt_rows_ft253(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride);
     default: return hipErrorInvalidValue;
   }
 }

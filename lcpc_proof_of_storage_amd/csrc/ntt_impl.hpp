@@ -53,14 +53,22 @@ __global__ __launch_bounds__(NTHREADS) void k_ntt_small(const uint32_t *__restri
                                                         uint32_t *__restrict__ dst,
                                                         size_t dst_stride,
                                                         const uint32_t *__restrict__ twn,
-                                                        int log_n) {
+                                                        int log_n, uint32_t *__restrict__ copy,
+                                                        size_t copy_stride) {
   __shared__ __align__(16) uint32_t smem[4096 * F::N];
   Fe<F> *buf = reinterpret_cast<Fe<F> *>(smem);
   const size_t row = blockIdx.x;
   const int n = 1 << log_n;
   const uint32_t *in = src + row * src_stride * F::N;
-  for (int i = threadIdx.x; i < n; i += NTHREADS)
-    buf[i] = (size_t)i < n_valid ? fe_load<F>(in, i) : fe_zero<F>();
+  uint32_t *cp = copy ? copy + row * copy_stride * F::N : nullptr;
+  for (int i = threadIdx.x; i < n; i += NTHREADS) {
+    if ((size_t)i < n_valid) {
+      buf[i] = fe_load<F>(in, i);
+      if (cp) fe_store<F>(cp, i, buf[i]);
+    } else {
+      buf[i] = fe_zero<F>();
+    }
+  }
   for (int gap = n / 2; gap > 0; gap /= 2) {
     __syncthreads();
     const int nchunks = n / (2 * gap);
@@ -120,16 +128,22 @@ hipError_t dispatch_logs(int l, Fn &&fn) {
 
 template <class F>
 hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst,
-                      size_t ds, size_t n_rows, hipStream_t s) {
+                      size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
   if (n_rows == 0) return hipSuccess;
   if (p.log_n == 0) {  // length-1 transform is the identity (fffft returns early)
-    return hipMemcpy2DAsync(dst, ds * F::N * 4, src, ss * F::N * 4, nv ? F::N * 4 : 0, n_rows,
+    if (cp && nv) {
+      hipError_t e = hipMemcpy2DAsync(cp, cs * F::N * 4, src, ss * F::N * 4, F::N * 4, n_rows,
+                                      hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return e;
+    }
+    if (!nv) return hipMemset2DAsync(dst, ds * F::N * 4, 0, F::N * 4, n_rows, s);
+    return hipMemcpy2DAsync(dst, ds * F::N * 4, src, ss * F::N * 4, F::N * 4, n_rows,
                             hipMemcpyDeviceToDevice, s);
   }
   if (p.log_n <= 12) {
     prof::Scope ps("ntt_small", s);
     hipLaunchKernelGGL((k_ntt_small<F>), dim3(n_rows), dim3(NTHREADS), 0, s, src, ss, nv, dst, ds,
-                       p.d_tw, p.log_n);
+                       p.d_tw, p.log_n, cp, cs);
     return hipGetLastError();
   }
   constexpr int R = Shape<F>::R, E = Shape<F>::E;
@@ -139,8 +153,8 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
     constexpr int CW = log_cw<L, E>();
     constexpr int T = L + CW - R;
     if (halfz)
-      return ntt_v2::launch_a<F, L, CW, T, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s);
-    return ntt_v2::launch_a<F, L, CW, T, false>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s);
+      return ntt_v2::launch_a<F, L, CW, T, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs);
+    return ntt_v2::launch_a<F, L, CW, T, false>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs);
   });
   if (e != hipSuccess) return e;
   return dispatch_logs<F, 7, HI>(p.l2, [&]<int L>() {

@@ -97,7 +97,8 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
                                                        uint32_t *__restrict__ dst,
                                                        size_t dst_stride,
                                                        const uint32_t *__restrict__ twn,
-                                                       int log_n) {
+                                                       int log_n, uint32_t *__restrict__ copy,
+                                                       size_t copy_stride) {
   constexpr int S = 1 << LOG_S, CW = 1 << LOG_CW, LD = CW > 1 ? CW + 1 : 1, T = 1 << LOG_T;
   constexpr int R = LOG_S + LOG_CW - LOG_T;
   static_assert(R >= 1 && R <= LOG_S, "tile / thread shape");
@@ -115,6 +116,7 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
 
   const uint32_t *in = src + row * src_stride * F::N;
   uint32_t *out = dst + row * dst_stride * F::N;
+  uint32_t *cp = copy ? copy + row * copy_stride * F::N : nullptr;
   // ---- round 0 straight from HBM (exactly one item per thread: ITEMS = CW * S / 2^R = T)
   {
     constexpr int RR = rr_of<LOG_S, R, 0>();
@@ -128,7 +130,12 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
         x[j] = fe_zero<F>();
       } else {
         const size_t pos = c + ((size_t)(q + j * GL) << log_m);
-        x[j] = pos < n_valid ? fe_load<F>(in, pos) : fe_zero<F>();
+        if (pos < n_valid) {
+          x[j] = fe_load<F>(in, pos);
+          if (cp) fe_store<F>(cp, pos, x[j]);  // coalesced: lanes = adjacent columns
+        } else {
+          x[j] = fe_zero<F>();
+        }
       }
     }
     __syncthreads();  // twiddle table
@@ -215,11 +222,12 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_b(uint32_t *__restrict__ da
 
 template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ>
 hipError_t launch_a(const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
-                    const uint32_t *tw, int log_n, size_t n_rows, hipStream_t s) {
+                    const uint32_t *tw, int log_n, size_t n_rows, hipStream_t s, uint32_t *cp,
+                    size_t cs) {
   const size_t groups = (size_t)1 << (log_n - LOG_S - LOG_CW);
   prof::Scope ps("ntt_pass_a", s);
   hipLaunchKernelGGL((k_pass_a<F, LOG_S, LOG_CW, LOG_T, HALFZ>), dim3((unsigned)(n_rows * groups)),
-                     dim3(1 << LOG_T), 0, s, src, ss, nv, dst, ds, tw, log_n);
+                     dim3(1 << LOG_T), 0, s, src, ss, nv, dst, ds, tw, log_n, cp, cs);
   return hipGetLastError();
 }
 

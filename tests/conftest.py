@@ -28,3 +28,38 @@ def gpu():
     assert n > 0, "no HIP device visible: the -m gpu tests need an MI355X"
     L.set_device(0)
     return L
+
+
+class _HipMem:
+    """Raw device buffers through the HIP runtime liblcpc_mi.so itself links (tests only).
+
+    torch wheels bundle a second HIP runtime; initialising it after ours can fail, so the GPU
+    tests do not use torch for device memory."""
+
+    H2D, D2H = 1, 2
+
+    def __init__(self):
+        import ctypes as C
+        self.C = C
+        self.L = C.CDLL("libamdhip64.so.7")
+        self.L.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        self.L.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        self.L.hipFree.argtypes = [C.c_void_p]
+
+    def to_device(self, a):
+        p = self.C.c_void_p()
+        assert self.L.hipMalloc(self.C.byref(p), max(a.nbytes, 16)) == 0
+        assert self.L.hipMemcpy(p, a.ctypes.data, a.nbytes, self.H2D) == 0
+        return p.value
+
+    def to_host(self, ptr, out):
+        assert self.L.hipMemcpy(out.ctypes.data, ptr, out.nbytes, self.D2H) == 0
+        return out
+
+    def free(self, ptr):
+        self.L.hipFree(ptr)
+
+
+@pytest.fixture(scope="session")
+def hipmem(gpu):
+    return _HipMem()

@@ -53,7 +53,7 @@ def ligero_case(fid, log_len, rho=(1, 2), length=None, x_seed=7):
         "p_eval_sha256": sha(pf.p_eval),
         "p_random_sha256": sha(pf.p_random),
         "cols_sha256": sha(pf.cols),
-        "paths_sha256": sha(pf.paths),
+        "paths_sha256": sha(pf.paths.tobytes()),
         "col_idx": [int(v) for v in pf.col_idx],
         "eval": hex(O.from_mont(fid, ev)[0]),
     }

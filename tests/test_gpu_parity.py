@@ -84,6 +84,36 @@ def test_commit_matches_oracle(gpu, oracle, fid, n_per_row, n_cols, length):
     assert g.get_root() == o.root()
 
 
+@pytest.mark.parametrize("fid,n_per_row,n_cols,length", [
+    (1, 2048, 4096, 1 << 16),          # small-row kernel
+    (0, 100, 256, 3000),               # ragged, small-row kernel
+    (1, 1, 2, 5),
+    (1, 8192, 16384, 128 * 8192),      # two-pass kernels, fused coefficient copy
+    (1, 8192, 16384, 100 * 8192 + 77), # two-pass, ragged last row
+    (0, 8192, 16384, 5000),            # two-pass, a single partial row (no full rows)
+    (3, 2048, 8192, 3 * 2048 + 1),     # two-pass Ft255, rate 1/4
+])
+def test_commit_device_matches_oracle(gpu, oracle, hipmem, fid, n_per_row, n_cols, length):
+    """lcpc_commit_new_device: coefficients already in HBM (bench path); the commitment's own
+    coefficient matrix is written by the first NTT pass."""
+    coeffs = rand_elems(oracle, fid, length, 13)
+    g_enc = gpu.RsEncoding.new(fid, n_per_row, n_cols, 16, 2)
+    o_enc = oracle.Encoding.ligero(fid, n_per_row, n_cols, 16, 2)
+    d = hipmem.to_device(coeffs)
+    try:
+        g = gpu.LcCommit.commit_device(d, length, g_enc)
+        o = oracle.Commit(o_enc, coeffs)
+        assert np.array_equal(g.coeffs.reshape(-1), o.coeffs)
+        assert np.array_equal(g.comm.reshape(-1), o.comm)
+        assert g.hashes == o.hashes
+        assert g.get_root() == o.root()
+        # the caller's buffer is only read
+        assert np.array_equal(hipmem.to_host(d, np.zeros_like(coeffs)), coeffs)
+        del g
+    finally:
+        hipmem.free(d)
+
+
 @pytest.mark.parametrize("fid,n_per_row,n_cols,length,nco,ndt", [
     (1, 2048, 4096, 1 << 16, 309, 2),
     (0, 100, 256, 3000, 128, 3),

@@ -66,7 +66,7 @@ void bench(const char *fname, int log_n, size_t rows) {
 #define V2(LA, CWA, TA, LB, CWB, TB)                                                           \
   vs.push_back({"v2 A(S=2^" #LA ",CW=2^" #CWA ",T=2^" #TA ") B(S=2^" #LB ",CW=2^" #CWB ",T=2^" #TB ")", \
                 [&](const uint32_t *c, uint32_t *o, hipStream_t st) {                          \
-                  CK((ntt_v2::launch_a<F, LA, CWA, TA, true>(c, np, np, o, n, tw, log_n, rows, st))); \
+                  CK((ntt_v2::launch_a<F, LA, CWA, TA, true>(c, np, np, o, n, tw, log_n, rows, st, nullptr, 0))); \
                   CK((ntt_v2::launch_b<F, LB, CWB, TB>(o, n, tw, log_n, rows, st)));           \
                 }});
   if constexpr (F::ID == 1) {

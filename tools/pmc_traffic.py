@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""HBM traffic of the encode kernels from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+    python tools/pmc_traffic.py gpurun_out/<tag> profiles/pmc_traffic.json [--len N --field F]
+
+Counter units are KiB.  Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): on gfx950
+FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced streaming read, so it is
+doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Both NTT passes load and
+store 16 B per lane for Ft127 (fe_load / fe_store of 4 x u32).
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+KERNELS = {"ntt_pass_a": "k_pass_a", "ntt_pass_b": "k_pass_b", "leaf_chunks": "k_leaf_chunks",
+           "collapse_partial": "k_collapse_partial"}
+
+
+def per_kernel(path):
+    acc = collections.defaultdict(list)
+    for row in csv.DictReader(open(path)):
+        for short, pat in KERNELS.items():
+            if pat in row["Kernel_Name"]:
+                acc[short].append(float(row["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run_dir")
+    ap.add_argument("out")
+    ap.add_argument("--len", type=int, default=1 << 24)
+    ap.add_argument("--field", default="Ft127")
+    a = ap.parse_args()
+    fpath = glob.glob(os.path.join(a.run_dir, "pmc_fetch", "*counter_collection.csv"))[0]
+    wpath = glob.glob(os.path.join(a.run_dir, "pmc_write", "*counter_collection.csv"))[0]
+    fetch, nf = per_kernel(fpath)
+    write, nw = per_kernel(wpath)
+    kern = {}
+    for k in fetch:
+        rd = 2.0 * fetch[k]
+        wr = write.get(k, 0.0)
+        kern[k] = {"fetch_bytes_raw": fetch[k], "read_bytes_corrected": rd, "write_bytes": wr,
+                   "hbm_bytes": rd + wr, "launches": nf[k]}
+    enc = kern["ntt_pass_a"]["hbm_bytes"] + kern["ntt_pass_b"]["hbm_bytes"]
+    out = {
+        "config_len": a.len, "field": a.field,
+        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
+                  "(bench.py --pipeline 1); FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> B",
+        "ntt_encode_bytes_per_launch": enc,
+        "kernels": kern,
+        "source": os.path.relpath(a.run_dir),
+    }
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps({k: round(v["hbm_bytes"] / 2**20, 1) for k, v in kern.items()}), "MiB;",
+          "encode", round(enc / 2**20, 1), "MiB")
+
+
+if __name__ == "__main__":
+    main()
