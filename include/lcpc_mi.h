@@ -111,6 +111,20 @@ lcpc_status lcpc_ligero_new_from_dims(lcpc_field f, size_t rho_num, size_t rho_d
  * (lcpc-2d/src/tests.rs:23-121: N_COL_OPENS = 128, 2 degree tests). */
 lcpc_status lcpc_rs_encoding_new(lcpc_field f, size_t n_per_row, size_t n_cols,
                                  size_t n_col_opens, size_t n_degree_tests, lcpc_encoding **out);
+/* Brakedown: SdigEncodingS<F, SdigCodeK> (lcpc-brakedown-pc/src/lib.rs:40-176), code = K in
+ * 1..6 (codespec.rs:169-232; the crate's default SdigEncoding is code 3).  The random expander
+ * matrices are matgen::generate(n_per_row, seed) (matgen.rs:28-52), drawn bit-exactly. */
+size_t lcpc_sdig_n_col_opens(int code);                       /* _n_col_opens :57-61 */
+/* the n_per_row SdigEncodingS::new would choose for `len` coefficients (:103-110, :69-99) */
+lcpc_status lcpc_sdig_get_n_per_row(lcpc_field f, int code, size_t len, size_t *n_per_row);
+lcpc_status lcpc_sdig_new(lcpc_field f, int code, size_t len, uint64_t seed,
+                          lcpc_encoding **out);                /* new :103-110 */
+lcpc_status lcpc_sdig_new_ml(lcpc_field f, int code, size_t n_vars, uint64_t seed,
+                             lcpc_encoding **out);             /* new_ml :114-123 */
+lcpc_status lcpc_sdig_new_from_dims(lcpc_field f, int code, size_t n_per_row, size_t n_cols,
+                                    uint64_t seed, lcpc_encoding **out); /* :126-137 */
+/* 0 = Reed-Solomon / fft_io (Ligero), 1 = SDIG expander code (Brakedown) */
+int lcpc_encoding_kind(const lcpc_encoding *e);
 void lcpc_encoding_free(lcpc_encoding *e);
 lcpc_field lcpc_encoding_field(const lcpc_encoding *e);
 /* LcEncoding::get_dims / dims_ok / get_n_col_opens / get_n_degree_tests (lib.rs:94-104) */
@@ -154,7 +168,10 @@ size_t lcpc_commit_n_hashes(const lcpc_commit *c);
 lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out);
 lcpc_status lcpc_commit_copy_coeffs(const lcpc_commit *c, uint64_t *out);
 lcpc_status lcpc_commit_copy_hashes(const lcpc_commit *c, uint8_t *out);
-/* device views (valid while the handle lives) */
+/* device views (valid while the handle lives).  The encoded matrix is row-major [n_rows][n_cols]
+ * for Ligero and element-major [n_cols][n_rows] for SDIG (lcpc_commit_col_major() == 1), where
+ * every Merkle leaf is one contiguous column; copy_comm always returns the row-major layout. */
+int lcpc_commit_col_major(const lcpc_commit *c);
 const void *lcpc_commit_device_comm(const lcpc_commit *c);
 const void *lcpc_commit_device_coeffs(const lcpc_commit *c);
 /* check_comm (:703-718) */

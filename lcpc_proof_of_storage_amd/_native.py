@@ -42,6 +42,12 @@ SIGNATURES = {
     "lcpc_ligero_new_ml": (i32, [i32, sz, sz, sz, C.POINTER(vp)]),
     "lcpc_ligero_new_from_dims": (i32, [i32, sz, sz, sz, sz, C.POINTER(vp)]),
     "lcpc_rs_encoding_new": (i32, [i32, sz, sz, sz, sz, C.POINTER(vp)]),
+    "lcpc_sdig_n_col_opens": (sz, [i32]),
+    "lcpc_sdig_get_n_per_row": (i32, [i32, i32, sz, szp]),
+    "lcpc_sdig_new": (i32, [i32, i32, sz, C.c_uint64, C.POINTER(vp)]),
+    "lcpc_sdig_new_ml": (i32, [i32, i32, sz, C.c_uint64, C.POINTER(vp)]),
+    "lcpc_sdig_new_from_dims": (i32, [i32, i32, sz, sz, C.c_uint64, C.POINTER(vp)]),
+    "lcpc_encoding_kind": (i32, [vp]),
     "lcpc_encoding_free": (None, [vp]),
     "lcpc_encoding_field": (i32, [vp]),
     "lcpc_encoding_get_dims": (None, [vp, sz, szp, szp, szp]),
@@ -64,6 +70,7 @@ SIGNATURES = {
     "lcpc_commit_copy_comm": (i32, [vp, u64p]),
     "lcpc_commit_copy_coeffs": (i32, [vp, u64p]),
     "lcpc_commit_copy_hashes": (i32, [vp, u8p]),
+    "lcpc_commit_col_major": (i32, [vp]),
     "lcpc_commit_device_comm": (vp, [vp]),
     "lcpc_commit_device_coeffs": (vp, [vp]),
     "lcpc_check_comm": (i32, [vp, vp]),

@@ -234,11 +234,12 @@ __global__ __launch_bounds__(256) void k_merkle(uint8_t *__restrict__ hashes, si
 template <class F>
 __global__ void k_gather_cols(const uint32_t *__restrict__ m, size_t n_rows, size_t n_cols,
                               const uint64_t *__restrict__ idx, size_t n_idx,
-                              uint32_t *__restrict__ cols) {
+                              uint32_t *__restrict__ cols, int col_major) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_idx * n_rows) return;
   const size_t k = t / n_rows, r = t % n_rows;
-  fe_store<F>(cols, t, fe_load<F>(m, r * n_cols + idx[k]));
+  const size_t at = col_major ? idx[k] * n_rows + r : r * n_cols + idx[k];
+  fe_store<F>(cols, t, fe_load<F>(m, at));
 }
 
 __global__ void k_gather_paths(const uint8_t *__restrict__ hashes, size_t np2,
@@ -348,13 +349,14 @@ hipError_t merkle_tree_io(const uint8_t *ins, size_t n_ins, uint8_t *outs, hipSt
 }
 
 hipError_t gather_columns(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
-                          const uint64_t *idx, size_t n_idx, uint32_t *cols, hipStream_t s) {
+                          const uint64_t *idx, size_t n_idx, uint32_t *cols, hipStream_t s,
+                          bool col_major) {
   const size_t n = n_idx * n_rows;
   if (!n) return hipSuccess;
   return dispatch_field(fid, [&]<class F>() {
     prof::Scope ps("gather_cols", s);
     hipLaunchKernelGGL((k_gather_cols<F>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, m,
-                       n_rows, n_cols, idx, n_idx, cols);
+                       n_rows, n_cols, idx, n_idx, cols, col_major ? 1 : 0);
     return hipGetLastError();
   });
 }

@@ -55,9 +55,11 @@ size_t collapse_scratch_bytes(int fid, size_t n_rows, size_t n_per_row, int n_te
 hipError_t collapse_rows(int fid, const uint32_t *coeffs, size_t n_rows, size_t n_per_row,
                          const uint32_t *tensors, int n_tensors, uint32_t *out, void *scratch,
                          hipStream_t s);
-// cols[k][r] = m[r][idx[k]]; paths[k][i] = sibling digests of leaf idx[k]
+// cols[k][r] = m[r][idx[k]] (m row-major) or m[idx[k]][r] (col_major);
+// paths[k][i] = sibling digests of leaf idx[k]
 hipError_t gather_columns(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
-                          const uint64_t *idx, size_t n_idx, uint32_t *cols, hipStream_t s);
+                          const uint64_t *idx, size_t n_idx, uint32_t *cols, hipStream_t s,
+                          bool col_major = false);
 hipError_t gather_paths(const uint8_t *hashes, size_t n_hashes, const uint64_t *idx,
                         size_t n_idx, size_t path_len, uint8_t *paths, hipStream_t s);
 

@@ -22,6 +22,7 @@
 #include "field.hpp"
 #include "kernels.hpp"
 #include "prof.hpp"
+#include "sdig.hpp"
 #include "transcript.hpp"
 
 using namespace lcpc;
@@ -299,18 +300,24 @@ size_t log2_np2(size_t v) {  // lcpc-2d log2 (:857-859)
 }  // namespace
 
 // ---------------------------------------------------------------- handles
+enum { KIND_RS = 0, KIND_SDIG = 1 };
+
 struct lcpc_encoding {
   int fid = 1;
-  int kind = 0;  // 0 = R-S / fft_io
+  int kind = KIND_RS;  // R-S / fft_io (Ligero) or SDIG expander code (Brakedown)
+  int code = 0;        // SdigCode id
+  uint64_t seed = 0;
   size_t n_per_row = 0, n_cols = 0, n_col_opens = 0, n_degree_tests = 0;
   Device *dev = nullptr;
   NttPlan plan;
+  SdigPlan sdig;
   ~lcpc_encoding() {
     if (dev) {
       Lease lease(dev);
       (void)hipSetDevice(dev->id);
       (void)hipStreamSynchronize(lease.s);
       ntt_plan_free(plan);
+      sdig_plan_free(sdig);
     }
   }
 };
@@ -319,6 +326,7 @@ struct lcpc_commit {
   int fid = 1;
   Device *dev = nullptr;
   size_t n_rows = 0, n_cols = 0, n_per_row = 0, n_hashes = 0;
+  bool col_major = false;  // comm stored [n_cols][n_rows] (SDIG) instead of [n_rows][n_cols]
   DBuf coeffs, comm, hashes;
   uint8_t root[32];
 };
@@ -339,6 +347,10 @@ struct lcpc_transcript {
 namespace {
 
 lcpc_status encoding_dims_ok(const lcpc_encoding *e, size_t n_per_row, size_t n_cols) {
+  if (e->kind == KIND_SDIG)  // SdigEncodingS::dims_ok (lcpc-brakedown-pc/src/lib.rs:157-164)
+    return (n_per_row < n_cols && n_per_row == e->n_per_row && n_cols == e->n_cols)
+               ? LCPC_OK
+               : LCPC_ERR_INVALID_ARG;
   // LigeroEncodingRho::dims_ok (lcpc-ligero-pc/src/lib.rs:171-177)
   const bool pow = n_cols && !(n_cols & (n_cols - 1));
   return (n_per_row < n_cols && pow && n_per_row == e->n_per_row && n_cols == e->n_cols) ? LCPC_OK
@@ -373,6 +385,68 @@ lcpc_status make_rs_encoding(int fid, size_t n_per_row, size_t n_cols, size_t nc
   HIP_TRY(hipStreamSynchronize(lease.s));
   e->dev = dev;
   *out = e.release();
+  return LCPC_OK;
+}
+
+// SdigEncodingS::_new_from_np1 / new_from_dims (lcpc-brakedown-pc/src/lib.rs:69-137) with the
+// n_per_row already chosen; want_cols = 0 accepts the generated codeword length.
+lcpc_status make_sdig_encoding(int fid, int code, size_t n_per_row, size_t want_cols, uint64_t seed,
+                               lcpc_encoding **out) {
+  if (!out) return fail(LCPC_ERR_INVALID_ARG, "null out");
+  if (!valid_field(fid)) return fail(LCPC_ERR_INVALID_ARG, "unknown field");
+  if (!field_gpu_supported(fid)) return fail(LCPC_ERR_UNSUPPORTED, "field has no gfx950 kernels");
+  const SdigSpec *sp = sdig_spec(code);
+  if (!sp) return fail(LCPC_ERR_INVALID_ARG, "SDIG code id must be 1..6");
+  if (!(n_per_row > sp->blen))  // matgen::get_dims asserts n > baselen
+    return fail(LCPC_ERR_INVALID_ARG, "SDIG: n_per_row must exceed the code's base length");
+  if (n_per_row > 0xffffffffu) return fail(LCPC_ERR_INVALID_ARG, "SDIG: n_per_row too large");
+  lcpc_status st;
+  Device *dev = get_device(g_device, &st);
+  if (!dev) return st;
+  const FieldInfo fi = field_info(fid);
+  std::vector<CsrHost> pre, post;
+  if (!sdig_generate(fi.limbs, fi.num_bits, fi.p, code, n_per_row, seed, pre, post))
+    return fail(LCPC_ERR_INVALID_ARG, "SDIG: matrix generation failed");
+  const size_t nc = sdig_codeword_length(pre, post);
+  if (want_cols && want_cols != nc)  // new_from_dims asserts n_cols == codeword_length
+    return fail(LCPC_ERR_INVALID_ARG, "SDIG: n_cols does not match the code's codeword length");
+  auto e = std::make_unique<lcpc_encoding>();
+  e->fid = fid;
+  e->kind = KIND_SDIG;
+  e->code = code;
+  e->seed = seed;
+  e->n_per_row = n_per_row;
+  e->n_cols = nc;
+  e->n_col_opens = sdig_n_col_opens(code);
+  e->n_degree_tests = lcpc_n_degree_tests(128, nc, fi.num_bits - 1);
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  HIP_TRY(sdig_plan_upload(e->sdig, fid, pre, post, lease.s));
+  e->dev = dev;
+  *out = e.release();
+  return LCPC_OK;
+}
+
+// Encode n_rows row-major rows: row r reads n_valid leading coefficients at src + r * ss (the
+// rest of its message zero) and writes n_cols elements at dst + r * ds.  Runs on stream s
+// (normally the caller's lease); scratch comes from the pool.
+lcpc_status encode_rows_any(const lcpc_encoding *e, const uint32_t *src, size_t ss, size_t nv,
+                            uint32_t *dst, size_t ds, size_t n_rows, hipStream_t s) {
+  if (n_rows == 0) return LCPC_OK;
+  if (e->kind == KIND_RS) {
+    HIP_TRY(ntt_rows(e->plan, src, ss, nv, dst, ds, n_rows, s));
+    return LCPC_OK;
+  }
+  // SDIG: element-major working codeword, then back to rows
+  const size_t nc = e->n_cols, np = e->n_per_row;
+  const int wb = field_bytes(e->fid);
+  DBuf cw, tmp;
+  HIP_TRY(cw.alloc(e->dev, nc * n_rows * wb));
+  HIP_TRY(tmp.alloc(e->dev, e->sdig.tmp_elems * n_rows * wb));
+  HIP_TRY(transpose_elems(e->fid, src, n_rows, np, ss, nv < np ? nv : np, cw.as<uint32_t>(), n_rows, s));
+  HIP_TRY(sdig_encode_cm(e->sdig, cw.as<uint32_t>(), n_rows, tmp.as<uint32_t>(), s));
+  HIP_TRY(transpose_elems(e->fid, cw.as<uint32_t>(), nc, n_rows, n_rows, n_rows, dst, ds, s));
+  HIP_TRY(hipStreamSynchronize(s));  // before the pool reuses cw / tmp
   return LCPC_OK;
 }
 
@@ -445,13 +519,24 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   c->n_cols = nc;
   c->n_per_row = np;
   c->n_hashes = 2 * np2 - 1;
-  // coeffs, zero padded to n_rows * n_per_row (:665, :669-674); comm row r = fft_io(coeffs
+  // coeffs, zero padded to n_rows * n_per_row (:665, :669-674); comm row r = encode(coeffs
   // row r || zeros) (:677-682)
   HIP_TRY(c->coeffs.alloc(dev, n_rows * np * wb));
   HIP_TRY(c->comm.alloc(dev, n_rows * nc * wb));
   uint8_t *cf = c->coeffs.as<uint8_t>();
   uint8_t *cm = c->comm.as<uint8_t>();
-  if (src_is_host) {
+  if (e->kind == KIND_SDIG) {
+    // element-major codeword [n_cols][n_rows]: the message part is the coefficient matrix
+    // transposed, the SDIG levels fill the rest, and each leaf is a contiguous column
+    c->col_major = true;
+    HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb,
+                           src_is_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
+    if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
+    HIP_TRY(transpose_elems(fid, (const uint32_t *)cf, n_rows, np, np, np, (uint32_t *)cm, n_rows, s));
+    DBuf tmp;
+    HIP_TRY(tmp.alloc(dev, e->sdig.tmp_elems * n_rows * wb));
+    HIP_TRY(sdig_encode_cm(e->sdig, (uint32_t *)cm, n_rows, tmp.as<uint32_t>(), s));
+  } else if (src_is_host) {
     HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb, hipMemcpyHostToDevice, s));
     if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
     HIP_TRY(ntt_rows(e->plan, (const uint32_t *)cf, np, np, (uint32_t *)cm, nc, n_rows, s));
@@ -475,7 +560,10 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   if (np2 > nc) HIP_TRY(hipMemsetAsync(c->hashes.as<uint8_t>() + nc * 32, 0, (np2 - nc) * 32, s));
   DBuf scratch;
   HIP_TRY(scratch.alloc(dev, leaf_hash_scratch_bytes(fid, n_rows, nc)));
-  HIP_TRY(leaf_hashes(fid, c->comm.as<uint32_t>(), n_rows, nc, nc, c->hashes.as<uint8_t>(), scratch.p, s));
+  if (c->col_major)
+    HIP_TRY(leaf_hashes_cols(fid, c->comm.as<uint32_t>(), n_rows, nc, c->hashes.as<uint8_t>(), scratch.p, s));
+  else
+    HIP_TRY(leaf_hashes(fid, c->comm.as<uint32_t>(), n_rows, nc, nc, c->hashes.as<uint8_t>(), scratch.p, s));
   HIP_TRY(merkle_tree(c->hashes.as<uint8_t>(), np2, s));
   HIP_TRY(hipMemcpyAsync(c->root, c->hashes.as<uint8_t>() + (c->n_hashes - 1) * 32, 32,
                          hipMemcpyDeviceToHost, s));
@@ -598,6 +686,39 @@ lcpc_status lcpc_rs_encoding_new(lcpc_field f, size_t n_per_row, size_t n_cols, 
   return make_rs_encoding(f, n_per_row, n_cols, nco, ndt, out);
 }
 
+size_t lcpc_sdig_n_col_opens(int code) { return sdig_n_col_opens(code); }
+
+lcpc_status lcpc_sdig_get_n_per_row(lcpc_field f, int code, size_t len, size_t *n_per_row) {
+  if (!valid_field(f) || !sdig_spec(code) || !n_per_row || len == 0)
+    return fail(LCPC_ERR_INVALID_ARG, "sdig_get_n_per_row arguments");
+  *n_per_row = sdig_new_np(code, field_info(f).num_bits, len);
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_sdig_new(lcpc_field f, int code, size_t len, uint64_t seed, lcpc_encoding **out) {
+  // SdigEncodingS::new (lcpc-brakedown-pc/src/lib.rs:103-110)
+  if (!valid_field(f) || !sdig_spec(code) || len == 0)
+    return fail(LCPC_ERR_INVALID_ARG, "sdig_new arguments");
+  return make_sdig_encoding(f, code, sdig_new_np(code, field_info(f).num_bits, len), 0, seed, out);
+}
+
+lcpc_status lcpc_sdig_new_ml(lcpc_field f, int code, size_t n_vars, uint64_t seed,
+                             lcpc_encoding **out) {
+  // SdigEncodingS::new_ml (lib.rs:114-123)
+  if (!valid_field(f) || !sdig_spec(code) || n_vars >= 63)
+    return fail(LCPC_ERR_INVALID_ARG, "sdig_new_ml arguments");
+  return make_sdig_encoding(f, code, sdig_new_ml_np(code, field_info(f).num_bits, n_vars), 0, seed, out);
+}
+
+lcpc_status lcpc_sdig_new_from_dims(lcpc_field f, int code, size_t n_per_row, size_t n_cols,
+                                    uint64_t seed, lcpc_encoding **out) {
+  // SdigEncodingS::new_from_dims (lib.rs:126-137)
+  if (n_cols == 0) return fail(LCPC_ERR_INVALID_ARG, "n_cols");
+  return make_sdig_encoding(f, code, n_per_row, n_cols, seed, out);
+}
+
+int lcpc_encoding_kind(const lcpc_encoding *e) { return e->kind; }
+
 void lcpc_encoding_free(lcpc_encoding *e) { delete e; }
 lcpc_field lcpc_encoding_field(const lcpc_encoding *e) { return (lcpc_field)e->fid; }
 
@@ -626,8 +747,9 @@ lcpc_status lcpc_encode_rows(const lcpc_encoding *e, uint64_t *rows, size_t n_ro
   HIP_TRY(d.alloc(dev, n_rows * e->n_cols * wb));
   HIP_TRY(hipMemcpy2DAsync(d.p, e->n_cols * wb, rows, stride * wb, e->n_cols * wb, n_rows,
                            hipMemcpyHostToDevice, lease.s));
-  HIP_TRY(ntt_rows(e->plan, d.as<uint32_t>(), e->n_cols, e->n_cols, d.as<uint32_t>(), e->n_cols,
-                   n_rows, lease.s));
+  lcpc_status st = encode_rows_any(e, d.as<uint32_t>(), e->n_cols, e->n_cols, d.as<uint32_t>(),
+                                   e->n_cols, n_rows, lease.s);
+  if (st) return st;
   HIP_TRY(hipMemcpy2DAsync(rows, stride * wb, d.p, e->n_cols * wb, e->n_cols * wb, n_rows,
                            hipMemcpyDeviceToHost, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
@@ -637,6 +759,8 @@ lcpc_status lcpc_encode_rows(const lcpc_encoding *e, uint64_t *rows, size_t n_ro
 lcpc_status lcpc_encode(const lcpc_encoding *e, uint64_t *inp, size_t len) {
   // fffft::fft_io_pc: the slice length must equal the precomputation length
   if (!e || !inp) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (e->kind == KIND_SDIG && len != e->n_cols)  // encode.rs:42 asserts the codeword length
+    return fail(LCPC_ERR_INVALID_ARG, "SDIG encode: slice length != codeword length");
   if (len != e->n_cols) {
     if (len == 0 || (len & (len - 1))) return fail(LCPC_FFT_NOT_POWER_OF_TWO, "FFTError::NotPowerOfTwo");
     if ((int)log2_np2(len) > field_info(e->fid).s) return fail(LCPC_FFT_TOO_BIG, "FFTError::TooBig");
@@ -655,8 +779,9 @@ lcpc_status lcpc_encode_rows_device(const lcpc_encoding *e, const void *d_src, s
   Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   hipStream_t s = stream ? (hipStream_t)stream : lease.s;
-  HIP_TRY(ntt_rows(e->plan, (const uint32_t *)d_src, src_stride, n_valid, (uint32_t *)d_dst,
-                   dst_stride, n_rows, s));
+  lcpc_status st = encode_rows_any(e, (const uint32_t *)d_src, src_stride, n_valid,
+                                   (uint32_t *)d_dst, dst_stride, n_rows, s);
+  if (st) return st;
   if (!stream) HIP_TRY(hipStreamSynchronize(s));
   return LCPC_OK;
 }
@@ -702,8 +827,20 @@ static lcpc_status copy_out(const lcpc_commit *c, void *dst, const void *src, si
   return LCPC_OK;
 }
 lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out) {
-  return copy_out(c, out, c->comm.p, c->n_rows * c->n_cols * field_bytes(c->fid));
+  const size_t bytes = c->n_rows * c->n_cols * field_bytes(c->fid);
+  if (!c->col_major) return copy_out(c, out, c->comm.p, bytes);
+  // element-major on the device -> the reference's row-major Vec<F>
+  Lease lease(c->dev);
+  HIP_TRY(hipSetDevice(c->dev->id));
+  DBuf rm;
+  HIP_TRY(rm.alloc(c->dev, bytes));
+  HIP_TRY(transpose_elems(c->fid, c->comm.as<uint32_t>(), c->n_cols, c->n_rows, c->n_rows, c->n_rows,
+                          rm.as<uint32_t>(), c->n_cols, lease.s));
+  HIP_TRY(hipMemcpyAsync(out, rm.p, bytes, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
 }
+int lcpc_commit_col_major(const lcpc_commit *c) { return c->col_major ? 1 : 0; }
 lcpc_status lcpc_commit_copy_coeffs(const lcpc_commit *c, uint64_t *out) {
   return copy_out(c, out, c->coeffs.p, c->n_rows * c->n_per_row * field_bytes(c->fid));
 }
@@ -737,7 +874,7 @@ lcpc_status lcpc_open_column(const lcpc_commit *c, size_t column, uint64_t *col_
   HIP_TRY(dcol.alloc(dev, c->n_rows * wb));
   HIP_TRY(dpath.alloc(dev, path_len * 32));
   HIP_TRY(gather_columns(c->fid, c->comm.as<uint32_t>(), c->n_rows, c->n_cols, didx.as<uint64_t>(), 1,
-                         dcol.as<uint32_t>(), lease.s));
+                         dcol.as<uint32_t>(), lease.s, c->col_major));
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), 1, path_len,
                        dpath.as<uint8_t>(), lease.s));
   if (col_out) HIP_TRY(hipMemcpyAsync(col_out, dcol.p, c->n_rows * wb, hipMemcpyDeviceToHost, lease.s));
@@ -857,7 +994,7 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   HIP_TRY(dcols.alloc(dev, nco * nr * wb));
   HIP_TRY(dpaths.alloc(dev, nco * p->path_len * 32));
   HIP_TRY(gather_columns(fid, c->comm.as<uint32_t>(), nr, c->n_cols, didx.as<uint64_t>(), nco,
-                         dcols.as<uint32_t>(), s));
+                         dcols.as<uint32_t>(), s, c->col_major));
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), nco, p->path_len,
                        dpaths.as<uint8_t>(), s));
   if (nco) {
@@ -958,7 +1095,8 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
                            hipMemcpyHostToDevice, s));
     st = upload(dev, dvec, p->p_random.data() + i * np * limbs, np * wb);
     if (st) return st;
-    HIP_TRY(ntt_rows(e->plan, dvec.as<uint32_t>(), np, np, denc.as<uint32_t>() + i * nc * limbs * 2, nc, 1, s));
+    st = encode_rows_any(e, dvec.as<uint32_t>(), np, np, denc.as<uint32_t>() + i * nc * limbs * 2, nc, 1, s);
+    if (st) return st;
     st = to_repr_host(dev, fid, dvec.as<uint32_t>(), np, &repr);
     if (st) return st;
     tr->t.append_messages(LABEL_PR, 6, repr, wb, np);
@@ -970,7 +1108,8 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
   tr->t.append_messages(LABEL_PE, 6, repr, wb, np);
   std::vector<uint64_t> idx;
   challenge_columns(tr->t, nc, nco, idx);
-  HIP_TRY(ntt_rows(e->plan, dvec.as<uint32_t>(), np, np, denc.as<uint32_t>() + ndt * nc * limbs * 2, nc, 1, s));
+  st = encode_rows_any(e, dvec.as<uint32_t>(), np, np, denc.as<uint32_t>() + ndt * nc * limbs * 2, nc, 1, s);
+  if (st) return st;
 
   // per-column checks (:953-974)
   st = upload(dev, didx, idx.data(), nco * 8);

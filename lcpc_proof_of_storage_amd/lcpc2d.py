@@ -290,6 +290,40 @@ class RsEncoding(LcEncoding):
         return cls(h.value)
 
 
+class SdigEncoding(LcEncoding):
+    """SdigEncodingS<F, SdigCodeK> (lcpc-brakedown-pc/src/lib.rs:40-176): Brakedown's expander
+    code; `code` K in 1..6 (codespec.rs:169-232), default 3 as the crate's SdigEncoding."""
+
+    @staticmethod
+    def _new(fn, *args) -> "SdigEncoding":
+        h = C.c_void_p()
+        _raise(fn(*args, C.byref(h)))
+        return SdigEncoding(h.value)
+
+    @classmethod
+    def new(cls, field: int, length: int, seed: int, code: int = 3) -> "SdigEncoding":
+        return cls._new(N.load().lcpc_sdig_new, field, code, length, seed)
+
+    @classmethod
+    def new_ml(cls, field: int, n_vars: int, seed: int, code: int = 3) -> "SdigEncoding":
+        return cls._new(N.load().lcpc_sdig_new_ml, field, code, n_vars, seed)
+
+    @classmethod
+    def new_from_dims(cls, field: int, n_per_row: int, n_cols: int, seed: int,
+                      code: int = 3) -> "SdigEncoding":
+        return cls._new(N.load().lcpc_sdig_new_from_dims, field, code, n_per_row, n_cols, seed)
+
+    @staticmethod
+    def n_col_opens(code: int = 3) -> int:
+        return N.load().lcpc_sdig_n_col_opens(code)
+
+    @staticmethod
+    def n_per_row_for(field: int, length: int, code: int = 3) -> int:
+        out = C.c_size_t()
+        _raise(N.load().lcpc_sdig_get_n_per_row(field, code, length, C.byref(out)))
+        return out.value
+
+
 # ---------------------------------------------------------------- commitment / proof
 @dataclass
 class LcColumn:

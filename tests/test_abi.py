@@ -103,6 +103,17 @@ def test_dims_and_counts_match_oracle(api, oracle):
         assert api.log2(v) == L.of_log2(v)
 
 
+def test_sdig_parameters_match_oracle(api, oracle):
+    """SdigEncodingS::_n_col_opens and new()'s n_per_row choice (lcpc-brakedown-pc/src/lib.rs:
+    57-110) are host-only."""
+    L = oracle.lib()
+    for code in range(1, 7):
+        assert api.SdigEncoding.n_col_opens(code) == L.of_sdig_n_col_opens(code)
+        for fid in [0, 1, 2, 3, 4]:
+            for n in [100, 5000, 1 << 16, 1 << 20, (1 << 24) + 17, 1 << 26]:
+                assert api.SdigEncoding.n_per_row_for(fid, n, code) == L.of_sdig_new_np(fid, code, n)
+
+
 def test_transcript_matches_oracle(api, oracle):
     """Merlin framing through both STROBE paths (records inside / across the 166-byte rate)."""
     rng = np.random.default_rng(4)
