@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--log-len", type=int, default=24)
     ap.add_argument("--field", default="Ft127")
+    ap.add_argument("--code", choices=["ligero", "sdig"], default="ligero",
+                    help="ligero: R-S / NTT rows (the BASELINE metric, cfg3); sdig: Brakedown "
+                         "SdigCode3 expander code, seed 0 (cfg4)")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the cores available (max 16)")
     ap.add_argument("--no-prof", action="store_true", help="disable HIP-event kernel timing")
@@ -120,7 +123,8 @@ def main():
     fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
     nl = L.limbs(fid)
     n = 1 << args.log_len
-    enc = L.LigeroEncoding.new(fid, n)
+    sdig = args.code == "sdig"
+    enc = L.SdigEncoding.new(fid, n, 0) if sdig else L.LigeroEncoding.new(fid, n)
     n_rows, n_per_row, n_cols = enc.get_dims(n)
     nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
 
@@ -210,7 +214,8 @@ def main():
     value = job_throughput(n, args.steps, world, elapsed)
     B = 8 * nl
     out = {
-        "metric": "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU",
+        "metric": ("committed field-elements/s (commit+open), 2^24-coeff Brakedown (cfg4)" if sdig else
+                   "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU"),
         "value": value,
         "unit": "field-elements/s",
         "n_gpus": world,
@@ -224,7 +229,9 @@ def main():
         "dtype": f"u64x{nl} ({args.field} Montgomery limbs)",
         "data": f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), resident in HBM",
         "config": {
-            "workload": f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho=1/2, "
+            "workload": (f"Brakedown (SdigCode3, seed 0) commit+open, {args.field}, 2^{args.log_len} coeffs, "
+                         if sdig else f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho=1/2, ")
+                        +
                         f"{n_rows}x{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, BLAKE3 Merkle",
             "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
             "n_col_opens": nco, "n_degree_tests": ndt,
@@ -241,23 +248,28 @@ def main():
     if iso:
         ki = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in iso.items()}
         out["kernels"] = ki
-        enc_ms = sum(ki[k]["avg_ms"] for k in ("ntt_pass_a", "ntt_pass_b") if k in ki)
-        algo = n_rows * n_per_row * B + n_rows * n_cols * B  # encode bytes per commit
+        enc_kernels = ("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b")
+        enc_ms = sum(ki[k]["avg_ms"] for k in enc_kernels if k in ki)
+        # encode bytes per commit (read the coefficients, write the codeword;
+        # SDIG also streams its code matrices once: 16-B values + 4-B indices)
+        algo = n_rows * n_per_row * B + n_rows * n_cols * B + (enc.matrix_nnz * (B + 4) if sdig else 0)
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):
             try:
                 tj = json.load(open(tpath))
-                if tj.get("config_len") == n and tj.get("field") == args.field:
+                if (tj.get("config_len") == n and tj.get("field") == args.field
+                        and tj.get("code", "ligero") == args.code):
                     traffic = tj.get("ntt_encode_bytes_per_launch")
             except Exception:
                 traffic = None
         achieved = algo / (enc_ms * 1e-3) / 1e9 if enc_ms else None
         tr_ms = None
         if stats:
-            tr_ms = sum(stats[k][0] / max(stats[k][1], 1) for k in ("ntt_pass_a", "ntt_pass_b") if k in stats)
+            tr_ms = sum(stats[k][0] / max(stats[k][1], 1) for k in enc_kernels if k in stats)
         out["roofline"] = {
-            "kernel": "ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all 512 rows)",
+            "kernel": ("sdig_encode = transpose + 13 SpMM / Reed-Solomon levels (per commit, all rows)" if sdig
+                       else f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
@@ -266,7 +278,7 @@ def main():
             "traffic": traffic,
             "algorithmic_bytes": algo,
             "avg_ms": enc_ms,
-            "launches": min(ki.get("ntt_pass_a", {}).get("launches", 0), ki.get("ntt_pass_b", {}).get("launches", 0)),
+            "launches": min(ki.get(k, {}).get("launches", 0) for k in enc_kernels),
             "measured": f"HIP events on the launching stream, {args.roofline_steps} serial steps after the "
                         f"timed region (same process, inputs and kernels)",
             "timed_region_avg_ms": tr_ms,
@@ -280,7 +292,8 @@ def main():
 
         cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         O.lib().of_set_threads(cores)
-        o_enc = O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
+        o_enc = (O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3) if sdig
+                 else O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt))
         t1 = time.perf_counter()
         oc = O.Commit(o_enc, coeffs.reshape(-1))
         otr = O.standard_transcript(nco, oc.root())

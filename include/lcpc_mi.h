@@ -125,6 +125,8 @@ lcpc_status lcpc_sdig_new_from_dims(lcpc_field f, int code, size_t n_per_row, si
                                     uint64_t seed, lcpc_encoding **out); /* :126-137 */
 /* 0 = Reed-Solomon / fft_io (Ligero), 1 = SDIG expander code (Brakedown) */
 int lcpc_encoding_kind(const lcpc_encoding *e);
+/* nonzeros of all SDIG precode + postcode matrices (0 for R-S encodings) */
+size_t lcpc_encoding_matrix_nnz(const lcpc_encoding *e);
 void lcpc_encoding_free(lcpc_encoding *e);
 lcpc_field lcpc_encoding_field(const lcpc_encoding *e);
 /* LcEncoding::get_dims / dims_ok / get_n_col_opens / get_n_degree_tests (lib.rs:94-104) */

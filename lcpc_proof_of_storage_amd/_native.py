@@ -48,6 +48,7 @@ SIGNATURES = {
     "lcpc_sdig_new_ml": (i32, [i32, i32, sz, C.c_uint64, C.POINTER(vp)]),
     "lcpc_sdig_new_from_dims": (i32, [i32, i32, sz, sz, C.c_uint64, C.POINTER(vp)]),
     "lcpc_encoding_kind": (i32, [vp]),
+    "lcpc_encoding_matrix_nnz": (sz, [vp]),
     "lcpc_encoding_free": (None, [vp]),
     "lcpc_encoding_field": (i32, [vp]),
     "lcpc_encoding_get_dims": (None, [vp, sz, szp, szp, szp]),

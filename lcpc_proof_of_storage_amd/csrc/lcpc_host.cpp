@@ -719,6 +719,13 @@ lcpc_status lcpc_sdig_new_from_dims(lcpc_field f, int code, size_t n_per_row, si
 
 int lcpc_encoding_kind(const lcpc_encoding *e) { return e->kind; }
 
+size_t lcpc_encoding_matrix_nnz(const lcpc_encoding *e) {
+  size_t nnz = 0;
+  for (const auto &m : e->sdig.pre) nnz += m.nnz;
+  for (const auto &m : e->sdig.post) nnz += m.nnz;
+  return nnz;
+}
+
 void lcpc_encoding_free(lcpc_encoding *e) { delete e; }
 lcpc_field lcpc_encoding_field(const lcpc_encoding *e) { return (lcpc_field)e->fid; }
 

@@ -223,6 +223,15 @@ class LcEncoding:
     def get_n_degree_tests(self) -> int:
         return N.load().lcpc_encoding_n_degree_tests(self._h)
 
+    @property
+    def kind(self) -> str:
+        return ["rs", "sdig"][N.load().lcpc_encoding_kind(self._h)]
+
+    @property
+    def matrix_nnz(self) -> int:
+        """Nonzeros of the SDIG code matrices (0 for R-S)."""
+        return N.load().lcpc_encoding_matrix_nnz(self._h)
+
     def encode(self, inp: np.ndarray) -> np.ndarray:
         """LcEncoding::encode: in place on one row of n_cols elements (uint64, C-contiguous)."""
         a = np.asarray(inp)
