@@ -236,6 +236,50 @@ int lcpc_verify_column_value(lcpc_field f, const uint64_t *col, const uint64_t *
 lcpc_status lcpc_hash_columns(lcpc_field f, const uint64_t *comm, size_t n_rows, size_t n_cols,
                               uint8_t *out);
 
+/* ------------------------------------------------------------------ proof-of-storage producers
+ * (proof-of-storage/src; the field is WriteableFt63 = LCPC_FT63's modulus and arithmetic) */
+/* DataField::from_byte_vec for WriteableFt63 (fields/data_field.rs:38-46, writable_ft63.rs:
+ * 35-40): each 7 little-endian data bytes (the last chunk zero padded) become one element whose
+ * RAW u64 limb holds them (no Montgomery conversion).  *n_out = ceil(n_bytes / 7). */
+lcpc_status lcpc_pos_bytes_to_field(const uint8_t *bytes, size_t n_bytes, uint64_t *out,
+                                    size_t *n_out);
+/* same on device buffers (8-byte aligned); asynchronous on `stream` (NULL: synchronous) */
+lcpc_status lcpc_pos_bytes_to_field_device(const void *d_bytes, size_t n_bytes, void *d_out,
+                                           void *stream);
+/* DataField::field_vec_to_byte_vec truncated to expected_len (data_field.rs:57-62,
+ * fields.rs:115-121) */
+lcpc_status lcpc_pos_field_to_bytes(const uint64_t *elems, size_t n, uint8_t *out,
+                                    size_t expected_len);
+/* get_aspect_ratio_default_from_field_len + get_soundness_from_matrix_dims
+ * (networking/server.rs:1139-1170) */
+void lcpc_pos_default_dims(size_t field_len, size_t *n_per_row, size_t *n_cols,
+                           size_t *soundness);
+/* get_column_indicies_from_random_seed (networking/client.rs:443-456): ChaCha8Rng +
+ * IteratorRandom::choose_multiple; *n_out = min(amount, max_index) */
+lcpc_status lcpc_pos_column_indices(uint64_t seed, size_t amount, size_t max_index,
+                                    uint64_t *out, size_t *n_out);
+/* form_side_vectors_for_polynomial_evaluation_from_point (lcpc_online.rs:603-627):
+ * right = [1, x, ..., x^(n_cols-1)], left = [1, x^n_cols, ..., x^((n_rows-1) n_cols)] */
+lcpc_status lcpc_pos_side_vectors(lcpc_field f, const uint64_t *x, size_t n_rows, size_t n_cols,
+                                  uint64_t *left, uint64_t *right);
+/* verifiable_polynomial_evaluation (lcpc_online.rs:454-484): out[j] = sum_r left[r] comm[r][j]
+ * over the ENCODED matrix (n_cols outputs; row-major commitments) */
+lcpc_status lcpc_pos_eval_encoded(const lcpc_commit *c, const uint64_t *left, size_t n_rows,
+                                  uint64_t *out);
+/* decode_row (lcpc_online.rs:568-574) = fffft ifft_oi on each of n_rows rows of len = 2^k
+ * elements (in place); FFTError codes on bad lengths */
+lcpc_status lcpc_ifft_oi_rows(lcpc_field f, uint64_t *rows, size_t n_rows, size_t len);
+/* open_column (lcpc-2d/src/lib.rs:818-855) for n columns at once (server_retreive_columns,
+ * lcpc_online.rs:241-247): cols_out n x n_rows elements, paths_out n x log2(n_cols) x 32 B */
+lcpc_status lcpc_open_columns(const lcpc_commit *c, const uint64_t *idx, size_t n,
+                              uint64_t *cols_out, uint8_t *paths_out);
+/* CommitRequestType::ColumnsWithoutPath / Leaves (lcpc_online.rs:144-224): encode `len`
+ * elements with e and return the requested columns (n x n_rows) and / or their BLAKE3 leaf
+ * digests (n x 32 B) without building the Merkle tree; either output may be NULL */
+lcpc_status lcpc_pos_columns(const lcpc_encoding *e, const uint64_t *elems, size_t len,
+                             const uint64_t *idx, size_t n, uint64_t *cols_out,
+                             uint8_t *leaves_out);
+
 /* ------------------------------------------------------------------ kernel timing
  * HIP-event timing of every kernel launch on the handle streams (off by default). */
 void lcpc_prof_enable(int enable);

@@ -100,6 +100,16 @@ SIGNATURES = {
     "lcpc_verify_column_path": (i32, [i32, u64p, sz, u8p, sz, sz, u8p]),
     "lcpc_verify_column_value": (i32, [i32, u64p, u64p, sz, u64p]),
     "lcpc_hash_columns": (i32, [i32, u64p, sz, sz, u8p]),
+    "lcpc_pos_bytes_to_field": (i32, [u8p, sz, u64p, szp]),
+    "lcpc_pos_bytes_to_field_device": (i32, [vp, sz, vp, vp]),
+    "lcpc_pos_field_to_bytes": (i32, [u64p, sz, u8p, sz]),
+    "lcpc_pos_default_dims": (None, [sz, szp, szp, szp]),
+    "lcpc_pos_column_indices": (i32, [C.c_uint64, sz, sz, u64p, szp]),
+    "lcpc_pos_side_vectors": (i32, [i32, u64p, sz, sz, u64p, u64p]),
+    "lcpc_pos_eval_encoded": (i32, [vp, u64p, sz, u64p]),
+    "lcpc_ifft_oi_rows": (i32, [i32, u64p, sz, sz]),
+    "lcpc_open_columns": (i32, [vp, u64p, sz, u64p, u8p]),
+    "lcpc_pos_columns": (i32, [vp, u64p, sz, u64p, sz, u64p, u8p]),
     "lcpc_prof_enable": (None, [i32]),
     "lcpc_prof_reset": (None, []),
     "lcpc_prof_get": (i32, [C.c_char_p, C.POINTER(C.c_double), u64p]),

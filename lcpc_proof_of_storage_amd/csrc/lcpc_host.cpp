@@ -21,6 +21,7 @@
 #include "../../include/lcpc_mi.h"
 #include "field.hpp"
 #include "kernels.hpp"
+#include "pos.hpp"
 #include "prof.hpp"
 #include "sdig.hpp"
 #include "transcript.hpp"
@@ -1269,6 +1270,321 @@ int lcpc_verify_column_value(lcpc_field f, const uint64_t *col, const uint64_t *
       hipStreamSynchronize(lease.s))
     return 0;
   return flag != 0;
+}
+
+}  // extern "C"
+
+// ================================================================= proof-of-storage producers
+namespace {
+
+// n^-1 mod p for n = 2^log_n | p - 1, canonical: p - (p - 1) / n
+void inv_pow2_canon(int fid, int log_n, uint32_t *words) {
+  const FieldInfo fi = field_info(fid);
+  uint64_t q[4] = {0, 0, 0, 0}, r[4] = {0, 0, 0, 0};
+  for (int i = 0; i < fi.limbs; i++) q[i] = fi.p[i];
+  q[0] -= 1;  // p odd: no borrow
+  for (int k = 0; k < log_n; k++) {  // q >>= 1 (multi-limb)
+    for (int i = 0; i < fi.limbs; i++) {
+      q[i] >>= 1;
+      if (i + 1 < fi.limbs) q[i] |= q[i + 1] << 63;
+    }
+  }
+  uint64_t br = 0;
+  for (int i = 0; i < fi.limbs; i++) {
+    const uint64_t a = fi.p[i], b = q[i];
+    const uint64_t d = a - b - br;
+    br = (a < b) || (a - b < br);
+    r[i] = d;
+  }
+  for (int i = 0; i < fi.limbs; i++) {
+    words[2 * i] = (uint32_t)r[i];
+    words[2 * i + 1] = (uint32_t)(r[i] >> 32);
+  }
+}
+
+lcpc_status check_fft_len(int fid, size_t len) {
+  if (len == 0 || (len & (len - 1))) return fail(LCPC_FFT_NOT_POWER_OF_TWO, "FFTError::NotPowerOfTwo");
+  if ((int)log2_np2(len) > field_info(fid).s) return fail(LCPC_FFT_TOO_BIG, "FFTError::TooBig");
+  return LCPC_OK;
+}
+
+// Encode `len` host elements with e into a temporary row-major codeword (Leaves /
+// ColumnsWithoutPath requests, lcpc_online.rs:144-224): no commitment, no Merkle tree.
+lcpc_status encode_matrix(const lcpc_encoding *e, const uint64_t *elems, size_t len, DBuf &comm,
+                          size_t *n_rows_out, hipStream_t s) {
+  const size_t np = e->n_per_row, nc = e->n_cols;
+  const size_t n_rows = (len + np - 1) / np;
+  const int wb = field_bytes(e->fid);
+  DBuf coeffs;
+  HIP_TRY(coeffs.alloc(e->dev, n_rows * np * wb));
+  HIP_TRY(hipMemcpyAsync(coeffs.p, elems, len * wb, hipMemcpyHostToDevice, s));
+  if (n_rows * np > len)
+    HIP_TRY(hipMemsetAsync(coeffs.as<uint8_t>() + len * wb, 0, (n_rows * np - len) * wb, s));
+  HIP_TRY(comm.alloc(e->dev, n_rows * nc * wb));
+  lcpc_status st = encode_rows_any(e, coeffs.as<uint32_t>(), np, np, comm.as<uint32_t>(), nc, n_rows, s);
+  if (st) return st;
+  *n_rows_out = n_rows;
+  return LCPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+lcpc_status lcpc_pos_bytes_to_field_device(const void *d_bytes, size_t n_bytes, void *d_out,
+                                           void *stream) {
+  if ((!d_bytes || !d_out) && n_bytes) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (((uintptr_t)d_bytes & 7) || ((uintptr_t)d_out & 7))
+    return fail(LCPC_ERR_INVALID_ARG, "device buffers must be 8-byte aligned");
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  hipStream_t s = stream ? (hipStream_t)stream : lease.s;
+  HIP_TRY(pos_pack7((const uint8_t *)d_bytes, n_bytes, (uint64_t *)d_out, s));
+  if (!stream) HIP_TRY(hipStreamSynchronize(s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_pos_bytes_to_field(const uint8_t *bytes, size_t n_bytes, uint64_t *out,
+                                    size_t *n_out) {
+  if ((!bytes || !out) && n_bytes) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  const size_t n = (n_bytes + 6) / 7;
+  if (n_out) *n_out = n;
+  if (!n) return LCPC_OK;
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf db, de;
+  if ((st = upload(dev, db, bytes, n_bytes))) return st;
+  HIP_TRY(de.alloc(dev, n * 8));
+  HIP_TRY(pos_pack7(db.as<uint8_t>(), n_bytes, de.as<uint64_t>(), lease.s));
+  HIP_TRY(hipMemcpyAsync(out, de.p, n * 8, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_pos_field_to_bytes(const uint64_t *elems, size_t n, uint8_t *out,
+                                    size_t expected_len) {
+  if ((!elems && n) || (!out && expected_len)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (expected_len > 7 * n) return fail(LCPC_ERR_INVALID_ARG, "expected_len > 7 * n");
+  if (!expected_len) return LCPC_OK;
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf de, db;
+  if ((st = upload(dev, de, elems, n * 8))) return st;
+  HIP_TRY(db.alloc(dev, expected_len));
+  HIP_TRY(pos_unpack7(de.as<uint64_t>(), n, db.as<uint8_t>(), expected_len, lease.s));
+  HIP_TRY(hipMemcpyAsync(out, db.p, expected_len, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+void lcpc_pos_default_dims(size_t field_len, size_t *n_per_row, size_t *n_cols, size_t *soundness) {
+  // get_aspect_ratio_default_from_field_len (networking/server.rs:1139-1158): f32 sqrt
+  const size_t w = (size_t)std::ceil(std::sqrt((float)field_len));
+  const size_t np = (w & (w - 1)) == 0 ? w : next_pow2(w);  // fields::is_power_of_two
+  const size_t nc = next_pow2(np + 1);
+  // get_soundness_from_matrix_dims (:1160-1170)
+  const double den = std::log2((1.0 + (double)np / (double)nc) / 2.0);
+  const size_t th = (size_t)std::ceil(-128.0 / den);
+  if (n_per_row) *n_per_row = np;
+  if (n_cols) *n_cols = nc;
+  if (soundness) *soundness = th < nc ? th : nc;
+}
+
+lcpc_status lcpc_pos_column_indices(uint64_t seed, size_t amount, size_t max_index, uint64_t *out,
+                                    size_t *n_out) {
+  // get_column_indicies_from_random_seed (networking/client.rs:443-456): ChaCha8Rng +
+  // IteratorRandom::choose_multiple (rand 0.8 reservoir; gen_index = gen_range(0..ub as u32))
+  if (!out && amount) return fail(LCPC_ERR_INVALID_ARG, "null out");
+  ChaCha20Rng rng = ChaCha20Rng::seed_from_u64(seed, 8);
+  size_t filled = 0;
+  for (size_t i = 0; i < max_index && filled < amount; i++) out[filled++] = i;
+  if (filled == amount) {
+    for (size_t i = 0; amount + i < max_index; i++) {
+      const size_t ub = i + 1 + amount;
+      size_t k;
+      if (ub <= 0xffffffffu) {
+        const uint32_t range = (uint32_t)ub;
+        const uint32_t zone = (range << __builtin_clz(range)) - 1;
+        for (;;) {
+          const uint64_t m = (uint64_t)rng.next_u32() * range;
+          if ((uint32_t)m <= zone) {
+            k = (size_t)(m >> 32);
+            break;
+          }
+        }
+      } else {
+        const uint64_t zone = ((uint64_t)ub << __builtin_clzll((uint64_t)ub)) - 1;
+        for (;;) {
+          const unsigned __int128 m = (unsigned __int128)rng.next_u64() * ub;
+          if ((uint64_t)m <= zone) {
+            k = (size_t)(m >> 64);
+            break;
+          }
+        }
+      }
+      if (k < amount) out[k] = amount + i;
+    }
+  }
+  if (n_out) *n_out = filled;
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_pos_side_vectors(lcpc_field f, const uint64_t *x, size_t n_rows, size_t n_cols,
+                                  uint64_t *left, uint64_t *right) {
+  // form_side_vectors_for_polynomial_evaluation_from_point (lcpc_online.rs:603-627):
+  // right = [1, x, ..., x^(n_cols-1)], left = [1, x^n_cols, x^(2 n_cols), ...]
+  if (!valid_field(f) || !x || (!left && n_rows) || (!right && n_cols))
+    return fail(LCPC_ERR_INVALID_ARG, "side vector arguments");
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  const int wb = field_bytes(f);
+  DBuf dx, dl, dr;
+  if ((st = upload(dev, dx, x, wb))) return st;
+  HIP_TRY(dl.alloc(dev, n_rows * wb));
+  HIP_TRY(dr.alloc(dev, n_cols * wb));
+  HIP_TRY(powers(f, dx.as<uint32_t>(), 1, n_cols, dr.as<uint32_t>(), lease.s));
+  HIP_TRY(powers(f, dx.as<uint32_t>(), (uint64_t)n_cols, n_rows, dl.as<uint32_t>(), lease.s));
+  if (n_cols) HIP_TRY(hipMemcpyAsync(right, dr.p, n_cols * wb, hipMemcpyDeviceToHost, lease.s));
+  if (n_rows) HIP_TRY(hipMemcpyAsync(left, dl.p, n_rows * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_pos_eval_encoded(const lcpc_commit *c, const uint64_t *left, size_t n_rows,
+                                  uint64_t *out) {
+  // verifiable_polynomial_evaluation (lcpc_online.rs:454-484): out[j] = sum_r left[r] comm[r][j]
+  if (!c || !left || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (n_rows != c->n_rows) return fail(LCPC_ERR_INVALID_ARG, "left vector length != n_rows");
+  if (c->col_major) return fail(LCPC_ERR_UNSUPPORTED, "row-major (Ligero) commitments only");
+  Device *dev = c->dev;
+  Lease lease(dev, true);
+  HIP_TRY(hipSetDevice(dev->id));
+  const int wb = field_bytes(c->fid);
+  DBuf dt, dout, scratch;
+  lcpc_status st;
+  if ((st = upload(dev, dt, left, n_rows * wb))) return st;
+  HIP_TRY(dout.alloc(dev, c->n_cols * wb));
+  HIP_TRY(scratch.alloc(dev, collapse_scratch_bytes(c->fid, n_rows, c->n_cols, 1)));
+  HIP_TRY(collapse_rows(c->fid, c->comm.as<uint32_t>(), n_rows, c->n_cols, dt.as<uint32_t>(), 1,
+                        dout.as<uint32_t>(), scratch.p, lease.s));
+  HIP_TRY(hipMemcpyAsync(out, dout.p, c->n_cols * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_ifft_oi_rows(lcpc_field f, uint64_t *rows, size_t n_rows, size_t len) {
+  // fffft::ifft_oi on each row (decode_row, lcpc_online.rs:568-574): bit-reversed evaluations
+  // in, natural-order coefficients out
+  if (!valid_field(f) || (!rows && n_rows)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  if (!field_gpu_supported(f)) return fail(LCPC_ERR_UNSUPPORTED, "field has no gfx950 kernels");
+  lcpc_status st = check_fft_len(f, len);
+  if (st) return st;
+  if (n_rows == 0) return LCPC_OK;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  const int log_n = (int)log2_np2(len);
+  const int wb = field_bytes(f);
+  NttPlan plan;
+  hipError_t he = ntt_plan_init(plan, f, log_n, true, lease.s);
+  if (he != hipSuccess) {
+    ntt_plan_free(plan);
+    if (he == hipErrorInvalidValue) return fail(LCPC_ERR_UNSUPPORTED, "length beyond the NTT range");
+    HIP_TRY(he);
+  }
+  struct PlanGuard {
+    NttPlan &p;
+    hipStream_t s;
+    ~PlanGuard() {
+      (void)hipStreamSynchronize(s);
+      ntt_plan_free(p);
+    }
+  } guard{plan, lease.s};
+  DBuf a, b;
+  if ((st = upload(dev, a, rows, n_rows * len * wb))) return st;
+  HIP_TRY(b.alloc(dev, n_rows * len * wb));
+  uint32_t inv[8] = {0};
+  inv_pow2_canon(f, log_n, inv);
+  HIP_TRY(bitrev_scale(f, a.as<uint32_t>(), b.as<uint32_t>(), log_n, n_rows, nullptr, lease.s));
+  HIP_TRY(ntt_rows(plan, b.as<uint32_t>(), len, len, a.as<uint32_t>(), len, n_rows, lease.s));
+  HIP_TRY(bitrev_scale(f, a.as<uint32_t>(), b.as<uint32_t>(), log_n, n_rows, inv, lease.s));
+  HIP_TRY(hipMemcpyAsync(rows, b.p, n_rows * len * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_open_columns(const lcpc_commit *c, const uint64_t *idx, size_t n, uint64_t *cols_out,
+                              uint8_t *paths_out) {
+  // open_column (lcpc-2d/src/lib.rs:818-855) for n columns at once (PoS server_retreive_columns,
+  // lcpc_online.rs:241-247)
+  if (!c || (!idx && n)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  for (size_t k = 0; k < n; k++)
+    if (idx[k] >= c->n_cols) return fail(LCPC_PROVER_COLUMN_NUMBER, "ProverError::ColumnNumber");
+  if (!n) return LCPC_OK;
+  Device *dev = c->dev;
+  Lease lease(dev, true);
+  HIP_TRY(hipSetDevice(dev->id));
+  const size_t path_len = log2_np2(c->n_cols);
+  const int wb = field_bytes(c->fid);
+  DBuf didx, dcol, dpath;
+  lcpc_status st;
+  if ((st = upload(dev, didx, idx, n * 8))) return st;
+  HIP_TRY(dcol.alloc(dev, n * c->n_rows * wb));
+  HIP_TRY(dpath.alloc(dev, n * path_len * 32 + 32));
+  HIP_TRY(gather_columns(c->fid, c->comm.as<uint32_t>(), c->n_rows, c->n_cols, didx.as<uint64_t>(), n,
+                         dcol.as<uint32_t>(), lease.s, c->col_major));
+  HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), n, path_len,
+                       dpath.as<uint8_t>(), lease.s));
+  if (cols_out) HIP_TRY(hipMemcpyAsync(cols_out, dcol.p, n * c->n_rows * wb, hipMemcpyDeviceToHost, lease.s));
+  if (paths_out && path_len)
+    HIP_TRY(hipMemcpyAsync(paths_out, dpath.p, n * path_len * 32, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_pos_columns(const lcpc_encoding *e, const uint64_t *elems, size_t len,
+                             const uint64_t *idx, size_t n, uint64_t *cols_out, uint8_t *leaves_out) {
+  // CommitRequestType::ColumnsWithoutPath / Leaves (lcpc_online.rs:144-224): encode the file,
+  // then return the requested columns and / or their BLAKE3 leaf digests -- no Merkle tree
+  if (!e || !elems || len == 0 || (!idx && n)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  for (size_t k = 0; k < n; k++)
+    if (idx[k] >= e->n_cols) return fail(LCPC_PROVER_COLUMN_NUMBER, "ProverError::ColumnNumber");
+  Device *dev = e->dev;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf comm, didx, dcol, dleaves, scratch;
+  size_t n_rows = 0;
+  lcpc_status st = encode_matrix(e, elems, len, comm, &n_rows, lease.s);
+  if (st) return st;
+  if (!n) return LCPC_OK;
+  const int wb = field_bytes(e->fid);
+  if ((st = upload(dev, didx, idx, n * 8))) return st;
+  HIP_TRY(dcol.alloc(dev, n * n_rows * wb));
+  HIP_TRY(gather_columns(e->fid, comm.as<uint32_t>(), n_rows, e->n_cols, didx.as<uint64_t>(), n,
+                         dcol.as<uint32_t>(), lease.s));
+  if (leaves_out) {
+    HIP_TRY(dleaves.alloc(dev, n * 32));
+    HIP_TRY(scratch.alloc(dev, leaf_hash_scratch_bytes(e->fid, n_rows, n)));
+    HIP_TRY(leaf_hashes_cols(e->fid, dcol.as<uint32_t>(), n_rows, n, dleaves.as<uint8_t>(), scratch.p,
+                             lease.s));
+    HIP_TRY(hipMemcpyAsync(leaves_out, dleaves.p, n * 32, hipMemcpyDeviceToHost, lease.s));
+  }
+  if (cols_out) HIP_TRY(hipMemcpyAsync(cols_out, dcol.p, n * n_rows * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
 }
 
 }  // extern "C"

@@ -414,6 +414,20 @@ class LcCommit:
         pb = bytes(path)
         return LcColumn(col, [pb[32 * i:32 * i + 32] for i in range(pl)])
 
+    def open_columns(self, columns) -> List[LcColumn]:
+        """open_column for many columns in one device pass."""
+        idx = np.ascontiguousarray(list(columns), dtype=np.uint64)
+        n = len(idx)
+        nr, nl = self.get_n_rows(), limbs(self.field)
+        pl = log2(self.get_n_cols())
+        cols = np.zeros((max(n, 1), nr, nl), np.uint64)
+        paths = (C.c_uint8 * max(32 * pl * n, 1))()
+        _raise(N.load().lcpc_open_columns(self._h, _p64(idx) if n else None, n, _p64(cols),
+                                          C.cast(paths, N.u8p)))
+        pb = bytes(paths)
+        return [LcColumn(cols[k].copy(), [pb[32 * (k * pl + i):32 * (k * pl + i + 1)] for i in range(pl)])
+                for k in range(n)]
+
     def prove(self, outer_tensor: np.ndarray, enc: LcEncoding, tr: Transcript) -> "LcEvalProof":
         o = _elems(outer_tensor, self.field)
         h = C.c_void_p()

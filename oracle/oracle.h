@@ -158,6 +158,14 @@ int of_verify_column_value(int fid, const uint64_t *col, const uint64_t *tensor,
 of_enc *of_enc_sdig(int fid, size_t n_per_row, size_t n_cols_hint, uint64_t seed, int code_id,
                     size_t n_col_opens, size_t n_degree_tests);
 
+/* ---------------- proof-of-storage producers (proof-of-storage/src) ---------------- */
+size_t of_pos_bytes_to_field(const uint8_t *bytes, size_t n_bytes, uint64_t *out);
+void of_pos_field_to_bytes(const uint64_t *elems, size_t n, uint8_t *out, size_t expected_len);
+void of_pos_default_dims(size_t field_len, size_t *n_per_row, size_t *n_cols, size_t *soundness);
+size_t of_pos_column_indices(uint64_t seed, size_t amount, size_t max_index, uint64_t *out);
+void of_pos_side_vectors(int fid, const uint64_t *x, size_t n_rows, size_t n_cols, uint64_t *left,
+                         uint64_t *right);
+
 #ifdef __cplusplus
 }
 #endif

@@ -113,6 +113,23 @@ def transcript_case():
             "seed_from_u64_7_u64": [O.ChaCha(seed_u64=7).next_u64() for _ in range(1)]}
 
 
+def pos_case():
+    """proof-of-storage: the reference's test_files/test.txt (committed as pos_test.txt) packed
+    7 bytes per WriteableFt63 element and committed with CommitDimensions::Square."""
+    data = open(os.path.join(HERE, "pos_test.txt"), "rb").read()
+    el = O.pos_bytes_to_field(data)
+    np_, nc, snd = O.pos_default_dims(len(el))
+    enc = O.Encoding.ligero(0, np_, nc)
+    comm = O.Commit(enc, el)
+    x = O.ChaCha(seed_u64=1337, rounds=8).field_random(0, 1)
+    left, right = O.pos_side_vectors(0, x, comm.n_rows, comm.n_per_row)
+    r = O.collapse(0, comm.comm, left, comm.n_rows, comm.n_cols)
+    return {"n_bytes": len(data), "elems_sha256": sha(el), "dims": [comm.n_rows, np_, nc],
+            "soundness": snd, "root": comm.root().hex(), "comm_sha256": sha(comm.comm),
+            "eval_x_seed_chacha8": 1337, "eval_encoded_sha256": sha(r),
+            "columns_1337_8": O.pos_column_indices(1337, 8, nc)}
+
+
 def main():
     out = {
         "cfg1_ft127_2_16": ligero_case(1, 16),
@@ -124,6 +141,7 @@ def main():
         "cfg2_ft127_2_20_encode": encode_case(1, 20),
         "brakedown_ft127_4096_seed0": brakedown_case(1, 4096, 0),
         "transcript": transcript_case(),
+        "pos_test_txt_square": pos_case(),
     }
     path = os.path.join(HERE, "golden.json")
     with open(path, "w") as f:

@@ -117,6 +117,11 @@ def _setup(L):
         "of_open_column": (C.c_int, [C.POINTER(OfCommit), C.c_size_t, u64p, u8p]),
         "of_verify_column_path": (C.c_int, [C.c_int, u64p, C.c_size_t, u8p, C.c_size_t, C.c_size_t, u8p]),
         "of_verify_column_value": (C.c_int, [C.c_int, u64p, u64p, C.c_size_t, u64p]),
+        "of_pos_bytes_to_field": (C.c_size_t, [u8p, C.c_size_t, u64p]),
+        "of_pos_field_to_bytes": (None, [u64p, C.c_size_t, u8p, C.c_size_t]),
+        "of_pos_default_dims": (None, [C.c_size_t, szp, szp, szp]),
+        "of_pos_column_indices": (C.c_size_t, [C.c_uint64, C.c_size_t, C.c_size_t, u64p]),
+        "of_pos_side_vectors": (None, [C.c_int, u64p, C.c_size_t, C.c_size_t, u64p, u64p]),
         "of_sdig_n_col_opens": (C.c_size_t, [C.c_int]),
         "of_sdig_new_np": (C.c_size_t, [C.c_int, C.c_int, C.c_size_t]),
         "of_sdig_levels": (C.c_int, [C.POINTER(OfEnc)]),
@@ -477,3 +482,54 @@ def standard_transcript(n_col_opens: int, root: bytes) -> Transcript:
     tr.append_message(b"polycommit", root)
     tr.append_message(b"ncols", int(n_col_opens).to_bytes(8, "big"))
     return tr
+
+
+# ---------------------------------------------------------------- proof-of-storage producers
+def pos_bytes_to_field(data: bytes) -> np.ndarray:
+    n = (len(data) + 6) // 7
+    out = np.zeros(max(n, 1), np.uint64)
+    ptr, keep = p8(data if data else b"\x00")
+    lib().of_pos_bytes_to_field(ptr, len(data), p64(out))
+    return out[:n]
+
+
+def pos_field_to_bytes(elems: np.ndarray, expected_len: int) -> bytes:
+    a = np.ascontiguousarray(elems, dtype=np.uint64).reshape(-1)
+    out = np.zeros(max(expected_len, 1), np.uint8)
+    lib().of_pos_field_to_bytes(p64(a) if a.size else None, a.size, out.ctypes.data_as(u8p), expected_len)
+    return out[:expected_len].tobytes()
+
+
+def pos_default_dims(field_len: int):
+    a, b, c = C.c_size_t(), C.c_size_t(), C.c_size_t()
+    lib().of_pos_default_dims(field_len, C.byref(a), C.byref(b), C.byref(c))
+    return a.value, b.value, c.value
+
+
+def pos_column_indices(seed: int, amount: int, max_index: int):
+    out = np.zeros(max(amount, 1), np.uint64)
+    n = lib().of_pos_column_indices(seed, amount, max_index, p64(out))
+    return [int(v) for v in out[:n]]
+
+
+def pos_side_vectors(fid: int, x: np.ndarray, n_rows: int, n_cols: int):
+    nl = limbs(fid)
+    left = np.zeros(max(n_rows, 1) * nl, np.uint64)
+    right = np.zeros(max(n_cols, 1) * nl, np.uint64)
+    lib().of_pos_side_vectors(fid, p64(np.ascontiguousarray(x, dtype=np.uint64)), n_rows, n_cols,
+                              p64(left), p64(right))
+    return left[:n_rows * nl], right[:n_cols * nl]
+
+
+def collapse(fid: int, m: np.ndarray, tensor: np.ndarray, n_rows: int, width: int) -> np.ndarray:
+    out = np.zeros(width * limbs(fid), np.uint64)
+    lib().of_collapse_columns(fid, p64(np.ascontiguousarray(m, dtype=np.uint64)),
+                              p64(np.ascontiguousarray(tensor, dtype=np.uint64)), p64(out), n_rows, width)
+    return out
+
+
+def hash_columns(fid: int, m: np.ndarray, n_rows: int, n_cols: int) -> bytes:
+    out = np.zeros(32 * n_cols, np.uint8)
+    lib().of_hash_columns(fid, p64(np.ascontiguousarray(m, dtype=np.uint64)), n_rows, n_cols,
+                          out.ctypes.data_as(u8p))
+    return out.tobytes()

@@ -114,6 +114,17 @@ def test_sdig_parameters_match_oracle(api, oracle):
                 assert api.SdigEncoding.n_per_row_for(fid, n, code) == L.of_sdig_new_np(fid, code, n)
 
 
+def test_pos_host_functions_match_oracle(native, oracle):
+    """get_aspect_ratio_default_from_field_len and get_column_indicies_from_random_seed are
+    host-only (networking/server.rs:1139-1170, client.rs:443-456)."""
+    from lcpc_proof_of_storage_amd import pos
+    for n in [1, 2, 5, 86, 1000, 4097, (1 << 30) // 8, 153391690, 10**9]:
+        assert pos.get_aspect_ratio_default_from_field_len(n) == oracle.pos_default_dims(n)
+    for seed, amount, mx in [(1337, 256, 32768), (1, 4, 10), (9, 10, 5), (3, 0, 7)]:
+        assert pos.get_column_indicies_from_random_seed(seed, amount, mx) == \
+            oracle.pos_column_indices(seed, amount, mx)
+
+
 def test_transcript_matches_oracle(api, oracle):
     """Merlin framing through both STROBE paths (records inside / across the 166-byte rate)."""
     rng = np.random.default_rng(4)

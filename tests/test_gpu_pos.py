@@ -1,0 +1,135 @@
+"""GPU parity of the proof-of-storage producers (proof-of-storage/src) against the oracle."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+FT63 = 0
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def pos(gpu):
+    from lcpc_proof_of_storage_amd import pos as P
+    return P
+
+
+def test_bytes_to_field_and_back(pos, oracle):
+    rng = np.random.default_rng(1)
+    for n in [1, 6, 7, 8, 55, 56, 57, 111, 112, 113, 999, 100003, 1 << 20]:
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        el = pos.convert_byte_vec_to_field_elements_vec(data)
+        assert np.array_equal(el.reshape(-1), oracle.pos_bytes_to_field(data))
+        assert pos.convert_field_elements_vec_to_byte_vec(el, n) == data
+
+
+def test_bytes_to_field_device(gpu, oracle, hipmem):
+    import ctypes as C
+    from lcpc_proof_of_storage_amd import _native as N
+    rng = np.random.default_rng(2)
+    n = 7 * 100000 + 3
+    data = rng.integers(0, 256, n, dtype=np.uint8)
+    d_in = hipmem.to_device(data)
+    out = np.zeros((n + 6) // 7, np.uint64)
+    d_out = hipmem.to_device(out)
+    try:
+        assert N.load().lcpc_pos_bytes_to_field_device(C.c_void_p(d_in), n, C.c_void_p(d_out), None) == 0
+        assert np.array_equal(hipmem.to_host(d_out, out), oracle.pos_bytes_to_field(data.tobytes()))
+    finally:
+        hipmem.free(d_in)
+        hipmem.free(d_out)
+
+
+def test_default_dims_and_columns(pos, oracle):
+    for n in [1, 5, 86, 1000, 4097, (1 << 30) // 8, 153391690]:
+        assert pos.get_aspect_ratio_default_from_field_len(n) == oracle.pos_default_dims(n)
+    assert pos.get_aspect_ratio_default_from_file_len(1 << 30) == (16384, 32768, 309)
+    for seed, amount, mx in [(1337, 256, 32768), (1, 4, 10), (9, 10, 5)]:
+        assert pos.get_column_indicies_from_random_seed(seed, amount, mx) == \
+            oracle.pos_column_indices(seed, amount, mx)
+
+
+@pytest.mark.parametrize("fid", [0, 1, 3])
+def test_side_vectors(pos, oracle, fid):
+    x = oracle.ChaCha(seed_u64=5).field_random(fid, 1)
+    left, right = pos.form_side_vectors_for_polynomial_evaluation_from_point(x, 37, 64, fid)
+    ol, orr = oracle.pos_side_vectors(fid, x, 37, 64)
+    assert np.array_equal(left.reshape(-1), ol) and np.array_equal(right.reshape(-1), orr)
+
+
+@pytest.mark.parametrize("fid", [0, 1, 3, 4])
+@pytest.mark.parametrize("log_n", [0, 1, 2, 5, 11, 12, 13, 16])
+def test_ifft_oi_matches_oracle(pos, oracle, fid, log_n):
+    n = 1 << log_n
+    rows = 3
+    nl = oracle.limbs(fid)
+    data = oracle.random_coeffs(fid, rows * n, 40 + log_n)
+    got = pos.ifft_oi_rows(data.reshape(rows, n, nl), fid)
+    for r in range(rows):
+        want = oracle.ifft_oi(fid, data[r * n * nl:(r + 1) * n * nl])
+        assert np.array_equal(got[r].reshape(-1), want)
+
+
+def test_ifft_oi_errors(gpu, pos):
+    with pytest.raises(gpu.FFTError):
+        pos.ifft_oi_rows(np.zeros((1, 6, 1), np.uint64))
+
+
+@pytest.mark.parametrize("np_,nc", [(4, 8), (8, 16), (1024, 2048), (8192, 32768)])
+def test_eval_identity_and_parity(gpu, pos, oracle, np_, nc):
+    """networking/tests.rs:374-466 on the GPU, and u^T Enc(M) bit-exact vs the oracle."""
+    n = 32 if np_ <= 8 else np_ * 7 + 5
+    coeffs = oracle.random_coeffs(FT63, n, 11)
+    comm = pos.convert_file_data_to_commit(coeffs, pos.Commit(), pos.Specified(np_, nc))
+    ocomm = oracle.Commit(oracle.Encoding.ligero(FT63, np_, nc), coeffs)
+    assert comm.get_root() == ocomm.root()
+    x = oracle.ChaCha(seed_u64=1337, rounds=8).field_random(FT63, 1)
+    left, right = pos.form_side_vectors_for_polynomial_evaluation_from_point(x, comm.get_n_rows(), np_)
+    r = pos.verifiable_polynomial_evaluation(comm, left)
+    assert np.array_equal(r.reshape(-1), oracle.collapse(FT63, ocomm.comm, left, ocomm.n_rows, nc))
+    dec = pos.decode_row(r)
+    d = oracle.from_mont(FT63, dec.reshape(-1))
+    assert all(v == 0 for v in d[np_:])
+    p = 5102708120182849537
+    got = sum(a * b for a, b in zip(d, oracle.from_mont(FT63, right.reshape(-1)))) % p
+    xv = oracle.from_mont(FT63, x)[0]
+    want = 0
+    for c in reversed(oracle.from_mont(FT63, coeffs)):
+        want = (want * xv + c) % p
+    assert got == want
+
+
+def test_request_types(gpu, pos, oracle):
+    """CommitRequestType::{Leaves, ColumnsWithoutPath, ColumnsWithPath} (lcpc_online.rs:80-239)."""
+    coeffs = oracle.random_coeffs(FT63, 5000, 3)
+    np_, nc = 128, 256
+    ocomm = oracle.Commit(oracle.Encoding.ligero(FT63, np_, nc), coeffs)
+    cols = oracle.pos_column_indices(1337, 16, nc)
+    leaves = pos.convert_file_data_to_commit(coeffs, pos.Leaves(cols), pos.Specified(np_, nc))
+    hashes = ocomm.hashes
+    assert leaves == [hashes[32 * c:32 * c + 32] for c in cols]
+    got = pos.convert_file_data_to_commit(coeffs, pos.ColumnsWithoutPath(cols), pos.Specified(np_, nc))
+    m = ocomm.comm.reshape(ocomm.n_rows, nc)
+    for k, c in enumerate(cols):
+        assert np.array_equal(got[k].reshape(-1), m[:, c])
+    opened = pos.convert_file_data_to_commit(coeffs, pos.ColumnsWithPath(cols), pos.Specified(np_, nc))
+    assert pos.client_online_verify_column_paths(ocomm.root(), cols, opened)
+    assert not pos.client_online_verify_column_paths(ocomm.root(), cols[::-1], opened)
+    comm = pos.convert_file_data_to_commit(coeffs, pos.Commit(), pos.Specified(np_, nc))
+    for k, c in enumerate(cols):
+        one = comm.open_column(c)
+        assert np.array_equal(one.col, opened[k].col) and one.path == opened[k].path
+
+
+def test_test_txt_golden(gpu, pos):
+    g = json.load(open(os.path.join(HERE, "golden", "golden.json")))["pos_test_txt_square"]
+    data = open(os.path.join(HERE, "golden", "pos_test.txt"), "rb").read()
+    el = pos.convert_byte_vec_to_field_elements_vec(data)
+    assert hashlib.sha256(el.tobytes()).hexdigest() == g["elems_sha256"]
+    comm = pos.convert_file_data_to_commit(el, pos.Commit(), pos.Square())
+    assert [comm.get_n_rows(), comm.get_n_per_row(), comm.get_n_cols()] == g["dims"]
+    assert comm.get_root().hex() == g["root"]
+    assert hashlib.sha256(comm.comm.tobytes()).hexdigest() == g["comm_sha256"]
