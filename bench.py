@@ -42,9 +42,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--log-len", type=int, default=24)
     ap.add_argument("--field", default="Ft127")
-    ap.add_argument("--code", choices=["ligero", "sdig"], default="ligero",
+    ap.add_argument("--code", choices=["ligero", "sdig", "pos"], default="ligero",
                     help="ligero: R-S / NTT rows (the BASELINE metric, cfg3); sdig: Brakedown "
-                         "SdigCode3 expander code, seed 0 (cfg4)")
+                         "SdigCode3 expander code, seed 0 (cfg4); pos: proof-of-storage request "
+                         "on a resident file (cfg5)")
+    ap.add_argument("--pos-bytes", type=int, default=1 << 30, help="file size for --code pos")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the cores available (max 16)")
     ap.add_argument("--no-prof", action="store_true", help="disable HIP-event kernel timing")
@@ -107,6 +109,127 @@ def job_throughput(n_per_step, steps, world, elapsed):
     return n_per_step * steps * world / elapsed
 
 
+class Workload:
+    """One bench configuration: `step(slot)` runs one pass of the hot path on resident inputs."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def ligero_or_sdig(args, L, torch, rank, local_rank):
+    """cfg3 (Ligero, the BASELINE metric) and cfg4 (Brakedown SdigCode3, seed 0): commit + open
+    of one polynomial (lcpc-2d/src/lib.rs:651-700, 1034-1123)."""
+    fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
+    nl = L.limbs(fid)
+    n = 1 << args.log_len
+    sdig = args.code == "sdig"
+    enc = L.SdigEncoding.new(fid, n, 0) if sdig else L.LigeroEncoding.new(fid, n)
+    n_rows, n_per_row, n_cols = enc.get_dims(n)
+    nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
+    # synthetic inputs (host RNG of the product library), then resident in HBM
+    coeffs = L.field_random(fid, n, replica_seed(rank))
+    outer = L.field_random(fid, n_rows, 7)  # prove accepts any outer tensor of n_rows elements
+    d_coeffs = torch.from_numpy(coeffs.view(np.int64)).to(f"cuda:{local_rank}")
+
+    def step(slot):
+        c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+        root = c.get_root()
+        tr = L.Transcript(b"test transcript")
+        tr.append_message(b"polycommit", root)
+        tr.append_message(b"ncols", nco.to_bytes(8, "big"))
+        c.prove(outer, enc, tr)
+        return root
+
+    def cpu_baseline(O):
+        o_enc = (O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3) if sdig
+                 else O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt))
+        t1 = time.perf_counter()
+        oc = O.Commit(o_enc, coeffs.reshape(-1))
+        oc.prove(o_enc, outer.reshape(-1), O.standard_transcript(nco, oc.root()))
+        return time.perf_counter() - t1, oc.root(), f"one full commit+open of the same 2^{args.log_len} {args.field} workload"
+
+    B = 8 * nl
+    name = (f"Brakedown (SdigCode3, seed 0) commit+open, {args.field}, 2^{args.log_len} coeffs, " if sdig
+            else f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho=1/2, ")
+    return Workload(
+        units=n, unit="field-elements/s", bytes_per_unit=B,
+        metric=("committed field-elements/s (commit+open), 2^24-coeff Brakedown (cfg4)" if sdig else
+                "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU"),
+        dtype=f"u64x{nl} ({args.field} Montgomery limbs)",
+        data=f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), resident in HBM",
+        config={"workload": name + f"{n_rows}x{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, "
+                                   f"BLAKE3 Merkle",
+                "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
+                "n_col_opens": nco, "n_degree_tests": ndt},
+        step=step, cpu_baseline=cpu_baseline,
+        enc_kernels=("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b"),
+        enc_kernel_desc=("sdig_encode = transpose + 13 SpMM / Reed-Solomon levels (per commit, all rows)" if sdig
+                         else f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
+        # SURVEY §8(d): encode bytes per commit (read the coefficients, write the codeword; SDIG
+        # also streams its code matrices once: 16-B values + 4-B indices)
+        algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B + (enc.matrix_nnz * (B + 4) if sdig else 0),
+        traffic_key=(n, args.field, args.code))
+
+
+def pos_workload(args, L, torch, rank, local_rank):
+    """cfg5: one proof-of-storage server request on a resident file (networking/server.rs:670-730):
+    pack the bytes into WriteableFt63 elements, commit with the default dims, evaluate u^T Enc(M)
+    at a point, and open the client's 256 columns with Merkle paths (client.rs:443-456)."""
+    from lcpc_proof_of_storage_amd import pos as P
+    n_bytes = args.pos_bytes
+    n_el = -(-n_bytes // 7)
+    np_, nc, snd = P.get_aspect_ratio_default_from_file_len(n_bytes)
+    enc = L.LigeroEncoding.new_from_dims(L.FT63, np_, nc)
+    n_rows = -(-n_el // np_)
+    rng = np.random.default_rng(1 + rank)
+    host = rng.integers(0, 256, n_bytes, dtype=np.uint8)
+    dev = f"cuda:{local_rank}"
+    d_bytes = torch.from_numpy(host).to(dev)
+    slots = [torch.empty(n_el, dtype=torch.int64, device=dev) for _ in range(max(1, args.pipeline))]
+    x = L.field_random(L.FT63, 1, 1337)
+    left, _ = P.form_side_vectors_for_polynomial_evaluation_from_point(x, n_rows, nc)
+    cols = P.get_column_indicies_from_random_seed(1337, 256, nc)
+    from lcpc_proof_of_storage_amd import _native
+    lib = _native.load()
+
+    def step(slot):
+        d_el = slots[slot]
+        rc = lib.lcpc_pos_bytes_to_field_device(d_bytes.data_ptr(), n_bytes, d_el.data_ptr(), None)
+        if rc:
+            raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
+        c = L.LcCommit.commit_device(d_el.data_ptr(), n_el, enc)
+        P.verifiable_polynomial_evaluation(c, left)
+        c.open_columns(cols)
+        return c.get_root()
+
+    def cpu_baseline(O):
+        # bounded sample: the first 1/16 of the file (rows are independent; same dims)
+        sample = host[: n_bytes // 16]
+        el = O.pos_bytes_to_field(sample.tobytes())
+        o_enc = O.Encoding.ligero(0, np_, nc)
+        t1 = time.perf_counter()
+        oc = O.Commit(o_enc, el)
+        O.collapse(0, oc.comm, O.pos_side_vectors(0, x.reshape(-1), oc.n_rows, nc)[0], oc.n_rows, nc)
+        dt = time.perf_counter() - t1
+        return dt * n_bytes / len(sample), None, (f"commit + u^T Enc(M) of the first 1/16 of the file "
+                                                  f"({len(sample)} B, {dt:.2f} s), scaled to the whole file")
+
+    return Workload(
+        units=n_el, unit="field-elements/s", bytes_per_unit=8,
+        metric="proof-of-storage server request: committed field-elements/s (pack+commit+eval+256-col open), "
+               f"{n_bytes / 2**30:g} GiB file",
+        dtype="u64 (WriteableFt63 Montgomery limbs)",
+        data=f"synthetic: {n_bytes} random bytes (numpy default_rng(1 + rank)), resident in HBM",
+        config={"workload": f"PoS request on a {n_bytes}-byte file: {n_el} WriteableFt63 elements, default "
+                            f"dims {n_rows}x{np_}->{nc}, u^T Enc(M) at a point, 256 opened columns",
+                "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd},
+        step=step, cpu_baseline=cpu_baseline,
+        enc_kernels=("ntt_pass_a", "ntt_pass_b"),
+        enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)",
+        algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
+        traffic_key=(n_el, "Ft63", "pos"))
+
+
 def main():
     args = parse()
     rank, local_rank, world = dist_env()
@@ -117,31 +240,10 @@ def main():
     torch.cuda.set_device(local_rank)
 
     import lcpc_proof_of_storage_amd as L
-    from lcpc_proof_of_storage_amd import _native
 
     L.set_device(local_rank)
-    fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
-    nl = L.limbs(fid)
-    n = 1 << args.log_len
-    sdig = args.code == "sdig"
-    enc = L.SdigEncoding.new(fid, n, 0) if sdig else L.LigeroEncoding.new(fid, n)
-    n_rows, n_per_row, n_cols = enc.get_dims(n)
-    nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
-
-    # synthetic inputs (host RNG of the product library), then resident in HBM
-    coeffs = L.field_random(fid, n, replica_seed(rank))
-    outer = L.field_random(fid, n_rows, 7)  # prove accepts any outer tensor of n_rows elements
-    d_coeffs = torch.from_numpy(coeffs.view(np.int64)).to(f"cuda:{local_rank}")
+    wl = (pos_workload if args.code == "pos" else ligero_or_sdig)(args, L, torch, rank, local_rank)
     torch.cuda.synchronize()
-
-    def step():
-        c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
-        root = c.get_root()
-        tr = L.Transcript(b"test transcript")
-        tr.append_message(b"polycommit", root)
-        tr.append_message(b"ncols", nco.to_bytes(8, "big"))
-        pf = c.prove(outer, enc, tr)
-        return c, pf, root
 
     prof = not args.no_prof
     n_workers = max(1, args.pipeline)
@@ -157,10 +259,10 @@ def main():
     ready = threading.Barrier(n_workers + 1)
     start = threading.Event()
 
-    def worker():
+    def worker(slot):
         try:
             for _ in range(warm_each):
-                step()
+                wl.step(slot)
         except Exception as e:  # surface after the join
             errors.append(e)
         ready.wait()
@@ -171,14 +273,12 @@ def main():
                     return
                 todo[0] -= 1
             try:
-                c, pf, r = step()
-                roots.append(r)
-                del c, pf
+                roots.append(wl.step(slot))
             except Exception as e:
                 errors.append(e)
                 return
 
-    workers = [threading.Thread(target=worker) for _ in range(n_workers)]
+    workers = [threading.Thread(target=worker, args=(i,)) for i in range(n_workers)]
     for w in workers:
         w.start()
     ready.wait()
@@ -207,17 +307,15 @@ def main():
         L.prof_reset()
         L.prof_enable(True)
         for _ in range(args.roofline_steps):
-            step()
+            wl.step(0)
         L.prof_enable(False)
         iso = L.prof_stats()
     elapsed = max_over_ranks(dist, elapsed, f"cuda:{local_rank}")
-    value = job_throughput(n, args.steps, world, elapsed)
-    B = 8 * nl
+    value = job_throughput(wl.units, args.steps, world, elapsed)
     out = {
-        "metric": ("committed field-elements/s (commit+open), 2^24-coeff Brakedown (cfg4)" if sdig else
-                   "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU"),
+        "metric": wl.metric,
         "value": value,
-        "unit": "field-elements/s",
+        "unit": wl.unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": warmup_done,
@@ -226,59 +324,45 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": f"u64x{nl} ({args.field} Montgomery limbs)",
-        "data": f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), resident in HBM",
-        "config": {
-            "workload": (f"Brakedown (SdigCode3, seed 0) commit+open, {args.field}, 2^{args.log_len} coeffs, "
-                         if sdig else f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho=1/2, ")
-                        +
-                        f"{n_rows}x{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, BLAKE3 Merkle",
-            "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
-            "n_col_opens": nco, "n_degree_tests": ndt,
-            "parallelism": f"replicas x{world} (independent commitments per GPU, {args.pipeline} in flight, "
-                           f"{args.stream_mode} streams)",
-        },
-        "mb_per_s": value * B / 1e6,
+        "dtype": wl.dtype,
+        "data": wl.data,
+        "config": dict(wl.config, parallelism=f"replicas x{world} (independent commitments per GPU, "
+                                              f"{args.pipeline} in flight, {args.stream_mode} streams)"),
+        "mb_per_s": value * wl.bytes_per_unit / 1e6,
     }
 
-    # ---- roofline of the dominant kernel (encode = pass A + pass B, HIP events on the lib stream)
+    # ---- roofline of the dominant kernel (the encode, HIP events on the launching stream)
     if stats:
         out["kernels_timed_region"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]}
                                        for k, v in stats.items()}
     if iso:
         ki = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in iso.items()}
         out["kernels"] = ki
-        enc_kernels = ("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b")
-        enc_ms = sum(ki[k]["avg_ms"] for k in enc_kernels if k in ki)
-        # encode bytes per commit (read the coefficients, write the codeword;
-        # SDIG also streams its code matrices once: 16-B values + 4-B indices)
-        algo = n_rows * n_per_row * B + n_rows * n_cols * B + (enc.matrix_nnz * (B + 4) if sdig else 0)
+        enc_ms = sum(ki[k]["avg_ms"] for k in wl.enc_kernels if k in ki)
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):
             try:
                 tj = json.load(open(tpath))
-                if (tj.get("config_len") == n and tj.get("field") == args.field
-                        and tj.get("code", "ligero") == args.code):
+                if (tj.get("config_len"), tj.get("field"), tj.get("code", "ligero")) == wl.traffic_key:
                     traffic = tj.get("ntt_encode_bytes_per_launch")
             except Exception:
                 traffic = None
-        achieved = algo / (enc_ms * 1e-3) / 1e9 if enc_ms else None
+        achieved = wl.algo_bytes / (enc_ms * 1e-3) / 1e9 if enc_ms else None
         tr_ms = None
         if stats:
-            tr_ms = sum(stats[k][0] / max(stats[k][1], 1) for k in enc_kernels if k in stats)
+            tr_ms = sum(stats[k][0] / max(stats[k][1], 1) for k in wl.enc_kernels if k in stats)
         out["roofline"] = {
-            "kernel": ("sdig_encode = transpose + 13 SpMM / Reed-Solomon levels (per commit, all rows)" if sdig
-                       else f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
+            "kernel": wl.enc_kernel_desc,
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": traffic,
-            "algorithmic_bytes": algo,
+            "algorithmic_bytes": wl.algo_bytes,
             "avg_ms": enc_ms,
-            "launches": min(ki.get(k, {}).get("launches", 0) for k in enc_kernels),
+            "launches": min(ki.get(k, {}).get("launches", 0) for k in wl.enc_kernels),
             "measured": f"HIP events on the launching stream, {args.roofline_steps} serial steps after the "
                         f"timed region (same process, inputs and kernels)",
             "timed_region_avg_ms": tr_ms,
@@ -292,23 +376,16 @@ def main():
 
         cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         O.lib().of_set_threads(cores)
-        o_enc = (O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3) if sdig
-                 else O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt))
-        t1 = time.perf_counter()
-        oc = O.Commit(o_enc, coeffs.reshape(-1))
-        otr = O.standard_transcript(nco, oc.root())
-        op = oc.prove(o_enc, outer.reshape(-1), otr)
-        cpu_s = time.perf_counter() - t1
+        cpu_s, oroot, sample = wl.cpu_baseline(O)
         out["cpu_baseline"] = {
-            "value": n / cpu_s,
-            "unit": "field-elements/s",
+            "value": wl.units / cpu_s,
+            "unit": wl.unit,
             "cores": cores,
             "kind": "port",
-            "sample": f"one full commit+open of the same 2^{args.log_len} {args.field} workload "
-                      f"({cpu_s:.2f} s on {cores} threads)",
+            "sample": f"{sample} ({cpu_s:.2f} s on {cores} threads)",
         }
-        out["parity_root_vs_oracle"] = oc.root() == root if root is not None else None
-        del op, oc
+        if oroot is not None:
+            out["parity_root_vs_oracle"] = oroot == root if root is not None else None
 
     if rank == 0:
         print(json.dumps(out))
