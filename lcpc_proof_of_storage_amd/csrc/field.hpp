@@ -5,11 +5,11 @@
 // endian), viewed as 2N little-endian u32 words.  Every result is fully reduced (< p), as
 // ff_derive's, so the words written back are bit-identical to the reference's.
 //
-// Arithmetic: CIOS Montgomery multiplication on 32-bit words with v_mad_u64_u32
-// (32x32+64 -> 64), add/sub with carry chains.  Every prime the reference declares has
-// p = 1 mod 2^32, so -p^-1 mod 2^32 = 0xffffffff and p[0] = 1: the reduction step's quotient
-// is m = -t0 and m*p[0] + t0 contributes only the carry (t0 != 0); the generic path stays for
-// completeness.
+// Arithmetic: Montgomery multiplication on 32-bit words with v_mad_u64_u32 (32x32+64 -> 64 plus
+// carry-out), add/sub with carry chains.  Every prime the reference declares has p = 1 mod 2^32,
+// so -p^-1 mod 2^32 = 0xffffffff and p[0] = 1: the quotient word is m = -t0 and m*p[0] + t0
+// contributes only a carry.  Those fields use product scanning (fe_mul_fips); CIOS
+// (fe_mul_cios) is the generic path.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -94,9 +94,9 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   return (uint64_t)a * (uint64_t)b + c;
 }
 
-// Montgomery product a*b*R^-1 mod p, R = 2^(32N)  (CIOS, 32-bit words)
+// Montgomery product a*b*R^-1 mod p, R = 2^(32N)  (CIOS, 32-bit words): any odd p
 template <class F>
-__device__ __forceinline__ Fe<F> fe_mul(const Fe<F>& a, const Fe<F>& b) {
+__device__ __forceinline__ Fe<F> fe_mul_cios(const Fe<F>& a, const Fe<F>& b) {
   constexpr int N = F::N;
   uint32_t t[N + 2];
 #pragma unroll
@@ -152,6 +152,91 @@ __device__ __forceinline__ Fe<F> fe_mul(const Fe<F>& a, const Fe<F>& b) {
 #pragma unroll
   for (int i = 0; i < N; i++) r.v[i] = take_u ? u.v[i] : t[i];
   return r;
+}
+
+// v_mad_u64_u32 with its carry-out (the compiler's own selection for a 64-bit multiply-add
+// discards the carry, so every accumulation step would cost extra adds and moves)
+__device__ __forceinline__ uint64_t mad_co_vv(uint32_t a, uint32_t b, uint64_t c, uint64_t &cm) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cm) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint64_t mad_co_vs(uint32_t a, uint32_t b, uint64_t c, uint64_t &cm) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cm) : "v"(a), "s"(b), "v"(c));
+  return d;
+}
+// x + carry (the SGPR lane mask written by mad_co_*)
+__device__ __forceinline__ uint32_t add_carry(uint32_t x, uint64_t cm) {
+  uint32_t d;
+  uint64_t co;
+  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(d), "=s"(co) : "v"(x), "s"(cm));
+  return d;
+}
+
+// Montgomery product for p = 1 mod 2^32 (every field the reference declares): finely integrated
+// product scanning.  Column k accumulates a_i b_(k-i) and m_i p_(k-i) into a 96-bit (acc, r2)
+// with one carry-out mad + one add-with-carry per product; for k < N the quotient word is
+// m_k = -acc mod 2^32 (-p^-1 = -1 mod 2^32) and m_k p_0 = m_k only clears the low word, leaving
+// a carry iff it was nonzero.  Each carry is folded into r2 one product later, so the SGPR a
+// mad writes is not read by the very next instruction.  tools/microbench/femul_variants.hip:
+// Ft127 366 -> 465 G mul/s on MI355X, bit-identical to the CIOS form.
+template <class F>
+__device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
+  constexpr int N = F::N;
+  uint32_t m[N], out[N];
+  uint64_t acc = 0;
+  uint32_t r2 = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N; k++) {
+    uint64_t cprev = 0, ccur;
+    bool have = false;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (j < 0 || j >= N) continue;
+      acc = mad_co_vv(a.v[i], b.v[j], acc, ccur);
+      if (have) r2 = add_carry(r2, cprev);
+      cprev = ccur;
+      have = true;
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i >= k || j < 1 || j >= N) continue;
+      acc = mad_co_vs(m[i], F::P[j], acc, ccur);
+      if (have) r2 = add_carry(r2, cprev);
+      cprev = ccur;
+      have = true;
+    }
+    if (have) r2 = add_carry(r2, cprev);
+    if (k < N) {
+      const uint32_t lo = (uint32_t)acc;
+      m[k] = 0u - lo;
+      acc = ((acc >> 32) | ((uint64_t)r2 << 32)) + (uint64_t)(lo != 0u);
+    } else {
+      out[k - N] = (uint32_t)acc;
+      acc = (acc >> 32) | ((uint64_t)r2 << 32);
+    }
+    r2 = 0;
+  }
+  // out + acc * 2^(32N) < 2p: one conditional subtraction
+  Fe<F> u, r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) u.v[i] = __builtin_subc(out[i], F::P[i], br, &br);
+  const bool take_u = ((uint32_t)acc != 0u) | (br ^ 1u);
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = take_u ? u.v[i] : out[i];
+  return r;
+}
+
+template <class F>
+__device__ __forceinline__ Fe<F> fe_mul(const Fe<F>& a, const Fe<F>& b) {
+  if constexpr (F::NP == 0xffffffffu && F::P[0] == 1u)
+    return fe_mul_fips<F>(a, b);
+  else
+    return fe_mul_cios<F>(a, b);
 }
 
 template <class F>
