@@ -35,7 +35,22 @@ __global__ __launch_bounds__(256) void k_collapse_partial(const uint32_t *__rest
   Fe<F> acc[T];
 #pragma unroll
   for (int t = 0; t < T; t++) acc[t] = fe_zero<F>();
-  for (size_t r = r0; r < r1; r++) {
+  // K rows per step, one Montgomery reduction per K products (fe_dot, lazy reduction)
+  constexpr int K = fe_dot_kmax<F>() < 4 ? fe_dot_kmax<F>() : 4;
+  size_t r = r0;
+  for (; r + K <= r1; r += K) {
+    Fe<F> x[K];
+#pragma unroll
+    for (int q = 0; q < K; q++) x[q] = fe_load<F>(coeffs, (r + q) * n_per_row + c);
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+      Fe<F> w[K];
+#pragma unroll
+      for (int q = 0; q < K; q++) w[q] = fe_load<F>(tensors, t * n_rows + r + q);
+      acc[t] = fe_add<F>(acc[t], fe_dot<F, K>(x, w));
+    }
+  }
+  for (; r < r1; r++) {
     const Fe<F> x = fe_load<F>(coeffs, r * n_per_row + c);
 #pragma unroll
     for (int t = 0; t < T; t++) acc[t] = fe_add<F>(acc[t], fe_mul<F>(x, fe_load<F>(tensors, t * n_rows + r)));

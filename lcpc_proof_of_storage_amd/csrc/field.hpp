@@ -231,6 +231,71 @@ __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
   return r;
 }
 
+// Largest K with K * p < R = 2^(32N) (a safe bound from the top word): a sum of K products,
+// each < p^2, stays below p R, so one Montgomery reduction of the sum lands in [0, 2p).
+template <class F>
+constexpr int fe_dot_kmax() {
+  return (int)((1ull << 32) / ((uint64_t)F::P[F::N - 1] + 1));
+}
+
+// sum_k a[k] b[k] R^-1 mod p with ONE reduction (lazy: the K double-width products are added
+// before reducing): K N^2 + N (N - 1) carry-out mads and one final subtraction, instead of K
+// full Montgomery products and K - 1 modular additions.  Requires p = 1 mod 2^32 and
+// K <= fe_dot_kmax<F>() (Ft127: 2, Ft63: 3, Ft255: 2, Ft253_192: 7).
+template <class F, int K>
+__device__ __forceinline__ Fe<F> fe_dot(const Fe<F>* a, const Fe<F>* b) {
+  constexpr int N = F::N;
+  static_assert(F::NP == 0xffffffffu && F::P[0] == 1u, "p = 1 mod 2^32");
+  static_assert(K >= 1 && K <= fe_dot_kmax<F>(), "K products would exceed p R");
+  uint32_t m[N], out[N];
+  uint64_t acc = 0;
+  uint32_t r2 = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N; k++) {
+    uint64_t cprev = 0, ccur;
+    bool have = false;
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        const int j = k - i;
+        if (j < 0 || j >= N) continue;
+        acc = mad_co_vv(a[q].v[i], b[q].v[j], acc, ccur);
+        if (have) r2 = add_carry(r2, cprev);
+        cprev = ccur;
+        have = true;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i >= k || j < 1 || j >= N) continue;
+      acc = mad_co_vs(m[i], F::P[j], acc, ccur);
+      if (have) r2 = add_carry(r2, cprev);
+      cprev = ccur;
+      have = true;
+    }
+    if (have) r2 = add_carry(r2, cprev);
+    if (k < N) {
+      const uint32_t lo = (uint32_t)acc;
+      m[k] = 0u - lo;
+      acc = ((acc >> 32) | ((uint64_t)r2 << 32)) + (uint64_t)(lo != 0u);
+    } else {
+      out[k - N] = (uint32_t)acc;
+      acc = (acc >> 32) | ((uint64_t)r2 << 32);
+    }
+    r2 = 0;
+  }
+  Fe<F> u, r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) u.v[i] = __builtin_subc(out[i], F::P[i], br, &br);
+  const bool take_u = ((uint32_t)acc != 0u) | (br ^ 1u);
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = take_u ? u.v[i] : out[i];
+  return r;
+}
+
 template <class F>
 __device__ __forceinline__ Fe<F> fe_mul(const Fe<F>& a, const Fe<F>& b) {
   if constexpr (F::NP == 0xffffffffu && F::P[0] == 1u)

@@ -27,7 +27,19 @@ __global__ __launch_bounds__(256) void k_spmm(const uint32_t *__restrict__ ptr,
   const uint32_t b = (uint32_t)(t - j * R);
   Fe<F> acc = fe_zero<F>();
   const uint32_t k1 = ptr[j + 1];
-  for (uint32_t k = ptr[j]; k < k1; k++)
+  uint32_t k = ptr[j];
+  // K nonzeros per step, one Montgomery reduction per K products (fe_dot, lazy reduction)
+  constexpr int K = fe_dot_kmax<F>() < 4 ? fe_dot_kmax<F>() : 4;
+  for (; k + K <= k1; k += K) {
+    Fe<F> v[K], xs[K];
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+      v[q] = fe_load<F>(val, k + q);
+      xs[q] = fe_load<F>(x, (size_t)idx[k + q] * R + b);
+    }
+    acc = fe_add<F>(acc, fe_dot<F, K>(v, xs));
+  }
+  for (; k < k1; k++)
     acc = fe_add<F>(acc, fe_mul<F>(fe_load<F>(val, k), fe_load<F>(x, (size_t)idx[k] * R + b)));
   fe_store<F>(y, t, acc);
 }

@@ -27,6 +27,20 @@ __global__ void k_check(const uint32_t* A, const uint32_t* B, size_t n, uint32_t
   Fe<F> x = fe_mul_cios<F>(a, b), y = fe_mul_fips<F>(a, b);
   if (!fe_eq<F>(x, y)) atomicAdd(bad, 1u);
 }
+// fe_dot<F, K> == sum of fe_mul (K = 2 and kmax), on random inputs
+template <class F, int K>
+__global__ void k_check_dot(const uint32_t* A, const uint32_t* B, size_t n, uint32_t* bad) {
+  size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t * K + K > n) return;
+  Fe<F> a[K], b[K];
+  Fe<F> want = fe_zero<F>();
+  for (int q = 0; q < K; q++) {
+    a[q] = fe_load<F>(A, t * K + q); b[q] = fe_load<F>(B, t * K + q);
+    want = fe_add<F>(want, fe_mul_cios<F>(a[q], b[q]));
+  }
+  if (!fe_eq<F>(want, fe_dot<F, K>(a, b))) atomicAdd(bad, 1u);
+}
+
 template <class F>
 void run(const char* name) {
   const size_t n = 1 << 22;
@@ -47,6 +61,11 @@ void run(const char* name) {
   hipMemset(dbad, 0, 4);
   hipLaunchKernelGGL(k_check<F>, dim3(n / 256), dim3(256), 0, 0, dA, dB, n, dbad);
   uint32_t bad = 0; hipMemcpy(&bad, dbad, 4, hipMemcpyDeviceToHost);
+  hipMemset(dbad, 0, 4);
+  hipLaunchKernelGGL((k_check_dot<F, 2>), dim3(n / 256), dim3(256), 0, 0, dA, dB, n, dbad);
+  hipLaunchKernelGGL((k_check_dot<F, fe_dot_kmax<F>() < 8 ? fe_dot_kmax<F>() : 8>), dim3(n / 256), dim3(256), 0, 0, dA, dB, n, dbad);
+  uint32_t bad_dot = 0; hipMemcpy(&bad_dot, dbad, 4, hipMemcpyDeviceToHost);
+  printf("%s: fe_dot mismatches %u (kmax %d)\n", name, bad_dot, fe_dot_kmax<F>());
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   float ms[2];
   for (int v = 0; v < 2; v++) {
