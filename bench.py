@@ -109,6 +109,13 @@ def job_throughput(n_per_step, steps, world, elapsed):
     return n_per_step * steps * world / elapsed
 
 
+def ntt_muls(n):
+    """Montgomery products of one length-n four-step fft_io (the last stage of each pass is
+    multiplication-free): (n/2)(log2 n - 2) butterflies + n inter-pass twiddles."""
+    lg = n.bit_length() - 1
+    return (n // 2) * max(lg - 2, 0) + n
+
+
 class Workload:
     """One bench configuration: `step(slot)` runs one pass of the hot path on resident inputs."""
 
@@ -168,7 +175,10 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
         # encode bytes per commit (read the coefficients, write the codeword; SDIG
         # also streams its code matrices once: 16-B values + 4-B indices)
         algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B + (enc.matrix_nnz * (B + 4) if sdig else 0),
-        traffic_key=(n, args.field, args.code))
+        traffic_key=(n, args.field, args.code),
+        mul_count=(n_rows * enc.matrix_nnz if sdig else n_rows * ntt_muls(n_cols)),
+        mul_model=("one product per nonzero per row" if sdig else
+                   "four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row"))
 
 
 def pos_workload(args, L, torch, rank, local_rank):
@@ -227,7 +237,9 @@ def pos_workload(args, L, torch, rank, local_rank):
         enc_kernels=("ntt_pass_a", "ntt_pass_b"),
         enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)",
         algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
-        traffic_key=(n_el, "Ft63", "pos"))
+        traffic_key=(n_el, "Ft63", "pos"),
+        mul_count=n_rows * ntt_muls(nc),
+        mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row")
 
 
 def main():
@@ -367,6 +379,18 @@ def main():
                         f"timed region (same process, inputs and kernels)",
             "timed_region_avg_ms": tr_ms,
         }
+        if wl.mul_count:
+            # the encode is bound by the 32-bit multiply-add pipe, not HBM: its VALU roofline is
+            # the Montgomery-multiply rate of the field measured in isolation
+            # (tools/microbench/femul_variants.hip, MI355X: Ft63 1390, Ft127 460, Ft255 128 G/s)
+            peak = {"Ft63": 1390.0, "Ft127": 460.0, "Ft255": 128.0}.get(args.field if args.code != "pos" else "Ft63")
+            ach = wl.mul_count / (enc_ms * 1e-3) / 1e9 if enc_ms else None
+            out["roofline_valu"] = {
+                "kernel": wl.enc_kernel_desc, "bound": "valu (v_mad_u64_u32 Montgomery products)",
+                "achieved": ach, "peak": peak, "unit": "G field-mul/s",
+                "frac": ach / peak if ach and peak else None, "muls_per_launch": wl.mul_count,
+                "model": wl.mul_model,
+            }
 
     # ---- CPU baseline: the oracle (C restatement) on the same workload, rank 0 at N = 1
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)

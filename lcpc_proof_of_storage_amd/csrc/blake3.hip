@@ -127,24 +127,33 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
   uint32_t cv[8];
   iv(cv);
   const uint32_t *colp = m + col * col_stride * N;
+  constexpr int EPB = 16 / N;  // elements per 64-byte block
+  // element e of the block starting at word gw: stream word gw + e N - 8 (negative: prefix)
+  auto fetch = [&](size_t gw, Fe<F> *raw) {
+#pragma unroll
+    for (int k = 0; k < EPB; k++) {
+      const long long ew = (long long)gw + k * N - 8;
+      const size_t row = ew < 0 ? n_rows : (size_t)ew / N;
+      raw[k] = row < n_rows ? fe_load<F>(colp, row * row_stride) : fe_zero<F>();
+    }
+  };
+  // the next block's elements are loaded before the current block is compressed, so HBM
+  // latency overlaps the 7 compression rounds
+  Fe<F> cur[EPB], nxt[EPB];
+  fetch(w0, cur);
   for (int b = 0; b < nb; b++) {
     const size_t gw = w0 + 16 * (size_t)b;
+    if (b + 1 < nb) fetch(gw + 16, nxt);
     uint32_t msg[16];
 #pragma unroll
-    for (int k = 0; k < 16 / N; k++) {
-      const long long ew = (long long)gw + k * N - 8;  // element-stream word index
+    for (int k = 0; k < EPB; k++) {
+      const long long ew = (long long)gw + k * N - 8;
       uint32_t w[N];
-      if (ew < 0) {
+      if (ew < 0 || (size_t)ew / N >= n_rows) {
 #pragma unroll
         for (int i = 0; i < N; i++) w[i] = 0;
       } else {
-        const size_t row = (size_t)ew / N;
-        if (row < n_rows) {
-          fe_repr_words<F>(fe_load<F>(colp, row * row_stride), w);
-        } else {
-#pragma unroll
-          for (int i = 0; i < N; i++) w[i] = 0;
-        }
+        fe_repr_words<F>(cur[k], w);
       }
 #pragma unroll
       for (int i = 0; i < N; i++) msg[k * N + i] = w[i];
@@ -154,6 +163,8 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
     uint32_t flags = b == 0 ? CHUNK_START : 0u;
     if (b == nb - 1) flags |= CHUNK_END | (n_chunks == 1 ? ROOT : 0u);
     compress(cv, msg, (uint64_t)chunk, blen, flags);
+#pragma unroll
+    for (int k = 0; k < EPB; k++) cur[k] = nxt[k];
   }
   if (n_chunks == 1) {
     store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);

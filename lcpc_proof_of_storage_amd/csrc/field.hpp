@@ -324,7 +324,7 @@ __device__ __forceinline__ Fe<F> fe_pow(Fe<F> a, uint64_t e) {
 // canonical (non-Montgomery) value of a: a * R^-1 mod p (Montgomery reduction of a
 // single-width value; a < p so the result is < p without a final subtraction)
 template <class F>
-__device__ __forceinline__ Fe<F> fe_from_mont(const Fe<F>& a) {
+__device__ __forceinline__ Fe<F> fe_from_mont_generic(const Fe<F>& a) {
   constexpr int N = F::N;
   uint32_t t[N + 1];
 #pragma unroll
@@ -348,6 +348,53 @@ __device__ __forceinline__ Fe<F> fe_from_mont(const Fe<F>& a) {
 #pragma unroll
   for (int i = 0; i < N; i++) r.v[i] = t[i];
   return r;
+}
+
+// the same reduction in product-scanning form for p = 1 mod 2^32 (b = 1 in fe_mul_fips: only
+// the N (N - 1) quotient products m_i p_j remain, each one carry-out mad)
+template <class F>
+__device__ __forceinline__ Fe<F> fe_from_mont_fips(const Fe<F>& a) {
+  constexpr int N = F::N;
+  uint32_t m[N], out[N];
+  uint64_t acc = 0;
+  uint32_t r2 = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N; k++) {
+    if (k < N) acc += a.v[k];  // acc < 2^40 here: no carry out
+    uint64_t cprev = 0, ccur;
+    bool have = false;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i >= k || j < 1 || j >= N) continue;
+      acc = mad_co_vs(m[i], F::P[j], acc, ccur);
+      if (have) r2 = add_carry(r2, cprev);
+      cprev = ccur;
+      have = true;
+    }
+    if (have) r2 = add_carry(r2, cprev);
+    if (k < N) {
+      const uint32_t lo = (uint32_t)acc;
+      m[k] = 0u - lo;
+      acc = ((acc >> 32) | ((uint64_t)r2 << 32)) + (uint64_t)(lo != 0u);
+    } else {
+      out[k - N] = (uint32_t)acc;
+      acc = (acc >> 32) | ((uint64_t)r2 << 32);
+    }
+    r2 = 0;
+  }
+  Fe<F> r;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = out[i];
+  return r;
+}
+
+template <class F>
+__device__ __forceinline__ Fe<F> fe_from_mont(const Fe<F>& a) {
+  if constexpr (F::NP == 0xffffffffu && F::P[0] == 1u)
+    return fe_from_mont_fips<F>(a);
+  else
+    return fe_from_mont_generic<F>(a);
 }
 
 // Montgomery form of a canonical value a < p: a * R^2 * R^-1

@@ -26,6 +26,7 @@ __global__ void k_check(const uint32_t* A, const uint32_t* B, size_t n, uint32_t
   Fe<F> a = fe_load<F>(A, t), b = fe_load<F>(B, t);
   Fe<F> x = fe_mul_cios<F>(a, b), y = fe_mul_fips<F>(a, b);
   if (!fe_eq<F>(x, y)) atomicAdd(bad, 1u);
+  if (!fe_eq<F>(fe_from_mont_generic<F>(a), fe_from_mont_fips<F>(a))) atomicAdd(bad, 1u);
 }
 // fe_dot<F, K> == sum of fe_mul (K = 2 and kmax), on random inputs
 template <class F, int K>
