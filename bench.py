@@ -47,6 +47,9 @@ def parse():
                          "SdigCode3 expander code, seed 0 (cfg4); pos: proof-of-storage request "
                          "on a resident file (cfg5)")
     ap.add_argument("--pos-bytes", type=int, default=1 << 30, help="file size for --code pos")
+    ap.add_argument("--shard", choices=["none", "rows"], default="none",
+                    help="rows: one Ligero commitment per step with its rows split across the "
+                         "ranks (shard.py; RCCL exchanges; strong scaling)")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the cores available (max 16)")
     ap.add_argument("--no-prof", action="store_true", help="disable HIP-event kernel timing")
@@ -181,6 +184,56 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
                    "four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row"))
 
 
+def shard_workload(args, L, torch, rank, local_rank, dist):
+    """cfg3 with one commitment's rows sharded across the ranks (shard.py): strong scaling."""
+    from lcpc_proof_of_storage_amd.shard import Comm, GpuBackend, RowShardedCommit
+    fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
+    nl = L.limbs(fid)
+    n = 1 << args.log_len
+    enc = L.LigeroEncoding.new(fid, n)
+    n_rows, n_per_row, n_cols = enc.get_dims(n)
+    nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
+    coeffs = L.field_random(fid, n, SEED)           # the same polynomial on every rank
+    rows = np.zeros((n_rows * n_per_row, nl), np.uint64)
+    rows[:n] = coeffs
+    rows = rows.reshape(n_rows, n_per_row * nl)
+    outer = L.field_random(fid, n_rows, 7)
+    be = GpuBackend(enc)
+    comm = Comm(dist, f"cuda:{local_rank}" if dist is not None else "cpu")
+
+    def step(slot):
+        sc = RowShardedCommit(be, comm, n_rows, 8 * nl)
+        root = sc.commit(rows[sc.r_lo:sc.r_hi])
+        tr = None
+        if comm.rank == 0:
+            tr = L.Transcript(b"test transcript")
+            tr.append_message(b"polycommit", root)
+            tr.append_message(b"ncols", nco.to_bytes(8, "big"))
+        sc.prove(outer, tr)
+        sc.close()
+        return root
+
+    def cpu_baseline(O):
+        o_enc = O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
+        t1 = time.perf_counter()
+        oc = O.Commit(o_enc, coeffs.reshape(-1))
+        oc.prove(o_enc, outer.reshape(-1), O.standard_transcript(nco, oc.root()))
+        return time.perf_counter() - t1, oc.root(), f"one full commit+open of the same 2^{args.log_len} {args.field} workload"
+
+    return Workload(
+        units=n, unit="field-elements/s", bytes_per_unit=8 * nl, scaling="strong",
+        metric="committed field-elements/s (commit+open), 2^24-coeff Ligero, rows sharded across GPUs",
+        dtype=f"u64x{nl} ({args.field} Montgomery limbs)",
+        data=f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x})), one polynomial, rows split over ranks",
+        config={"workload": f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, {n_rows}x{n_per_row}->"
+                            f"{n_cols}, rows sharded at BLAKE3 chunk boundaries",
+                "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
+                "n_col_opens": nco, "n_degree_tests": ndt},
+        step=step, cpu_baseline=cpu_baseline, enc_kernels=("ntt_pass_a", "ntt_pass_b"),
+        enc_kernel_desc="ntt_encode = ntt_pass_a + ntt_pass_b (this rank's rows)",
+        algo_bytes=0, traffic_key=None, mul_count=0, mul_model="")
+
+
 def pos_workload(args, L, torch, rank, local_rank):
     """cfg5: one proof-of-storage server request on a resident file (networking/server.rs:670-730):
     pack the bytes into WriteableFt63 elements, commit with the default dims, evaluate u^T Enc(M)
@@ -254,7 +307,11 @@ def main():
     import lcpc_proof_of_storage_amd as L
 
     L.set_device(local_rank)
-    wl = (pos_workload if args.code == "pos" else ligero_or_sdig)(args, L, torch, rank, local_rank)
+    if args.shard == "rows":
+        args.pipeline = 1  # the ranks' collectives must be issued in one order
+        wl = shard_workload(args, L, torch, rank, local_rank, dist)
+    else:
+        wl = (pos_workload if args.code == "pos" else ligero_or_sdig)(args, L, torch, rank, local_rank)
     torch.cuda.synchronize()
 
     prof = not args.no_prof
@@ -323,7 +380,8 @@ def main():
         L.prof_enable(False)
         iso = L.prof_stats()
     elapsed = max_over_ranks(dist, elapsed, f"cuda:{local_rank}")
-    value = job_throughput(wl.units, args.steps, world, elapsed)
+    scaling = getattr(wl, "scaling", "weak")
+    value = job_throughput(wl.units, args.steps, world if scaling == "weak" else 1, elapsed)
     out = {
         "metric": wl.metric,
         "value": value,
@@ -334,12 +392,13 @@ def main():
         "ms_per_step": 1e3 * elapsed / args.steps,
         "pipeline": args.pipeline,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": wl.dtype,
         "data": wl.data,
-        "config": dict(wl.config, parallelism=f"replicas x{world} (independent commitments per GPU, "
-                                              f"{args.pipeline} in flight, {args.stream_mode} streams)"),
+        "config": dict(wl.config, parallelism=(f"rows sharded x{world} (one commitment, shard.py)" if scaling == "strong"
+                                               else f"replicas x{world} (independent commitments per GPU, "
+                                                    f"{args.pipeline} in flight, {args.stream_mode} streams)")),
         "mb_per_s": value * wl.bytes_per_unit / 1e6,
     }
 
@@ -347,7 +406,7 @@ def main():
     if stats:
         out["kernels_timed_region"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]}
                                        for k, v in stats.items()}
-    if iso:
+    if iso and wl.algo_bytes:
         ki = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in iso.items()}
         out["kernels"] = ki
         enc_ms = sum(ki[k]["avg_ms"] for k in wl.enc_kernels if k in ki)
@@ -379,7 +438,7 @@ def main():
                         f"timed region (same process, inputs and kernels)",
             "timed_region_avg_ms": tr_ms,
         }
-        if wl.mul_count:
+        if wl.mul_count:  # noqa: E501
             # the encode is bound by the 32-bit multiply-add pipe, not HBM: its VALU roofline is
             # the Montgomery-multiply rate of the field measured in isolation
             # (tools/microbench/femul_variants.hip, MI355X: Ft63 1390, Ft127 460, Ft255 128 G/s)

@@ -280,6 +280,43 @@ lcpc_status lcpc_pos_columns(const lcpc_encoding *e, const uint64_t *elems, size
                              const uint64_t *idx, size_t n, uint64_t *cols_out,
                              uint8_t *leaves_out);
 
+/* ------------------------------------------------------------------ row shards (multi-GPU)
+ * One process per GPU holds rows [row0, row0 + n_shard_rows) of an n_rows x n_per_row Ligero
+ * coefficient matrix.  With the exchanges done by the caller (lcpc_proof_of_storage_amd/
+ * shard.py over RCCL: chaining values by column block, subtree roots, partial row sums,
+ * challenge broadcasts) these reproduce commit (lcpc-2d/src/lib.rs:651-815) and prove
+ * (:1034-1123) bit for bit.  Shard boundaries must fall on BLAKE3 chunk boundaries of the leaf
+ * message (32 zero bytes || column): lcpc_leaf_chunk_first_row gives them. */
+typedef struct lcpc_shard lcpc_shard;
+size_t lcpc_leaf_n_chunks(lcpc_field f, size_t n_rows);          /* 1-KiB chunks per leaf */
+size_t lcpc_leaf_chunk_first_row(lcpc_field f, size_t chunk);    /* first row of chunk */
+lcpc_status lcpc_shard_new(const lcpc_encoding *e, const uint64_t *coeffs, size_t row0,
+                           size_t n_shard_rows, size_t n_rows_total, lcpc_shard **out);
+void lcpc_shard_free(lcpc_shard *s);
+/* chaining values of leaf chunks [chunk_lo, chunk_hi) of every column: out[chunk][col][32] */
+lcpc_status lcpc_shard_chunk_cvs(const lcpc_shard *s, size_t chunk_lo, size_t chunk_hi,
+                                 uint8_t *out);
+/* leaf digests from all n_chunks chaining values of n_cols columns ([chunk][col][32]) */
+lcpc_status lcpc_leaves_from_cvs(const uint8_t *cvs, size_t n_chunks, size_t n_cols,
+                                 uint8_t *leaves);
+/* partial collapse_columns over the shard's rows; tensors: n_tensors x n_shard_rows */
+lcpc_status lcpc_shard_collapse(const lcpc_shard *s, const uint64_t *tensors, size_t n_tensors,
+                                uint64_t *out);
+/* the shard's rows of columns idx[]: out[k][r] (n x n_shard_rows elements) */
+lcpc_status lcpc_shard_gather_columns(const lcpc_shard *s, const uint64_t *idx, size_t n,
+                                      uint64_t *out);
+/* out[i] = sum_k vecs[k][i] mod p */
+lcpc_status lcpc_field_sum(lcpc_field f, const uint64_t *vecs, size_t n_vecs, size_t len,
+                           uint64_t *out);
+/* the Fiat-Shamir steps of prove: degree-test tensor ("$l//DT" -> ChaCha20 -> Field::random,
+ * lib.rs:1056-1062), absorbing field elements as their repr (lib.rs:1075-1077, 1096-1098) and
+ * the column choice ("$l//CO" -> ChaCha20 -> Uniform(0, n_cols), lib.rs:1101-1110) */
+lcpc_status lcpc_challenge_tensor(lcpc_transcript *tr, lcpc_field f, size_t n, uint64_t *out);
+lcpc_status lcpc_transcript_append_field_elems(lcpc_transcript *tr, const uint8_t *label,
+                                               size_t label_len, lcpc_field f,
+                                               const uint64_t *elems, size_t n);
+lcpc_status lcpc_challenge_columns(lcpc_transcript *tr, size_t n_cols, size_t n, uint64_t *out);
+
 /* ------------------------------------------------------------------ kernel timing
  * HIP-event timing of every kernel launch on the handle streams (off by default). */
 void lcpc_prof_enable(int enable);

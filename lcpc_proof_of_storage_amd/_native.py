@@ -110,6 +110,18 @@ SIGNATURES = {
     "lcpc_ifft_oi_rows": (i32, [i32, u64p, sz, sz]),
     "lcpc_open_columns": (i32, [vp, u64p, sz, u64p, u8p]),
     "lcpc_pos_columns": (i32, [vp, u64p, sz, u64p, sz, u64p, u8p]),
+    "lcpc_leaf_n_chunks": (sz, [i32, sz]),
+    "lcpc_leaf_chunk_first_row": (sz, [i32, sz]),
+    "lcpc_shard_new": (i32, [vp, u64p, sz, sz, sz, C.POINTER(vp)]),
+    "lcpc_shard_free": (None, [vp]),
+    "lcpc_shard_chunk_cvs": (i32, [vp, sz, sz, u8p]),
+    "lcpc_leaves_from_cvs": (i32, [u8p, sz, sz, u8p]),
+    "lcpc_shard_collapse": (i32, [vp, u64p, sz, u64p]),
+    "lcpc_shard_gather_columns": (i32, [vp, u64p, sz, u64p]),
+    "lcpc_field_sum": (i32, [i32, u64p, sz, sz, u64p]),
+    "lcpc_challenge_tensor": (i32, [vp, i32, sz, u64p]),
+    "lcpc_transcript_append_field_elems": (i32, [vp, u8p, sz, i32, u64p, sz]),
+    "lcpc_challenge_columns": (i32, [vp, sz, sz, u64p]),
     "lcpc_prof_enable": (None, [i32]),
     "lcpc_prof_reset": (None, []),
     "lcpc_prof_get": (i32, [C.c_char_p, C.POINTER(C.c_double), u64p]),

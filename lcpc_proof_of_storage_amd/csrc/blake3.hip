@@ -108,18 +108,21 @@ __device__ __forceinline__ void store8(uint32_t *p, const uint32_t v[8]) {
 
 // One thread per (column, chunk).  Message word w of a column: w < 8 is the zero prefix,
 // else word (w-8) % N of element row (w-8) / N.  N in {2, 4, 8} divides both 8 and 16, so
-// every 16-word block holds whole elements.
+// every 16-word block holds whole elements.  The launch covers chunks [chunk0, chunk_end) of
+// messages of n_rows rows; m holds rows [row0, ...) (a row shard: every row those chunks read
+// is present), and chaining values go to cvs[chunk - chunk0][col].
 template <class F>
 __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict__ m,
                                                      size_t n_rows, size_t n_cols,
                                                      size_t row_stride, size_t col_stride,
                                                      uint32_t *__restrict__ cvs,
-                                                     uint8_t *__restrict__ leaves, int n_chunks) {
+                                                     uint8_t *__restrict__ leaves, int n_chunks,
+                                                     size_t row0, int chunk0, int chunk_end) {
   constexpr int N = F::N;
   static_assert(16 % N == 0 && 8 % N == 0, "element must tile a BLAKE3 block");
   const size_t col = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int chunk = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (col >= n_cols || chunk >= n_chunks) return;
+  const int chunk = chunk0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (col >= n_cols || chunk >= chunk_end) return;
   const size_t total_words = 8 + n_rows * N;
   const size_t w0 = (size_t)chunk * 256;
   const size_t cw = total_words - w0 < 256 ? total_words - w0 : 256;
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
     for (int k = 0; k < EPB; k++) {
       const long long ew = (long long)gw + k * N - 8;
       const size_t row = ew < 0 ? n_rows : (size_t)ew / N;
-      raw[k] = row < n_rows ? fe_load<F>(colp, row * row_stride) : fe_zero<F>();
+      raw[k] = row < n_rows ? fe_load<F>(colp, (row - row0) * row_stride) : fe_zero<F>();
     }
   };
   // the next block's elements are loaded before the current block is compressed, so HBM
@@ -166,10 +169,10 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
 #pragma unroll
     for (int k = 0; k < EPB; k++) cur[k] = nxt[k];
   }
-  if (n_chunks == 1) {
+  if (n_chunks == 1 && leaves) {
     store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
   } else {
-    store8(cvs + ((size_t)chunk * n_cols + col) * 8, cv);
+    store8(cvs + ((size_t)(chunk - chunk0) * n_cols + col) * 8, cv);
   }
 }
 
@@ -312,7 +315,7 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
     if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
       prof::Scope ps("leaf_chunks", s);
       hipLaunchKernelGGL((k_leaf_chunks<F>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
-                         col_stride, (uint32_t *)scratch, leaves, n_chunks);
+                         col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
       return hipGetLastError();
     } else {
       return hipErrorInvalidValue;
@@ -322,6 +325,39 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
   prof::Scope ps("leaf_merge", s);
   hipLaunchKernelGGL(k_leaf_merge, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, s,
                      (uint32_t *)scratch, n_cols, n_chunks, leaves);
+  return hipGetLastError();
+}
+
+size_t leaf_n_chunks(int fid, size_t n_rows) {
+  return (8 + n_rows * (size_t)field_words(fid) + 255) / 256;
+}
+
+hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows, size_t n_cols,
+                          size_t stride, size_t chunk_lo, size_t chunk_hi, uint32_t *cvs,
+                          hipStream_t s) {
+  if (n_cols == 0 || chunk_hi <= chunk_lo) return hipSuccess;
+  const int n_chunks = (int)leaf_n_chunks(fid, n_rows);
+  dim3 grid((unsigned)((n_cols + 63) / 64), (unsigned)((chunk_hi - chunk_lo + 3) / 4));
+  return dispatch_field(fid, [&]<class F>() {
+    if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
+      prof::Scope ps("leaf_chunks", s);
+      hipLaunchKernelGGL((k_leaf_chunks<F>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
+                         (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
+                         (int)chunk_hi);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
+  });
+}
+
+hipError_t leaves_from_cvs(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t *leaves,
+                           hipStream_t s) {
+  if (!n_cols) return hipSuccess;
+  if (n_chunks == 1) return hipMemcpyAsync(leaves, cvs, n_cols * 32, hipMemcpyDeviceToDevice, s);
+  prof::Scope ps("leaf_merge", s);
+  hipLaunchKernelGGL(k_leaf_merge, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, s, cvs, n_cols,
+                     n_chunks, leaves);
   return hipGetLastError();
 }
 

@@ -153,6 +153,15 @@ hipError_t collapse_t(const uint32_t *coeffs, size_t n_rows, size_t n_per_row,
 
 }  // namespace
 
+hipError_t collapse_fold_rows(int fid, const uint32_t *vecs, size_t n_vecs, size_t len, uint32_t *out,
+                              hipStream_t s) {
+  return dispatch_field(fid, [&]<class F>() {
+    hipLaunchKernelGGL((k_collapse_fold<F, 1>), dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s,
+                       vecs, n_vecs, len, out);
+    return hipGetLastError();
+  });
+}
+
 size_t collapse_scratch_bytes(int fid, size_t n_rows, size_t n_per_row, int n_tensors) {
   return n_splits_for(n_rows, n_per_row) * (size_t)n_tensors * n_per_row * field_bytes(fid);
 }

@@ -41,6 +41,16 @@ hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, si
 size_t leaf_hash_scratch_bytes(int fid, size_t n_rows, size_t n_cols);
 hipError_t leaf_hashes(int fid, const uint32_t *m, size_t n_rows, size_t n_cols, size_t stride,
                        uint8_t *leaves, void *scratch, hipStream_t s);
+// Row shards: chaining values of chunks [chunk_lo, chunk_hi) of every column's leaf message
+// (messages of n_rows rows in total) from a row-major shard m holding rows [row0, ...);
+// cvs[(chunk - chunk_lo) * n_cols + col] (8 words).  Chunk c starts at message byte 1024 c.
+size_t leaf_n_chunks(int fid, size_t n_rows);
+hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows, size_t n_cols,
+                          size_t stride, size_t chunk_lo, size_t chunk_hi, uint32_t *cvs,
+                          hipStream_t s);
+// leaf digests from all n_chunks chaining values ([chunk][col] layout; cvs is clobbered)
+hipError_t leaves_from_cvs(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t *leaves,
+                           hipStream_t s);
 // same, for a [column][row] matrix (opened columns of a proof)
 hipError_t leaf_hashes_cols(int fid, const uint32_t *cols, size_t n_rows, size_t n_cols,
                             uint8_t *leaves, void *scratch, hipStream_t s);
@@ -55,6 +65,9 @@ size_t collapse_scratch_bytes(int fid, size_t n_rows, size_t n_per_row, int n_te
 hipError_t collapse_rows(int fid, const uint32_t *coeffs, size_t n_rows, size_t n_per_row,
                          const uint32_t *tensors, int n_tensors, uint32_t *out, void *scratch,
                          hipStream_t s);
+// out[c] = sum_k vecs[k][c] (n_vecs vectors of len elements)
+hipError_t collapse_fold_rows(int fid, const uint32_t *vecs, size_t n_vecs, size_t len, uint32_t *out,
+                              hipStream_t s);
 // cols[k][r] = m[r][idx[k]] (m row-major) or m[idx[k]][r] (col_major);
 // paths[k][i] = sibling digests of leaf idx[k]
 hipError_t gather_columns(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,

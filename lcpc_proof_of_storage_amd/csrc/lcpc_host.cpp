@@ -1588,3 +1588,220 @@ lcpc_status lcpc_pos_columns(const lcpc_encoding *e, const uint64_t *elems, size
 }
 
 }  // extern "C"
+
+// ================================================================= row shards (multi-GPU commit)
+// One GPU's share of a Ligero commitment whose rows are split across processes:
+// the shard encodes its rows, computes the BLAKE3 chunk chaining values of the leaf-message
+// chunks its rows cover, its partial row combinations and its rows of opened columns.  The
+// exchanges between shards (chaining values by column block, subtree roots, partial sums,
+// challenge broadcasts) are the caller's (lcpc_proof_of_storage_amd/shard.py, RCCL through
+// torch.distributed); together they reproduce commit / prove bit for bit.
+struct lcpc_shard {
+  const lcpc_encoding *e = nullptr;
+  size_t row0 = 0, n_rows = 0, n_rows_total = 0;
+  DBuf coeffs, comm;
+};
+
+extern "C" {
+
+size_t lcpc_leaf_n_chunks(lcpc_field f, size_t n_rows) {
+  return valid_field(f) ? leaf_n_chunks(f, n_rows) : 0;
+}
+
+size_t lcpc_leaf_chunk_first_row(lcpc_field f, size_t chunk) {
+  // first row of the leaf message at or after byte 1024 * chunk (32-byte zero prefix)
+  if (!valid_field(f) || chunk == 0) return 0;
+  const size_t wb = (size_t)field_bytes(f);
+  return (1024 * chunk - 32 + wb - 1) / wb;
+}
+
+lcpc_status lcpc_shard_new(const lcpc_encoding *e, const uint64_t *coeffs, size_t row0,
+                           size_t n_shard_rows, size_t n_rows_total, lcpc_shard **out) {
+  if (!e || !out || (!coeffs && n_shard_rows)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (e->kind != KIND_RS) return fail(LCPC_ERR_UNSUPPORTED, "row shards: Ligero / R-S encodings only");
+  if (row0 + n_shard_rows > n_rows_total) return fail(LCPC_ERR_INVALID_ARG, "shard rows out of range");
+  Device *dev = e->dev;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  auto sh = std::make_unique<lcpc_shard>();
+  sh->e = e;
+  sh->row0 = row0;
+  sh->n_rows = n_shard_rows;
+  sh->n_rows_total = n_rows_total;
+  const size_t np = e->n_per_row, nc = e->n_cols;
+  const int wb = field_bytes(e->fid);
+  HIP_TRY(sh->coeffs.alloc(dev, n_shard_rows * np * wb + 16));
+  HIP_TRY(sh->comm.alloc(dev, n_shard_rows * nc * wb + 16));
+  if (n_shard_rows) {
+    HIP_TRY(hipMemcpyAsync(sh->coeffs.p, coeffs, n_shard_rows * np * wb, hipMemcpyHostToDevice, lease.s));
+    HIP_TRY(ntt_rows(e->plan, sh->coeffs.as<uint32_t>(), np, np, sh->comm.as<uint32_t>(), nc, n_shard_rows,
+                     lease.s));
+  }
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  sh->coeffs.settle();
+  sh->comm.settle();
+  *out = sh.release();
+  return LCPC_OK;
+}
+
+void lcpc_shard_free(lcpc_shard *s) {
+  if (!s) return;
+  Lease lease(s->e->dev);
+  (void)hipStreamSynchronize(lease.s);
+  delete s;
+}
+
+lcpc_status lcpc_shard_chunk_cvs(const lcpc_shard *s, size_t chunk_lo, size_t chunk_hi,
+                                 uint8_t *out) {
+  if (!s || (!out && chunk_hi > chunk_lo)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  const int fid = s->e->fid;
+  const size_t nc = s->e->n_cols;
+  if (chunk_hi > leaf_n_chunks(fid, s->n_rows_total) || chunk_lo > chunk_hi)
+    return fail(LCPC_ERR_INVALID_ARG, "chunk range");
+  // every row the chunks read must be in the shard
+  const size_t need_lo = lcpc_leaf_chunk_first_row((lcpc_field)fid, chunk_lo);
+  const size_t need_hi = chunk_hi >= leaf_n_chunks(fid, s->n_rows_total)
+                             ? s->n_rows_total
+                             : lcpc_leaf_chunk_first_row((lcpc_field)fid, chunk_hi);
+  if (chunk_hi > chunk_lo && (need_lo < s->row0 || need_hi > s->row0 + s->n_rows))
+    return fail(LCPC_ERR_INVALID_ARG, "the shard does not hold every row of those chunks");
+  if (chunk_hi == chunk_lo) return LCPC_OK;
+  Device *dev = s->e->dev;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf cvs;
+  HIP_TRY(cvs.alloc(dev, (chunk_hi - chunk_lo) * nc * 32));
+  HIP_TRY(leaf_chunk_cvs(fid, s->comm.as<uint32_t>(), s->row0, s->n_rows_total, nc, nc, chunk_lo, chunk_hi,
+                         cvs.as<uint32_t>(), lease.s));
+  HIP_TRY(hipMemcpyAsync(out, cvs.p, (chunk_hi - chunk_lo) * nc * 32, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_leaves_from_cvs(const uint8_t *cvs, size_t n_chunks, size_t n_cols, uint8_t *leaves) {
+  if ((!cvs || !leaves) && n_cols) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (n_chunks == 0) return fail(LCPC_ERR_INVALID_ARG, "n_chunks");
+  if (!n_cols) return LCPC_OK;
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf dc, dl;
+  if ((st = upload(dev, dc, cvs, n_chunks * n_cols * 32))) return st;
+  HIP_TRY(dl.alloc(dev, n_cols * 32));
+  HIP_TRY(leaves_from_cvs(dc.as<uint32_t>(), n_cols, (int)n_chunks, dl.as<uint8_t>(), lease.s));
+  HIP_TRY(hipMemcpyAsync(leaves, dl.p, n_cols * 32, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_shard_collapse(const lcpc_shard *s, const uint64_t *tensors, size_t n_tensors,
+                                uint64_t *out) {
+  // partial collapse_columns over the shard's rows: out[t][c] = sum_{r in shard} t[r] coeffs[r][c]
+  if (!s || !out || (!tensors && s->n_rows)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (n_tensors < 1 || n_tensors > 4) return fail(LCPC_ERR_INVALID_ARG, "1..4 tensors");
+  const int fid = s->e->fid, wb = field_bytes(fid);
+  const size_t np = s->e->n_per_row;
+  Device *dev = s->e->dev;
+  Lease lease(dev, true);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf dt, dout, scratch;
+  lcpc_status st;
+  HIP_TRY(dout.alloc(dev, n_tensors * np * wb));
+  if (s->n_rows == 0) {
+    HIP_TRY(hipMemsetAsync(dout.p, 0, n_tensors * np * wb, lease.s));
+  } else {
+    if ((st = upload(dev, dt, tensors, n_tensors * s->n_rows * wb))) return st;
+    HIP_TRY(scratch.alloc(dev, collapse_scratch_bytes(fid, s->n_rows, np, (int)n_tensors)));
+    HIP_TRY(collapse_rows(fid, s->coeffs.as<uint32_t>(), s->n_rows, np, dt.as<uint32_t>(), (int)n_tensors,
+                          dout.as<uint32_t>(), scratch.p, lease.s));
+  }
+  HIP_TRY(hipMemcpyAsync(out, dout.p, n_tensors * np * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_shard_gather_columns(const lcpc_shard *s, const uint64_t *idx, size_t n, uint64_t *out) {
+  if (!s || (!idx && n) || (!out && n)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  const size_t nc = s->e->n_cols;
+  for (size_t k = 0; k < n; k++)
+    if (idx[k] >= nc) return fail(LCPC_PROVER_COLUMN_NUMBER, "ProverError::ColumnNumber");
+  if (!n || !s->n_rows) return LCPC_OK;
+  const int fid = s->e->fid, wb = field_bytes(fid);
+  Device *dev = s->e->dev;
+  Lease lease(dev, true);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf didx, dcol;
+  lcpc_status st;
+  if ((st = upload(dev, didx, idx, n * 8))) return st;
+  HIP_TRY(dcol.alloc(dev, n * s->n_rows * wb));
+  HIP_TRY(gather_columns(fid, s->comm.as<uint32_t>(), s->n_rows, nc, didx.as<uint64_t>(), n,
+                         dcol.as<uint32_t>(), lease.s));
+  HIP_TRY(hipMemcpyAsync(out, dcol.p, n * s->n_rows * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_field_sum(lcpc_field f, const uint64_t *vecs, size_t n_vecs, size_t len, uint64_t *out) {
+  // out[i] = sum_k vecs[k][i] mod p (folds the shards' partial row combinations)
+  if (!valid_field(f) || (!vecs && n_vecs * len) || (!out && len)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  if (!len) return LCPC_OK;
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  const int wb = field_bytes(f);
+  DBuf dv, dout;
+  if (n_vecs == 0) {
+    std::memset(out, 0, len * wb);
+    return LCPC_OK;
+  }
+  if ((st = upload(dev, dv, vecs, n_vecs * len * wb))) return st;
+  HIP_TRY(dout.alloc(dev, len * wb));
+  // the fold kernel of collapse: partial[split][t][c] with T = 1
+  HIP_TRY(collapse_fold_rows(f, dv.as<uint32_t>(), n_vecs, len, dout.as<uint32_t>(), lease.s));
+  HIP_TRY(hipMemcpyAsync(out, dout.p, len * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_challenge_tensor(lcpc_transcript *tr, lcpc_field f, size_t n, uint64_t *out) {
+  // prove / verify degree-test tensor (lcpc-2d/src/lib.rs:1056-1062, 899-907)
+  if (!tr || !valid_field(f) || (!out && n)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  std::vector<uint64_t> t;
+  challenge_tensor(tr->t, f, n, t);
+  if (n) std::memcpy(out, t.data(), t.size() * 8);
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_challenge_columns(lcpc_transcript *tr, size_t n_cols, size_t n, uint64_t *out) {
+  // column choice (lcpc-2d/src/lib.rs:1101-1110, 932-941)
+  if (!tr || !n_cols || (!out && n)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  std::vector<uint64_t> idx;
+  challenge_columns(tr->t, n_cols, n, idx);
+  if (n) std::memcpy(out, idx.data(), n * 8);
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_transcript_append_field_elems(lcpc_transcript *tr, const uint8_t *label, size_t ln,
+                                               lcpc_field f, const uint64_t *elems, size_t n) {
+  // append_message(label, to_repr(e)) for every e (lcpc-2d/src/lib.rs:1075-1077, 1096-1098)
+  if (!tr || !valid_field(f) || (!elems && n)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  if (!n) return LCPC_OK;
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev, true);
+  HIP_TRY(hipSetDevice(dev->id));
+  const int wb = field_bytes(f);
+  DBuf de;
+  if ((st = upload(dev, de, elems, n * wb))) return st;
+  const uint8_t *repr = nullptr;
+  if ((st = to_repr_host(dev, f, de.as<uint32_t>(), n, &repr))) return st;
+  tr->t.append_messages(label, ln, repr, wb, n);
+  return LCPC_OK;
+}
+
+}  // extern "C"

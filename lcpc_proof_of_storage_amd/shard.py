@@ -1,0 +1,330 @@
+"""Row-sharded Ligero commit / prove across GPUs (one process per GPU).
+
+One commitment's n_rows rows are split across the ranks.  Every rank encodes its rows and
+hashes what it can of the column leaves; the exchanges are small and go over RCCL (torch
+"nccl") or gloo:
+
+  commit  (lcpc-2d/src/lib.rs:651-815)
+    1. rank g encodes rows [r_g, r_g+1) -- the cut points fall on BLAKE3 chunk boundaries of
+       the leaf message (32 zero bytes || column), so rank g can compute the chaining values
+       of its chunks [c_g, c_g+1) for every column by itself;
+    2. all-to-all: rank g sends the chaining values of column block k to rank k
+       ((chunks of g) x n_cols/G x 32 B -- 2-4 MiB at cfg3, not the 64 MiB codeword shard);
+    3. rank k merges the chunks of its column block into leaves and builds that subtree;
+    4. all-gather of the G subtree roots; every rank finishes the top log2(G) levels.
+  prove   (lcpc-2d/src/lib.rs:1034-1123)
+    rank 0 owns the Merlin transcript; it broadcasts each degree-test tensor (the challenge
+    vector, n_rows elements), every rank returns its partial row combination, rank 0 folds
+    them mod p and absorbs the result, and so on; the opened columns are assembled from every
+    rank's rows and the Merkle paths from the owners' subtrees and the shared top tree.
+
+The proof is bit-identical to the single-GPU LcCommit.prove (tests/test_shard.py runs the
+protocol over gloo at world_size 2 against a single-process commit).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+LEAF_PREFIX = 32
+CHUNK = 1024
+
+
+# ---------------------------------------------------------------- partition
+def chunk_partition(field_bytes: int, n_rows: int, world: int, n_chunks: Optional[int] = None):
+    """[(chunk_lo, chunk_hi, row_lo, row_hi)] per rank; rows cut at chunk boundaries."""
+    if n_chunks is None:
+        n_chunks = -(-(LEAF_PREFIX + n_rows * field_bytes) // CHUNK)
+
+    def first_row(c):
+        if c <= 0:
+            return 0
+        if c >= n_chunks:
+            return n_rows
+        return min(n_rows, -(-(CHUNK * c - LEAF_PREFIX) // field_bytes))
+
+    out = []
+    for g in range(world):
+        c_lo, c_hi = g * n_chunks // world, (g + 1) * n_chunks // world
+        out.append((c_lo, c_hi, first_row(c_lo), first_row(c_hi)))
+    return out
+
+
+def _level_offset(n_leaves: int, level: int) -> int:
+    """Offset of Merkle level `level` (>= 1) in merkle_tree's output [level1 | level2 | ...]."""
+    return n_leaves - (n_leaves >> (level - 1))
+
+
+# ---------------------------------------------------------------- collectives
+class Comm:
+    """torch.distributed on numpy buffers: gloo keeps them on the CPU, nccl (RCCL) stages them
+    through the rank's GPU."""
+
+    def __init__(self, dist=None, device: str = "cpu"):
+        self.dist = dist
+        self.device = device
+        self.rank = dist.get_rank() if dist else 0
+        self.world = dist.get_world_size() if dist else 1
+
+    def _t(self, a: np.ndarray):
+        import torch
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).to(self.device)
+
+    def bcast(self, a: Optional[np.ndarray], shape, dtype, src: int = 0) -> np.ndarray:
+        if self.world == 1:
+            return a
+        import torch
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        t = self._t(a) if self.rank == src else torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        self.dist.broadcast(t, src)
+        return t.cpu().numpy().view(dtype).reshape(shape)
+
+    def all_gather(self, a: np.ndarray) -> List[np.ndarray]:
+        """Same-shaped arrays from every rank, in rank order."""
+        if self.world == 1:
+            return [a]
+        t = self._t(a)
+        outs = [t.clone() for _ in range(self.world)]
+        self.dist.all_gather(outs, t)
+        return [o.cpu().numpy().view(a.dtype).reshape(a.shape) for o in outs]
+
+    def all_gather_v(self, a: np.ndarray) -> List[np.ndarray]:
+        """Arrays whose first dimension differs per rank (padded to the max, then trimmed)."""
+        if self.world == 1:
+            return [a]
+        lens = self.all_gather(np.array([a.shape[0]], np.int64))
+        m = int(max(int(x[0]) for x in lens))
+        pad = np.zeros((m,) + a.shape[1:], a.dtype)
+        pad[:a.shape[0]] = a
+        got = self.all_gather(pad)
+        return [g[:int(n[0])] for g, n in zip(got, lens)]
+
+    def all_to_all(self, parts: Sequence[np.ndarray]) -> List[np.ndarray]:
+        """parts[k] goes to rank k; returns what every rank sent here, in rank order.  Parts
+        may differ in their first dimension across senders (not across receivers)."""
+        if self.world == 1:
+            return [parts[0]]
+        recv = []
+        for k in range(self.world):  # one all-gather per destination keeps it backend-neutral
+            got = self.all_gather_v(parts[k])
+            if k == self.rank:
+                recv = got
+        return recv
+
+
+# ---------------------------------------------------------------- GPU backend
+class GpuBackend:
+    """The compute steps of a shard, through liblcpc_mi.so (the product path)."""
+
+    def __init__(self, enc):
+        from . import _native as N
+        from .lcpc2d import limbs, log2
+        self.N = N
+        self.L = N.load()
+        self.enc = enc
+        self.field = enc.field
+        self.limbs = limbs(enc.field)
+        self.n_per_row, self.n_cols = enc.n_per_row, enc.n_cols
+        self.n_col_opens = enc.get_n_col_opens()
+        self.n_degree_tests = enc.get_n_degree_tests()
+        self.path_len = log2(self.n_cols)
+
+    def _raise(self, rc):
+        from .lcpc2d import _raise
+        _raise(rc)
+
+    @staticmethod
+    def _p64(a):
+        return np.ascontiguousarray(a).ctypes.data_as(C.POINTER(C.c_uint64))
+
+    def n_chunks(self, n_rows):
+        return self.L.lcpc_leaf_n_chunks(self.field, n_rows)
+
+    def shard_new(self, rows: np.ndarray, row0: int, n_rows_total: int):
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        n = rows.size // (self.limbs * self.n_per_row)
+        h = C.c_void_p()
+        self._raise(self.L.lcpc_shard_new(self.enc._h, self._p64(rows) if n else None, row0, n, n_rows_total,
+                                          C.byref(h)))
+        return (h.value, n)
+
+    def shard_free(self, sh):
+        self.L.lcpc_shard_free(sh[0])
+
+    def chunk_cvs(self, sh, c_lo, c_hi) -> np.ndarray:
+        out = np.zeros((max(c_hi - c_lo, 0), self.n_cols, 32), np.uint8)
+        self._raise(self.L.lcpc_shard_chunk_cvs(sh[0], c_lo, c_hi, out.ctypes.data_as(self.N.u8p)))
+        return out
+
+    def leaves_from_cvs(self, cvs: np.ndarray) -> np.ndarray:
+        cvs = np.ascontiguousarray(cvs, dtype=np.uint8)
+        out = np.zeros((cvs.shape[1], 32), np.uint8)
+        self._raise(self.L.lcpc_leaves_from_cvs(cvs.ctypes.data_as(self.N.u8p), cvs.shape[0], cvs.shape[1],
+                                                out.ctypes.data_as(self.N.u8p)))
+        return out
+
+    def merkle(self, leaves: np.ndarray) -> np.ndarray:
+        leaves = np.ascontiguousarray(leaves, dtype=np.uint8)
+        n = leaves.shape[0]
+        out = np.zeros((max(n - 1, 1), 32), np.uint8)
+        if n > 1:
+            self._raise(self.L.lcpc_merkle_tree(leaves.ctypes.data_as(self.N.u8p), n,
+                                                out.ctypes.data_as(self.N.u8p)))
+        return out[:n - 1]
+
+    def collapse(self, sh, tensors: np.ndarray) -> np.ndarray:
+        t = np.ascontiguousarray(tensors, dtype=np.uint64)
+        nt = t.shape[0]
+        out = np.zeros((nt, self.n_per_row, self.limbs), np.uint64)
+        self._raise(self.L.lcpc_shard_collapse(sh[0], self._p64(t) if t.size else None, nt, self._p64(out)))
+        return out
+
+    def gather_columns(self, sh, idx: np.ndarray) -> np.ndarray:
+        idx = np.ascontiguousarray(idx, dtype=np.uint64)
+        out = np.zeros((len(idx), sh[1], self.limbs), np.uint64)
+        if sh[1] and len(idx):
+            self._raise(self.L.lcpc_shard_gather_columns(sh[0], self._p64(idx), len(idx), self._p64(out)))
+        return out
+
+    def field_sum(self, vecs: np.ndarray) -> np.ndarray:
+        v = np.ascontiguousarray(vecs, dtype=np.uint64)
+        out = np.zeros(v.shape[1:], np.uint64)
+        self._raise(self.L.lcpc_field_sum(self.field, self._p64(v), v.shape[0], v.shape[1], self._p64(out)))
+        return out
+
+    def challenge_tensor(self, tr, n) -> np.ndarray:
+        out = np.zeros((n, self.limbs), np.uint64)
+        self._raise(self.L.lcpc_challenge_tensor(tr._h, self.field, n, self._p64(out)))
+        return out
+
+    def append_field_elems(self, tr, label: bytes, elems: np.ndarray):
+        e = np.ascontiguousarray(elems, dtype=np.uint64)
+        lab = (C.c_uint8 * len(label)).from_buffer_copy(label)
+        self._raise(self.L.lcpc_transcript_append_field_elems(tr._h, C.cast(lab, self.N.u8p), len(label),
+                                                              self.field, self._p64(e), e.size // self.limbs))
+
+    def challenge_columns(self, tr, n) -> np.ndarray:
+        out = np.zeros(n, np.uint64)
+        self._raise(self.L.lcpc_challenge_columns(tr._h, self.n_cols, n, self._p64(out)))
+        return out
+
+    def proof_from_parts(self, p_eval, p_random, cols, paths):
+        from .lcpc2d import LcColumn, LcEvalProof
+        columns = [LcColumn(cols[k], [bytes(paths[k, i]) for i in range(paths.shape[1])])
+                   for k in range(cols.shape[0])]
+        return LcEvalProof.from_parts(self.field, self.n_cols, p_eval, list(p_random), columns)
+
+
+LABEL_PR = b"$l//PR"
+LABEL_PE = b"$l//PE"
+
+
+# ---------------------------------------------------------------- the protocol
+class RowShardedCommit:
+    """One rank's share of a row-sharded commitment (see the module docstring)."""
+
+    def __init__(self, backend, comm: Comm, n_rows: int, field_bytes: int):
+        self.b, self.comm = backend, comm
+        self.n_rows = n_rows
+        G = comm.world
+        self.n_chunks = backend.n_chunks(n_rows)
+        self.part = chunk_partition(field_bytes, n_rows, G, self.n_chunks)
+        self.c_lo, self.c_hi, self.r_lo, self.r_hi = self.part[comm.rank]
+        np2 = backend.n_cols
+        if np2 & (np2 - 1) or G & (G - 1) or np2 % G:
+            raise ValueError("row shards need power-of-two n_cols and world size, world | n_cols")
+        self.block = np2 // G
+        self.sh = None
+
+    # -- commit
+    def commit(self, coeff_rows: np.ndarray) -> bytes:
+        """coeff_rows: this rank's rows [r_lo, r_hi) of the zero-padded coefficient matrix."""
+        b, comm, G = self.b, self.comm, self.comm.world
+        self.sh = b.shard_new(coeff_rows, self.r_lo, self.n_rows)
+        cvs = b.chunk_cvs(self.sh, self.c_lo, self.c_hi)                 # (my chunks, n_cols, 32)
+        B = self.block
+        recv = comm.all_to_all([cvs[:, k * B:(k + 1) * B] for k in range(G)])
+        all_cvs = np.concatenate(recv, axis=0)                            # (n_chunks, B, 32)
+        self.leaves = b.leaves_from_cvs(all_cvs)                          # my column block
+        self.sub = b.merkle(self.leaves)                                  # B - 1 nodes
+        sub_root = self.sub[-1] if B > 1 else self.leaves[0]
+        self.roots = np.stack(comm.all_gather(sub_root))                  # (G, 32)
+        self.top = b.merkle(self.roots)                                   # G - 1 nodes
+        self.root = bytes(self.top[-1] if G > 1 else self.roots[0])
+        return self.root
+
+    def _lower_path(self, j: int) -> np.ndarray:
+        """Sibling digests of column j below the subtree root (j in my block)."""
+        B = self.block
+        lvls = B.bit_length() - 1
+        out = np.zeros((lvls, 32), np.uint8)
+        jl = j - self.comm.rank * B
+        for lvl in range(lvls):
+            sib = (jl >> lvl) ^ 1
+            out[lvl] = self.leaves[sib] if lvl == 0 else self.sub[_level_offset(B, lvl) + sib]
+        return out
+
+    def _upper_path(self, j: int) -> np.ndarray:
+        G, B = self.comm.world, self.block
+        lvls = G.bit_length() - 1
+        out = np.zeros((lvls, 32), np.uint8)
+        jb = j // B
+        for lvl in range(lvls):
+            sib = (jb >> lvl) ^ 1
+            out[lvl] = self.roots[sib] if lvl == 0 else self.top[_level_offset(G, lvl) + sib]
+        return out
+
+    # -- prove
+    def prove(self, outer: np.ndarray, tr=None):
+        """Every rank calls this; rank 0 passes the transcript and gets the LcEvalProof."""
+        b, comm = self.b, self.comm
+        rank0 = comm.rank == 0
+        nl = b.limbs
+        n_rows, lo, hi = self.n_rows, self.r_lo, self.r_hi
+        outer = np.ascontiguousarray(outer, dtype=np.uint64).reshape(n_rows, nl)
+        ndt = b.n_degree_tests
+        p_random = []
+        p_eval = None
+        for i in range(max(ndt, 1)):
+            tens = []
+            if i < ndt:
+                t = b.challenge_tensor(tr, n_rows) if rank0 else None
+                t = comm.bcast(t, (n_rows, nl), np.uint64)   # the challenge vector
+                tens.append(t[lo:hi])
+            if i == 0:
+                tens.append(outer[lo:hi])                     # the evaluation tensor rides along
+            parts = b.collapse(self.sh, np.stack(tens))        # (len(tens), n_per_row, limbs)
+            allp = comm.all_gather(parts)
+            if rank0:
+                sums = [b.field_sum(np.stack([p[k] for p in allp])) for k in range(len(tens))]
+                if i < ndt:
+                    p_random.append(sums[0])
+                    b.append_field_elems(tr, LABEL_PR, sums[0])
+                if i == 0:
+                    p_eval = sums[-1]
+        if rank0:
+            b.append_field_elems(tr, LABEL_PE, p_eval)
+        nco = b.n_col_opens
+        idx = b.challenge_columns(tr, nco) if rank0 else None
+        idx = comm.bcast(idx, (nco,), np.uint64)
+        cols = comm.all_gather_v(b.gather_columns(self.sh, idx).transpose(1, 0, 2).copy())
+        lower = np.zeros((nco, self.block.bit_length() - 1, 32), np.uint8)
+        for k, j in enumerate(idx):
+            if int(j) // self.block == comm.rank:
+                lower[k] = self._lower_path(int(j))
+        lowers = comm.all_gather(lower)
+        if not rank0:
+            return None
+        cols = np.concatenate(cols, axis=0).transpose(1, 0, 2)          # (nco, n_rows, limbs)
+        paths = np.zeros((nco, b.path_len, 32), np.uint8)
+        for k, j in enumerate(idx):
+            owner = int(j) // self.block
+            paths[k] = np.concatenate([lowers[owner][k], self._upper_path(int(j))], axis=0)
+        return b.proof_from_parts(p_eval, p_random, np.ascontiguousarray(cols), paths)
+
+    def close(self):
+        if self.sh is not None:
+            self.b.shard_free(self.sh)
+            self.sh = None

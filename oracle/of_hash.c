@@ -122,6 +122,41 @@ static void b3_subtree(const uint8_t *in, size_t len, uint64_t chunk0, int is_ro
   b3_parent_cv(l, r, is_root, out);
 }
 
+/* exported pieces of the tree (used by the row-shard protocol test): the chaining value of one
+ * chunk, and the left-balanced merge of n chunk chaining values into the root */
+static void cv_to_bytes(const uint32_t h[8], uint8_t *out) {
+  for (int i = 0; i < 8; i++)
+    for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(h[i] >> (8 * k));
+}
+static void cv_from_bytes(const uint8_t *in, uint32_t h[8]) {
+  for (int i = 0; i < 8; i++)
+    h[i] = (uint32_t)in[4 * i] | ((uint32_t)in[4 * i + 1] << 8) | ((uint32_t)in[4 * i + 2] << 16) |
+           ((uint32_t)in[4 * i + 3] << 24);
+}
+void of_blake3_chunk_cv(const uint8_t *in, size_t len, uint64_t counter, int is_root,
+                        uint8_t out[32]) {
+  uint32_t h[8];
+  b3_chunk_cv(in, len, counter, is_root, h);
+  cv_to_bytes(h, out);
+}
+static void merge_rec(const uint8_t *cvs, size_t n, int is_root, uint32_t out[8]) {
+  if (n == 1) {
+    cv_from_bytes(cvs, out);
+    return;
+  }
+  size_t p2 = 1;
+  while (p2 * 2 < n) p2 *= 2; /* left subtree: largest power of two < n */
+  uint32_t l[8], r[8];
+  merge_rec(cvs, p2, 0, l);
+  merge_rec(cvs + 32 * p2, n - p2, 0, r);
+  b3_parent_cv(l, r, is_root, out);
+}
+void of_blake3_merge_cvs(const uint8_t *cvs, size_t n, uint8_t out[32]) {
+  uint32_t h[8];
+  merge_rec(cvs, n, 1, h);
+  cv_to_bytes(h, out);
+}
+
 void of_blake3(const uint8_t *in, size_t len, uint8_t out[32]) {
   uint32_t h[8];
   b3_subtree(in, len, 0, 1, h);

@@ -158,6 +158,11 @@ int of_verify_column_value(int fid, const uint64_t *col, const uint64_t *tensor,
 of_enc *of_enc_sdig(int fid, size_t n_per_row, size_t n_cols_hint, uint64_t seed, int code_id,
                     size_t n_col_opens, size_t n_degree_tests);
 
+/* BLAKE3 tree pieces: one chunk's chaining value; left-balanced merge of n chunk CVs (root) */
+void of_blake3_chunk_cv(const uint8_t *in, size_t len, uint64_t counter, int is_root,
+                        uint8_t out[32]);
+void of_blake3_merge_cvs(const uint8_t *cvs, size_t n, uint8_t out[32]);
+
 /* ---------------- proof-of-storage producers (proof-of-storage/src) ---------------- */
 size_t of_pos_bytes_to_field(const uint8_t *bytes, size_t n_bytes, uint64_t *out);
 void of_pos_field_to_bytes(const uint64_t *elems, size_t n, uint8_t *out, size_t expected_len);

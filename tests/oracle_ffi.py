@@ -117,6 +117,8 @@ def _setup(L):
         "of_open_column": (C.c_int, [C.POINTER(OfCommit), C.c_size_t, u64p, u8p]),
         "of_verify_column_path": (C.c_int, [C.c_int, u64p, C.c_size_t, u8p, C.c_size_t, C.c_size_t, u8p]),
         "of_verify_column_value": (C.c_int, [C.c_int, u64p, u64p, C.c_size_t, u64p]),
+        "of_blake3_chunk_cv": (None, [u8p, C.c_size_t, C.c_uint64, C.c_int, u8p]),
+        "of_blake3_merge_cvs": (None, [u8p, C.c_size_t, u8p]),
         "of_pos_bytes_to_field": (C.c_size_t, [u8p, C.c_size_t, u64p]),
         "of_pos_field_to_bytes": (None, [u64p, C.c_size_t, u8p, C.c_size_t]),
         "of_pos_default_dims": (None, [C.c_size_t, szp, szp, szp]),

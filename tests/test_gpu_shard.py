@@ -1,0 +1,91 @@
+"""GPU: the row-sharded protocol (shard.py) with the product backend reproduces the single-GPU
+commit / prove bit for bit -- one rank, and two ranks (gloo) sharing the one GPU."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+CASES = {"ft127": (1, 1 << 16), "ft63": (0, 3 * 4096 + 17), "ft255": (3, 20000)}
+
+
+def _single(L, fid, n):
+    enc = L.LigeroEncoding.new(fid, n)
+    coeffs = L.field_random(fid, n, 9)
+    comm = L.LcCommit.commit(coeffs, enc)
+    outer = L.field_random(fid, comm.get_n_rows(), 10)
+    tr = L.Transcript(b"test transcript")
+    tr.append_message(b"polycommit", comm.get_root())
+    tr.append_message(b"ncols", enc.get_n_col_opens().to_bytes(8, "big"))
+    return enc, comm, outer, comm.prove(outer, enc, tr)
+
+
+def _run_sharded(L, dist, device, fid, n):
+    from lcpc_proof_of_storage_amd.shard import Comm, GpuBackend, RowShardedCommit
+    enc, comm, outer, pf = _single(L, fid, n)
+    be = GpuBackend(enc)
+    sc = RowShardedCommit(be, Comm(dist, device), comm.get_n_rows(), 8 * be.limbs)
+    rows = comm.coeffs.reshape(comm.get_n_rows(), -1)
+    root = sc.commit(rows[sc.r_lo:sc.r_hi])
+    tr = None
+    if sc.comm.rank == 0:
+        tr = L.Transcript(b"test transcript")
+        tr.append_message(b"polycommit", root)
+        tr.append_message(b"ncols", enc.get_n_col_opens().to_bytes(8, "big"))
+    spf = sc.prove(outer, tr)
+    sc.close()
+    if sc.comm.rank != 0:
+        return None
+    cols, scols = pf.columns, spf.columns
+    return dict(root=root == comm.get_root(),
+                p_eval=np.array_equal(spf.p_eval, pf.p_eval),
+                p_random=all(np.array_equal(a, b) for a, b in zip(spf.p_random_vec, pf.p_random_vec)),
+                cols=all(np.array_equal(a.col, b.col) for a, b in zip(scols, cols)),
+                paths=all(a.path == b.path for a, b in zip(scols, cols)))
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_sharded_world1(gpu, case):
+    fid, n = CASES[case]
+    res = _run_sharded(gpu, None, "cpu", fid, n)
+    assert all(res.values()), res
+
+
+def _worker(rank, world, port, case, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import lcpc_proof_of_storage_amd as L
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L.set_device(0)
+        fid, n = CASES[case]
+        q.put((rank, _run_sharded(L, dist, "cpu", fid, n)))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("case", ["ft127", "ft63"])
+def test_sharded_world2_one_gpu(gpu, case):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=280) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert res[1] is None or "error" not in res[1], res[1]
+    assert all(v is True for v in res[0].values()), res[0]

@@ -1,0 +1,208 @@
+"""Row-sharded commit / prove protocol (lcpc_proof_of_storage_amd/shard.py), world_size 2 over
+gloo on the CPU, with the compute steps supplied by the oracle (OracleBackend below).  The
+sharded root and proof must equal the single-process oracle's commit / prove bit for bit; the
+GPU run of the same protocol uses GpuBackend (tests/test_gpu_shard.py).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+
+
+class OracleBackend:
+    """The shard compute steps restated on the oracle (test infrastructure only)."""
+
+    def __init__(self, O, fid, n_per_row, n_cols, nco, ndt):
+        import pyref
+        self.O, self.field = O, fid
+        self.f = pyref.Field(fid)
+        self.limbs = O.limbs(fid)
+        self.wb = 8 * self.limbs
+        self.n_per_row, self.n_cols = n_per_row, n_cols
+        self.n_col_opens, self.n_degree_tests = nco, ndt
+        self.path_len = n_cols.bit_length() - 1
+        self.enc = O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
+
+    def n_chunks(self, n_rows):
+        return -(-(32 + n_rows * self.wb) // 1024)
+
+    def shard_new(self, rows, row0, n_total):
+        nl = self.limbs
+        rows = np.ascontiguousarray(rows, dtype=np.uint64).reshape(-1, self.n_per_row * nl)
+        comm = []
+        for r in rows:
+            buf = np.zeros(self.n_cols * nl, np.uint64)
+            buf[:self.n_per_row * nl] = r
+            comm.append(self.enc.encode(buf))
+        comm = np.array(comm, dtype=np.uint64).reshape(len(rows), self.n_cols, nl)
+        return {"rows": rows, "comm": comm, "row0": row0, "n_total": n_total}
+
+    def shard_free(self, sh):
+        pass
+
+    def _repr(self, elems):
+        vals = self.O.from_mont(self.field, np.ascontiguousarray(elems).reshape(-1))
+        return b"".join(self.f.repr_bytes(v) for v in vals)
+
+    def chunk_cvs(self, sh, c_lo, c_hi):
+        O = self.O
+        total = self.n_chunks(sh["n_total"])
+        out = np.zeros((c_hi - c_lo, self.n_cols, 32), np.uint8)
+        for j in range(self.n_cols):
+            msg = (bytes(32) if c_lo == 0 else b"") + self._repr(sh["comm"][:, j])
+            for c in range(c_lo, c_hi):
+                piece = msg[(c - c_lo) * 1024:(c - c_lo + 1) * 1024]
+                cv = np.zeros(32, np.uint8)
+                p, keep = O.p8(piece if piece else b"\0")
+                O.lib().of_blake3_chunk_cv(p, len(piece), c, 1 if total == 1 else 0, cv.ctypes.data_as(O.u8p))
+                out[c - c_lo, j] = cv
+        return out
+
+    def leaves_from_cvs(self, cvs):
+        O = self.O
+        out = np.zeros((cvs.shape[1], 32), np.uint8)
+        for j in range(cvs.shape[1]):
+            col = np.ascontiguousarray(cvs[:, j])
+            if cvs.shape[0] == 1:
+                out[j] = col[0]
+                continue
+            O.lib().of_blake3_merge_cvs(col.ctypes.data_as(O.u8p), cvs.shape[0], out[j].ctypes.data_as(O.u8p))
+        return out
+
+    def merkle(self, leaves):
+        O = self.O
+        n = leaves.shape[0]
+        out = np.zeros((max(n - 1, 1), 32), np.uint8)
+        leaves = np.ascontiguousarray(leaves)
+        if n > 1:
+            O.lib().of_merkle_tree(leaves.ctypes.data_as(O.u8p), n, out.ctypes.data_as(O.u8p))
+        return out[:n - 1]
+
+    def collapse(self, sh, tensors):
+        out = []
+        n = sh["rows"].shape[0]
+        for t in tensors:
+            if n == 0:
+                out.append(np.zeros(self.n_per_row * self.limbs, np.uint64))
+            else:
+                out.append(self.O.collapse(self.field, sh["rows"].reshape(-1), t.reshape(-1), n, self.n_per_row))
+        return np.array(out, dtype=np.uint64).reshape(len(tensors), self.n_per_row, self.limbs)
+
+    def gather_columns(self, sh, idx):
+        return np.ascontiguousarray(sh["comm"][:, [int(i) for i in idx]].transpose(1, 0, 2))
+
+    def field_sum(self, vecs):
+        acc = vecs[0].reshape(-1).copy()
+        for v in vecs[1:]:
+            nxt = np.zeros_like(acc)
+            self.O.lib().of_add(self.field, self.O.p64(acc), self.O.p64(np.ascontiguousarray(v.reshape(-1))),
+                                self.O.p64(nxt), acc.size // self.limbs)
+            acc = nxt
+        return acc.reshape(vecs.shape[1:])
+
+    def challenge_tensor(self, tr, n):
+        key = tr.challenge_bytes(b"$l//DT", 32)
+        return self.O.ChaCha(key).field_random(self.field, n).reshape(n, self.limbs)
+
+    def append_field_elems(self, tr, label, elems):
+        vals = self.O.from_mont(self.field, np.ascontiguousarray(elems).reshape(-1))
+        for v in vals:
+            tr.append_message(label, self.f.repr_bytes(v))
+
+    def challenge_columns(self, tr, n):
+        key = tr.challenge_bytes(b"$l//CO", 32)
+        r = self.O.ChaCha(key)
+        return np.array([r.uniform(0, self.n_cols) for _ in range(n)], np.uint64)
+
+    def proof_from_parts(self, p_eval, p_random, cols, paths):
+        return {"p_eval": np.ascontiguousarray(p_eval).reshape(-1),
+                "p_random": np.concatenate([np.ascontiguousarray(p).reshape(-1) for p in p_random])
+                if p_random else np.zeros(0, np.uint64),
+                "cols": np.ascontiguousarray(cols).reshape(-1), "paths": np.ascontiguousarray(paths).tobytes()}
+
+
+CASES = {
+    "ft127": dict(fid=1, n_per_row=64, n_cols=128, length=64 * 150 + 7, nco=12, ndt=2),
+    "ft63": dict(fid=0, n_per_row=32, n_cols=64, length=32 * 300, nco=9, ndt=3),
+}
+
+
+def reference(case):
+    import oracle_ffi as O
+    c = CASES[case]
+    enc = O.Encoding.ligero(c["fid"], c["n_per_row"], c["n_cols"], c["nco"], c["ndt"])
+    coeffs = O.random_coeffs(c["fid"], c["length"], 5)
+    comm = O.Commit(enc, coeffs)
+    outer = O.random_coeffs(c["fid"], comm.n_rows, 6)
+    tr = O.standard_transcript(c["nco"], comm.root())
+    pf = comm.prove(enc, outer, tr)
+    return comm, outer, pf
+
+
+def _worker(rank, world, port, case, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import oracle_ffi as O
+    from lcpc_proof_of_storage_amd.shard import Comm, RowShardedCommit
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = CASES[case]
+        comm_ref, outer, pf_ref = reference(case)
+        be = OracleBackend(O, c["fid"], c["n_per_row"], c["n_cols"], c["nco"], c["ndt"])
+        sc = RowShardedCommit(be, Comm(dist, "cpu"), comm_ref.n_rows, be.wb)
+        rows = comm_ref.coeffs.reshape(comm_ref.n_rows, -1)
+        root = sc.commit(rows[sc.r_lo:sc.r_hi])
+        tr = O.standard_transcript(c["nco"], root) if rank == 0 else None
+        pf = sc.prove(outer, tr)
+        res = None
+        if rank == 0:
+            res = dict(root=root == comm_ref.root(),
+                       p_eval=np.array_equal(pf["p_eval"], pf_ref.p_eval),
+                       p_random=np.array_equal(pf["p_random"], pf_ref.p_random),
+                       cols=np.array_equal(pf["cols"], pf_ref.cols),
+                       paths=pf["paths"] == pf_ref.paths.tobytes(),
+                       part=sc.part)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chunk_partition():
+    from lcpc_proof_of_storage_amd.shard import chunk_partition
+    # cfg3 (Ft127, 512 rows): 9 chunks over 8 ranks, cuts at rows 64c - 2
+    p = chunk_partition(16, 512, 8)
+    assert p[0] == (0, 1, 0, 62) and p[1] == (1, 2, 62, 126) and p[7] == (7, 9, 446, 512)
+    assert [x[3] for x in p[:-1]] == [x[2] for x in p[1:]]
+    for fb, rows, g in [(8, 100, 2), (32, 7, 4), (16, 1, 2), (16, 2000, 8)]:
+        p = chunk_partition(fb, rows, g)
+        assert p[0][2] == 0 and p[-1][3] == rows
+        assert all(a[3] == b[2] for a, b in zip(p, p[1:]))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_row_sharded_protocol_world2(case):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=280) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    r0 = res[0]
+    assert r0["root"] and r0["p_eval"] and r0["p_random"] and r0["cols"] and r0["paths"], r0
