@@ -200,10 +200,13 @@ def shard_workload(args, L, torch, rank, local_rank, dist):
     outer = L.field_random(fid, n_rows, 7)
     be = GpuBackend(enc)
     comm = Comm(dist, f"cuda:{local_rank}" if dist is not None else "cpu")
+    sc0 = RowShardedCommit(be, comm, n_rows, 8 * nl)
+    mine = np.ascontiguousarray(rows[sc0.r_lo:sc0.r_hi])  # this rank's rows stay resident in HBM
+    d_mine = torch.from_numpy(mine.view(np.int64)).to(f"cuda:{local_rank}")
 
     def step(slot):
         sc = RowShardedCommit(be, comm, n_rows, 8 * nl)
-        root = sc.commit(rows[sc.r_lo:sc.r_hi])
+        root = sc.commit((d_mine.data_ptr(), sc.r_hi - sc.r_lo))
         tr = None
         if comm.rank == 0:
             tr = L.Transcript(b"test transcript")

@@ -292,6 +292,9 @@ size_t lcpc_leaf_n_chunks(lcpc_field f, size_t n_rows);          /* 1-KiB chunks
 size_t lcpc_leaf_chunk_first_row(lcpc_field f, size_t chunk);    /* first row of chunk */
 lcpc_status lcpc_shard_new(const lcpc_encoding *e, const uint64_t *coeffs, size_t row0,
                            size_t n_shard_rows, size_t n_rows_total, lcpc_shard **out);
+/* same with the shard's coefficient rows already in device memory */
+lcpc_status lcpc_shard_new_device(const lcpc_encoding *e, const void *d_coeffs, size_t row0,
+                                  size_t n_shard_rows, size_t n_rows_total, lcpc_shard **out);
 void lcpc_shard_free(lcpc_shard *s);
 /* chaining values of leaf chunks [chunk_lo, chunk_hi) of every column: out[chunk][col][32] */
 lcpc_status lcpc_shard_chunk_cvs(const lcpc_shard *s, size_t chunk_lo, size_t chunk_hi,

@@ -113,6 +113,7 @@ SIGNATURES = {
     "lcpc_leaf_n_chunks": (sz, [i32, sz]),
     "lcpc_leaf_chunk_first_row": (sz, [i32, sz]),
     "lcpc_shard_new": (i32, [vp, u64p, sz, sz, sz, C.POINTER(vp)]),
+    "lcpc_shard_new_device": (i32, [vp, vp, sz, sz, sz, C.POINTER(vp)]),
     "lcpc_shard_free": (None, [vp]),
     "lcpc_shard_chunk_cvs": (i32, [vp, sz, sz, u8p]),
     "lcpc_leaves_from_cvs": (i32, [u8p, sz, sz, u8p]),

@@ -1615,8 +1615,21 @@ size_t lcpc_leaf_chunk_first_row(lcpc_field f, size_t chunk) {
   return (1024 * chunk - 32 + wb - 1) / wb;
 }
 
+static lcpc_status shard_new_impl(const lcpc_encoding *e, const void *coeffs, bool on_device, size_t row0,
+                                  size_t n_shard_rows, size_t n_rows_total, lcpc_shard **out);
+
 lcpc_status lcpc_shard_new(const lcpc_encoding *e, const uint64_t *coeffs, size_t row0,
                            size_t n_shard_rows, size_t n_rows_total, lcpc_shard **out) {
+  return shard_new_impl(e, coeffs, false, row0, n_shard_rows, n_rows_total, out);
+}
+
+lcpc_status lcpc_shard_new_device(const lcpc_encoding *e, const void *d_coeffs, size_t row0,
+                                  size_t n_shard_rows, size_t n_rows_total, lcpc_shard **out) {
+  return shard_new_impl(e, d_coeffs, true, row0, n_shard_rows, n_rows_total, out);
+}
+
+static lcpc_status shard_new_impl(const lcpc_encoding *e, const void *coeffs, bool on_device, size_t row0,
+                                  size_t n_shard_rows, size_t n_rows_total, lcpc_shard **out) {
   if (!e || !out || (!coeffs && n_shard_rows)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   if (e->kind != KIND_RS) return fail(LCPC_ERR_UNSUPPORTED, "row shards: Ligero / R-S encodings only");
   if (row0 + n_shard_rows > n_rows_total) return fail(LCPC_ERR_INVALID_ARG, "shard rows out of range");
@@ -1632,7 +1645,10 @@ lcpc_status lcpc_shard_new(const lcpc_encoding *e, const uint64_t *coeffs, size_
   const int wb = field_bytes(e->fid);
   HIP_TRY(sh->coeffs.alloc(dev, n_shard_rows * np * wb + 16));
   HIP_TRY(sh->comm.alloc(dev, n_shard_rows * nc * wb + 16));
-  if (n_shard_rows) {
+  if (n_shard_rows && on_device) {  // encode straight from the caller's rows; pass A copies them
+    HIP_TRY(ntt_rows(e->plan, (const uint32_t *)coeffs, np, np, sh->comm.as<uint32_t>(), nc, n_shard_rows,
+                     lease.s, sh->coeffs.as<uint32_t>(), np));
+  } else if (n_shard_rows) {
     HIP_TRY(hipMemcpyAsync(sh->coeffs.p, coeffs, n_shard_rows * np * wb, hipMemcpyHostToDevice, lease.s));
     HIP_TRY(ntt_rows(e->plan, sh->coeffs.as<uint32_t>(), np, np, sh->comm.as<uint32_t>(), nc, n_shard_rows,
                      lease.s));

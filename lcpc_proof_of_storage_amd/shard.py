@@ -142,10 +142,16 @@ class GpuBackend:
     def n_chunks(self, n_rows):
         return self.L.lcpc_leaf_n_chunks(self.field, n_rows)
 
-    def shard_new(self, rows: np.ndarray, row0: int, n_rows_total: int):
+    def shard_new(self, rows, row0: int, n_rows_total: int):
+        """rows: host array of the shard's coefficient rows, or (device pointer, n_rows)."""
+        h = C.c_void_p()
+        if isinstance(rows, tuple):
+            ptr, n = rows
+            self._raise(self.L.lcpc_shard_new_device(self.enc._h, C.c_void_p(ptr) if n else None, row0, n,
+                                                     n_rows_total, C.byref(h)))
+            return (h.value, n)
         rows = np.ascontiguousarray(rows, dtype=np.uint64)
         n = rows.size // (self.limbs * self.n_per_row)
-        h = C.c_void_p()
         self._raise(self.L.lcpc_shard_new(self.enc._h, self._p64(rows) if n else None, row0, n, n_rows_total,
                                           C.byref(h)))
         return (h.value, n)
@@ -239,8 +245,9 @@ class RowShardedCommit:
         self.sh = None
 
     # -- commit
-    def commit(self, coeff_rows: np.ndarray) -> bytes:
-        """coeff_rows: this rank's rows [r_lo, r_hi) of the zero-padded coefficient matrix."""
+    def commit(self, coeff_rows) -> bytes:
+        """coeff_rows: this rank's rows [r_lo, r_hi) of the zero-padded coefficient matrix (host
+        array, or (device pointer, n_rows) with the GPU backend)."""
         b, comm, G = self.b, self.comm, self.comm.world
         self.sh = b.shard_new(coeff_rows, self.r_lo, self.n_rows)
         cvs = b.chunk_cvs(self.sh, self.c_lo, self.c_hi)                 # (my chunks, n_cols, 32)
