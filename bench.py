@@ -58,7 +58,7 @@ def parse():
                          "commitments overlap); serial: one in-order stream per GPU")
     ap.add_argument("--roofline-steps", type=int, default=3,
                     help="serial steps after the timed region whose encode launches give the roofline")
-    ap.add_argument("--pipeline", type=int, default=12,
+    ap.add_argument("--pipeline", type=int, default=16,
                     help="independent commitments in flight per GPU (host threads); the serial "
                          "Merlin transcript of one overlaps the kernels of the others")
     return ap.parse_args()
