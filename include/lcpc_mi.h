@@ -280,6 +280,52 @@ lcpc_status lcpc_pos_columns(const lcpc_encoding *e, const uint64_t *elems, size
                              const uint64_t *idx, size_t n, uint64_t *cols_out,
                              uint8_t *leaves_out);
 
+/* ------------------------------------------------------------------ PoS encoded files
+ * (proof-of-storage/src/lcpc_online/encoded_file_{writer,reader}.rs, WriteableFt63).
+ * A `.porenc` image is column-major: column c holds row_capacity elements starting at byte
+ * c * row_capacity * 8, each the 8-byte little-endian canonical repr (F::WRITTEN_BYTES_WIDTH,
+ * field_vec_to_raw_bytes, data_field.rs:24,62-70); rows past rows_written are not touched (zero in
+ * a fresh set_len file).  A `.portree` image is MerkleTree::to_bytes: the 2 enc - 1 digests
+ * leaves || parents, root last (merkle_tree.rs:14-27,61-63).  Callers pass mmaps of the files. */
+/* EncodedFileWriter::convert_unencoded_file (encoded_file_writer.rs:134-231): the data's 7-byte
+ * elements in rows of pre, each row zero padded and Ligero-encoded to enc elements, written to
+ * porenc; tree = the Merkle tree of the column digests (ColumnDigestAccumulator,
+ * column_digest_accumulator.rs:62-118).  *rows_written = ceil(ceil(n_bytes / 7) / pre) and
+ * row_capacity must be >= it (the reference writer allocates 2 * rows, :77-80). */
+lcpc_status lcpc_pos_encode_file(const uint8_t *data, size_t n_bytes, size_t pre, size_t enc,
+                                 size_t row_capacity, uint8_t *porenc, uint8_t *tree,
+                                 size_t *rows_written);
+/* same, processing at most batch_rows rows per GPU pass (rounded to whole 1-KiB column-digest
+ * chunks; 0 = automatic, about 4 GiB of device memory per pass) */
+lcpc_status lcpc_pos_encode_file_batched(const uint8_t *data, size_t n_bytes, size_t pre, size_t enc,
+                                         size_t row_capacity, uint8_t *porenc, uint8_t *tree,
+                                         size_t *rows_written, size_t batch_rows);
+/* The streaming writer itself: EncodedFileWriter::new (:40-105; porenc = the preallocated
+ * image of row_capacity rows, batch_rows as above), push_bytes (:233-262), and
+ * finalize_to_column_digest / _to_commit / _to_merkle_tree (:452-501): digests = the enc column
+ * digests, tree = MerkleTree::to_bytes; either may be NULL.  Rows are encoded and written as
+ * soon as the data is known to continue past them, the last ones at finalize.  When the file
+ * must grow, the caller re-lays it out (EncodedFileReader::set_new_capacity, reader.rs:348-381)
+ * and passes the new image with set_target. */
+typedef struct lcpc_pos_writer lcpc_pos_writer;
+lcpc_status lcpc_pos_writer_new(size_t pre, size_t enc, uint8_t *porenc, size_t row_capacity,
+                                size_t batch_rows, lcpc_pos_writer **out);
+void lcpc_pos_writer_free(lcpc_pos_writer *w);
+lcpc_status lcpc_pos_writer_set_target(lcpc_pos_writer *w, uint8_t *porenc, size_t row_capacity);
+size_t lcpc_pos_writer_rows_written(const lcpc_pos_writer *w);
+lcpc_status lcpc_pos_writer_push_bytes(lcpc_pos_writer *w, const uint8_t *bytes, size_t n);
+lcpc_status lcpc_pos_writer_finalize(lcpc_pos_writer *w, uint8_t *digests, uint8_t *tree,
+                                     size_t *rows_written, size_t *bytes_of_data);
+/* EncodedFileReader::process_file_to_merkle_tree (encoded_file_reader.rs:328-346).
+ * LCPC_ERR_INVALID_ARG if an element is not canonical (from_repr(..).unwrap() panics there). */
+lcpc_status lcpc_pos_porenc_tree(const uint8_t *porenc, size_t enc, size_t rows_written,
+                                 size_t row_capacity, uint8_t *tree);
+/* EncodedFileReader::get_unencoded_row_bytes / decode_to_target_file (encoded_file_reader.rs:
+ * 59-91) for rows [row_lo, row_hi): (row_hi - row_lo) * pre * 7 bytes into out */
+lcpc_status lcpc_pos_decode_porenc(const uint8_t *porenc, size_t pre, size_t enc,
+                                   size_t row_capacity, size_t row_lo, size_t row_hi,
+                                   uint8_t *out);
+
 /* ------------------------------------------------------------------ row shards (multi-GPU)
  * One process per GPU holds rows [row0, row0 + n_shard_rows) of an n_rows x n_per_row Ligero
  * coefficient matrix.  With the exchanges done by the caller (lcpc_proof_of_storage_amd/

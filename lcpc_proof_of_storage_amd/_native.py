@@ -110,6 +110,16 @@ SIGNATURES = {
     "lcpc_ifft_oi_rows": (i32, [i32, u64p, sz, sz]),
     "lcpc_open_columns": (i32, [vp, u64p, sz, u64p, u8p]),
     "lcpc_pos_columns": (i32, [vp, u64p, sz, u64p, sz, u64p, u8p]),
+    "lcpc_pos_encode_file": (i32, [u8p, sz, sz, sz, sz, u8p, u8p, szp]),
+    "lcpc_pos_encode_file_batched": (i32, [u8p, sz, sz, sz, sz, u8p, u8p, szp, sz]),
+    "lcpc_pos_writer_new": (i32, [sz, sz, u8p, sz, sz, C.POINTER(vp)]),
+    "lcpc_pos_writer_free": (None, [vp]),
+    "lcpc_pos_writer_set_target": (i32, [vp, u8p, sz]),
+    "lcpc_pos_writer_rows_written": (sz, [vp]),
+    "lcpc_pos_writer_push_bytes": (i32, [vp, u8p, sz]),
+    "lcpc_pos_writer_finalize": (i32, [vp, u8p, u8p, szp, szp]),
+    "lcpc_pos_porenc_tree": (i32, [u8p, sz, sz, sz, u8p]),
+    "lcpc_pos_decode_porenc": (i32, [u8p, sz, sz, sz, sz, sz, u8p]),
     "lcpc_leaf_n_chunks": (sz, [i32, sz]),
     "lcpc_leaf_chunk_first_row": (sz, [i32, sz]),
     "lcpc_shard_new": (i32, [vp, u64p, sz, sz, sz, C.POINTER(vp)]),

@@ -119,10 +119,12 @@ __global__ __launch_bounds__(1024) void k_dot(const uint32_t *__restrict__ a,
 
 template <class F>
 __global__ void k_convert(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, size_t n,
-                          int to_mont) {
+                          int to_mont, uint32_t *__restrict__ bad) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Fe<F> x = fe_load<F>(in, i);
+  // canonical input that is not < p: flagged (PrimeField::from_repr would refuse it)
+  if (bad && to_mont && !fe_is_canonical<F>(x)) atomicOr(bad, 1u);
   fe_store<F>(out, i, to_mont ? fe_to_mont<F>(x) : fe_from_mont<F>(x));
 }
 
@@ -203,11 +205,11 @@ hipError_t dot(int fid, const uint32_t *a, const uint32_t *b, size_t n, uint32_t
 }
 
 hipError_t convert(int fid, const uint32_t *in, uint32_t *out, size_t n, bool to_mont,
-                   hipStream_t s) {
+                   hipStream_t s, uint32_t *bad) {
   if (!n) return hipSuccess;
   return dispatch_field(fid, [&]<class F>() {
     hipLaunchKernelGGL((k_convert<F>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out,
-                       n, to_mont ? 1 : 0);
+                       n, to_mont ? 1 : 0, bad);
     return hipGetLastError();
   });
 }

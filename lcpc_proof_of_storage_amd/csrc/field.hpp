@@ -56,6 +56,16 @@ __device__ __forceinline__ bool fe_eq(const Fe<F>& a, const Fe<F>& b) {
   return o == 0;
 }
 
+// a < p (a canonical value: PrimeField::from_repr accepts it)
+template <class F>
+__device__ __forceinline__ bool fe_is_canonical(const Fe<F>& a) {
+#pragma unroll
+  for (int i = F::N - 1; i >= 0; i--) {
+    if (a.v[i] != F::P[i]) return a.v[i] < F::P[i];
+  }
+  return false;
+}
+
 // r = a + b mod p  (a, b < p)
 template <class F>
 __device__ __forceinline__ Fe<F> fe_add(const Fe<F>& a, const Fe<F>& b) {

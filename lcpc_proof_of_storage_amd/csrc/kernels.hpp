@@ -88,9 +88,10 @@ hipError_t path_checks(const uint8_t *leaves, const uint8_t *paths, size_t n, si
 // out = sum_i a[i] * b[i]
 hipError_t dot(int fid, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out,
                void *scratch, hipStream_t s);
-// elementwise Montgomery <-> canonical conversion (device)
+// elementwise Montgomery <-> canonical conversion (device); with bad non-null, canonical
+// inputs that are not < p set *bad = 1
 hipError_t convert(int fid, const uint32_t *in, uint32_t *out, size_t n, bool to_mont,
-                   hipStream_t s);
+                   hipStream_t s, uint32_t *bad = nullptr);
 // chunk-local self-test entry: out = a * b elementwise (Montgomery)
 hipError_t mul_elementwise(int fid, const uint32_t *a, const uint32_t *b, uint32_t *out,
                            size_t n, hipStream_t s);

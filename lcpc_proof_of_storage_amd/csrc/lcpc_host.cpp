@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -16,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lcpc_mi.h"
@@ -1817,6 +1819,419 @@ lcpc_status lcpc_transcript_append_field_elems(lcpc_transcript *tr, const uint8_
   const uint8_t *repr = nullptr;
   if ((st = to_repr_host(dev, f, de.as<uint32_t>(), n, &repr))) return st;
   tr->t.append_messages(label, ln, repr, wb, n);
+  return LCPC_OK;
+}
+
+}  // extern "C"
+
+// ================================================================= PoS encoded files
+// The `.porenc` / `.portree` formats of proof-of-storage/src/lcpc_online.
+// The whole data path (byte packing, Ligero encode, canonical conversion + transpose to the
+// column-major file layout, BLAKE3 column digests, Merkle tree) runs on the GPU in row batches
+// that end on BLAKE3 chunk boundaries of the column messages, so each batch contributes whole
+// chunk chaining values and the file streams through bounded device memory.  The host only
+// moves bytes between the caller's buffers (typically mmaps of the files) and pinned staging.
+namespace {
+
+constexpr int POS_FID = LCPC_FT63;  // WriteableFt63: Ft63's modulus (writable_ft63.rs:8-12)
+constexpr size_t POS_WB = 8;        // F::WRITTEN_BYTES_WIDTH = size_of::<F>() (data_field.rs:24)
+constexpr size_t POS_DB = 7;        // F::DATA_BYTE_CAPACITY (data_field.rs:22)
+constexpr size_t POS_BATCH_BYTES = (size_t)4 << 30;  // device working set per batch
+
+template <class Fn>
+void parallel_for(size_t n, Fn fn) {
+  const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t T = std::min<size_t>(n, std::min<size_t>(16, hw));
+  if (T <= 1) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  const size_t grain = std::max<size_t>(1, n / (T * 8));
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < T; t++)
+    th.emplace_back([&] {
+      for (;;) {
+        const size_t i0 = next.fetch_add(grain);
+        if (i0 >= n) break;
+        const size_t i1 = std::min(n, i0 + grain);
+        for (size_t i = i0; i < i1; i++) fn(i);
+      }
+    });
+  for (auto &t : th) t.join();
+}
+
+struct PinnedBuf {
+  void *p = nullptr;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t alloc(size_t n) { return hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault); }
+  uint8_t *b() const { return (uint8_t *)p; }
+};
+
+lcpc_status pos_dims_check(size_t pre, size_t enc) {
+  // EncodedFileWriter::convert_unencoded_file / new (encoded_file_writer.rs:53-67, 146-163)
+  if (pre < 1) return fail(LCPC_ERR_INVALID_ARG, "Number of pre-encoded columns must be greater than 0");
+  if (enc < 2 || (enc & (enc - 1)))
+    return fail(LCPC_ERR_INVALID_ARG, "Number of encoded columns must be a power of 2 (>= 2)");
+  if (enc <= pre)
+    return fail(LCPC_ERR_INVALID_ARG, "Number of encoded columns must be greater than the number of columns");
+  if ((int)log2_np2(enc) > field_info(POS_FID).s) return fail(LCPC_FFT_TOO_BIG, "FFTError::TooBig");
+  return LCPC_OK;
+}
+
+}  // namespace
+
+// EncodedFileWriter (encoded_file_writer.rs:24-38): bytes arrive in pushes; whole batches of
+// rows are encoded once the data provably continues past them (so no chunk they close can be
+// a column message's last chunk), the rest at finalize when the row count is known.
+struct lcpc_pos_writer {
+  std::unique_ptr<lcpc_encoding> e;
+  size_t pre = 0, enc = 0, row_capacity = 0;
+  uint8_t *porenc = nullptr;
+  size_t cpb = 1, bmax = 1;        // chunks per batch, rows per batch (at most)
+  size_t rows_done = 0, chunks_done = 0, bytes_received = 0;
+  bool finalized = false;
+  std::vector<uint8_t> pending;   // data bytes from row rows_done on
+  std::vector<uint8_t> cvs;       // [chunk][column] chaining values of the chunks done
+  DBuf dbytes, coeffs, comm, dout, dcv;
+  PinnedBuf stg[2];
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  ~lcpc_pos_writer() {
+    if (e && e->dev) {
+      (void)hipSetDevice(e->dev->id);
+      for (auto &x : ev)
+        if (x) (void)hipEventDestroy(x);
+    }
+  }
+};
+
+namespace {
+
+size_t pos_row_bytes(const lcpc_pos_writer *w) { return w->pre * POS_DB; }
+
+// Encode chunks [chunks_done, c_end) (rows from pending), n_rows_cv = the row count the chunk
+// chaining values are computed for (exact at finalize; any larger-than-covered count before).
+lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_t n_rows_max) {
+  if (c_end <= w->chunks_done) return LCPC_OK;
+  const int fid = POS_FID;
+  const size_t pre = w->pre, enc = w->enc, rb = pos_row_bytes(w);
+  Device *dev = w->e->dev;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  hipStream_t s = lease.s;
+  for (auto *b : {&w->dbytes, &w->coeffs, &w->comm, &w->dout, &w->dcv}) b->s = s;
+  lcpc_status st;
+  struct Pending {
+    int slot = -1;
+    size_t r0 = 0, rows = 0;
+  } pend;
+  auto scatter = [&](const Pending &p) -> lcpc_status {
+    if (p.slot < 0) return LCPC_OK;
+    HIP_TRY(hipEventSynchronize(w->ev[p.slot]));
+    const uint8_t *src = w->stg[p.slot].b();
+    uint8_t *dst = w->porenc;
+    const size_t cap = w->row_capacity;
+    parallel_for(enc, [&](size_t c) {
+      std::memcpy(dst + (c * cap + p.r0) * POS_WB, src + c * p.rows * POS_WB, p.rows * POS_WB);
+    });
+    return LCPC_OK;
+  };
+  const size_t pend_row0 = w->rows_done;
+  // chaining values land in w->cvs by async copies: no reallocation while they are queued
+  w->cvs.reserve(c_end * w->enc * 32);
+  int k = 0;
+  for (size_t c_lo = w->chunks_done; c_lo < c_end; c_lo += w->cpb, k++) {
+    const size_t c_hi = std::min(c_end, c_lo + w->cpb);
+    const size_t r0 = std::min(n_rows_max, lcpc_leaf_chunk_first_row((lcpc_field)fid, c_lo));
+    const size_t r1 = std::min(n_rows_max, lcpc_leaf_chunk_first_row((lcpc_field)fid, c_hi));
+    const size_t rr1 = c_hi == leaf_n_chunks(fid, n_rows_cv) ? n_rows_max : r1;
+    const size_t B = rr1 - r0;
+    if (B > w->bmax) return fail(LCPC_ERR_INVALID_ARG, "internal: batch larger than its buffers");
+    if (B) {
+      if (r0 + B > w->row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row capacity exceeded");
+      // rows r0..r0+B are data bytes [rb (r0 - pend_row0), ...) of pending (the last may be short)
+      const size_t b0 = (r0 - pend_row0) * rb;
+      const size_t b1 = std::min(w->pending.size(), b0 + B * rb);
+      const size_t ne = (b1 - b0 + POS_DB - 1) / POS_DB;
+      HIP_TRY(hipMemcpyAsync(w->dbytes.p, w->pending.data() + b0, b1 - b0, hipMemcpyHostToDevice, s));
+      if (B * pre > ne)
+        HIP_TRY(hipMemsetAsync(w->coeffs.as<uint8_t>() + ne * POS_WB, 0, (B * pre - ne) * POS_WB, s));
+      HIP_TRY(pos_pack7(w->dbytes.as<uint8_t>(), b1 - b0, w->coeffs.as<uint64_t>(), s));
+      HIP_TRY(ntt_rows(w->e->plan, w->coeffs.as<uint32_t>(), pre, pre, w->comm.as<uint32_t>(), enc, B, s));
+      HIP_TRY(transpose_elems(fid, w->comm.as<uint32_t>(), B, enc, enc, enc, w->dout.as<uint32_t>(), B, s,
+                              TR_FROM_MONT));
+    }
+    // column-digest chunks of these rows (ColumnDigestAccumulator::update, :62-87)
+    HIP_TRY(leaf_chunk_cvs(fid, w->comm.as<uint32_t>(), r0, n_rows_cv, enc, enc, c_lo, c_hi,
+                           w->dcv.as<uint32_t>(), s));
+    const size_t cv_bytes = (c_hi - c_lo) * enc * 32;
+    const size_t cv_off = w->cvs.size();
+    w->cvs.resize(cv_off + cv_bytes);
+    HIP_TRY(hipMemcpyAsync(w->cvs.data() + cv_off, w->dcv.p, cv_bytes, hipMemcpyDeviceToHost, s));
+    if (B) {
+      const int slot = k & 1;
+      HIP_TRY(hipMemcpyAsync(w->stg[slot].p, w->dout.p, B * enc * POS_WB, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipEventRecord(w->ev[slot], s));
+      if ((st = scatter(pend))) return st;
+      pend = Pending{slot, r0, B};
+    }
+    w->chunks_done = c_hi;
+    w->rows_done = rr1;
+  }
+  if ((st = scatter(pend))) return st;
+  HIP_TRY(hipStreamSynchronize(s));
+  for (auto *b : {&w->dbytes, &w->coeffs, &w->comm, &w->dout, &w->dcv}) b->settle();
+  const size_t used = std::min(w->pending.size(), (w->rows_done - pend_row0) * rb);
+  w->pending.erase(w->pending.begin(), w->pending.begin() + used);
+  return LCPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+lcpc_status lcpc_pos_writer_new(size_t pre, size_t enc, uint8_t *porenc, size_t row_capacity,
+                                size_t batch_rows, lcpc_pos_writer **out) {
+  lcpc_status st = pos_dims_check(pre, enc);
+  if (st) return st;
+  if (!out || (!porenc && row_capacity)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  lcpc_encoding *ep = nullptr;
+  if ((st = make_rs_encoding(POS_FID, pre, enc, 0, 0, &ep))) return st;
+  auto w = std::make_unique<lcpc_pos_writer>();
+  w->e.reset(ep);
+  w->pre = pre;
+  w->enc = enc;
+  w->porenc = porenc;
+  w->row_capacity = row_capacity;
+  const size_t rows_per_chunk = 1024 / POS_WB;
+  size_t want = batch_rows;
+  if (!want) want = POS_BATCH_BYTES / (2 * enc * POS_WB + pre * (POS_WB + POS_DB));
+  w->cpb = std::max<size_t>(1, want / rows_per_chunk);
+  w->bmax = w->cpb * rows_per_chunk;
+  Device *dev = w->e->dev;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  HIP_TRY(w->dbytes.alloc(dev, w->bmax * pre * POS_DB + 64));
+  HIP_TRY(w->coeffs.alloc(dev, w->bmax * pre * POS_WB));
+  HIP_TRY(w->comm.alloc(dev, w->bmax * enc * POS_WB));
+  HIP_TRY(w->dout.alloc(dev, w->bmax * enc * POS_WB));
+  HIP_TRY(w->dcv.alloc(dev, w->cpb * enc * 32));
+  for (int i = 0; i < 2; i++) {
+    HIP_TRY(w->stg[i].alloc(w->bmax * enc * POS_WB));
+    HIP_TRY(hipEventCreateWithFlags(&w->ev[i], hipEventDisableTiming));
+  }
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  for (auto *b : {&w->dbytes, &w->coeffs, &w->comm, &w->dout, &w->dcv}) b->settle();
+  *out = w.release();
+  return LCPC_OK;
+}
+
+void lcpc_pos_writer_free(lcpc_pos_writer *w) { delete w; }
+
+lcpc_status lcpc_pos_writer_set_target(lcpc_pos_writer *w, uint8_t *porenc, size_t row_capacity) {
+  // after the caller grew the file (EncodedFileReader::set_new_capacity layout, :348-381)
+  if (!w || (!porenc && row_capacity)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (row_capacity < w->rows_done) return fail(LCPC_ERR_INVALID_ARG, "row_capacity < rows written");
+  w->porenc = porenc;
+  w->row_capacity = row_capacity;
+  return LCPC_OK;
+}
+
+size_t lcpc_pos_writer_rows_written(const lcpc_pos_writer *w) { return w ? w->rows_done : 0; }
+
+lcpc_status lcpc_pos_writer_push_bytes(lcpc_pos_writer *w, const uint8_t *bytes, size_t n) {
+  // push_bytes (encoded_file_writer.rs:233-262)
+  if (!w || (!bytes && n)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (w->finalized) return fail(LCPC_ERR_INVALID_ARG, "writer already finalized");
+  w->pending.insert(w->pending.end(), bytes, bytes + n);
+  w->bytes_received += n;
+  // whole batches whose rows are followed by at least one more full row
+  const size_t full_rows = w->rows_done + w->pending.size() / pos_row_bytes(w);
+  size_t c_end = w->chunks_done;
+  while (lcpc_leaf_chunk_first_row(LCPC_FT63, c_end + w->cpb) < full_rows) c_end += w->cpb;
+  if (c_end == w->chunks_done) return LCPC_OK;
+  return writer_run(w, c_end, full_rows, lcpc_leaf_chunk_first_row(LCPC_FT63, c_end));
+}
+
+lcpc_status lcpc_pos_writer_finalize(lcpc_pos_writer *w, uint8_t *digests, uint8_t *tree,
+                                     size_t *rows_written, size_t *bytes_of_data) {
+  // finalize_to_column_digest / _to_commit / _to_merkle_tree (encoded_file_writer.rs:452-501):
+  // digests = the enc column digests, tree = MerkleTree::to_bytes (2 enc - 1 digests); either
+  // may be NULL
+  if (!w) return fail(LCPC_ERR_INVALID_ARG, "null writer");
+  if (w->finalized) return fail(LCPC_ERR_INVALID_ARG, "writer already finalized");
+  const size_t rb = pos_row_bytes(w);
+  const size_t n_rows = w->rows_done + (w->pending.size() + rb - 1) / rb;
+  if (n_rows > w->row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row capacity exceeded");
+  const int fid = POS_FID;
+  const size_t n_chunks = leaf_n_chunks(fid, n_rows);
+  lcpc_status st = writer_run(w, n_chunks, n_rows, n_rows);
+  if (st) return st;
+  w->finalized = true;
+  const size_t enc = w->enc;
+  Device *dev = w->e->dev;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  hipStream_t s = lease.s;
+  DBuf dc, hashes;
+  if ((st = upload(dev, dc, w->cvs.data(), w->cvs.size()))) return st;
+  HIP_TRY(hashes.alloc(dev, (2 * enc - 1) * 32));
+  HIP_TRY(leaves_from_cvs(dc.as<uint32_t>(), enc, (int)n_chunks, hashes.as<uint8_t>(), s));
+  if (tree) {
+    HIP_TRY(merkle_tree(hashes.as<uint8_t>(), enc, s));
+    HIP_TRY(hipMemcpyAsync(tree, hashes.p, (2 * enc - 1) * 32, hipMemcpyDeviceToHost, s));
+  }
+  if (digests) HIP_TRY(hipMemcpyAsync(digests, hashes.p, enc * 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (rows_written) *rows_written = w->rows_done;
+  if (bytes_of_data) *bytes_of_data = w->bytes_received;
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_pos_encode_file_batched(const uint8_t *data, size_t n_bytes, size_t pre, size_t enc,
+                                         size_t row_capacity, uint8_t *porenc, uint8_t *tree,
+                                         size_t *rows_written, size_t batch_rows) {
+  lcpc_status st = pos_dims_check(pre, enc);
+  if (st) return st;
+  if (!tree || (!data && n_bytes)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  const size_t n_rows = ((n_bytes + POS_DB - 1) / POS_DB + pre - 1) / pre;
+  if (rows_written) *rows_written = n_rows;
+  if (row_capacity < n_rows) return fail(LCPC_ERR_INVALID_ARG, "row_capacity < rows to write");
+  lcpc_pos_writer *w = nullptr;
+  if ((st = lcpc_pos_writer_new(pre, enc, porenc, row_capacity, batch_rows, &w))) return st;
+  std::unique_ptr<lcpc_pos_writer> guard(w);
+  // one batch of bytes per push keeps the writer's pending buffer at about a batch
+  const size_t step = w->bmax * pre * POS_DB;
+  for (size_t off = 0; off < n_bytes; off += step)
+    if ((st = lcpc_pos_writer_push_bytes(w, data + off, std::min(step, n_bytes - off)))) return st;
+  return lcpc_pos_writer_finalize(w, nullptr, tree, rows_written, nullptr);
+}
+
+lcpc_status lcpc_pos_encode_file(const uint8_t *data, size_t n_bytes, size_t pre, size_t enc,
+                                 size_t row_capacity, uint8_t *porenc, uint8_t *tree,
+                                 size_t *rows_written) {
+  return lcpc_pos_encode_file_batched(data, n_bytes, pre, enc, row_capacity, porenc, tree, rows_written, 0);
+}
+
+lcpc_status lcpc_pos_porenc_tree(const uint8_t *porenc, size_t enc, size_t rows_written,
+                                 size_t row_capacity, uint8_t *tree) {
+  // EncodedFileReader::process_file_to_merkle_tree (encoded_file_reader.rs:328-346): every
+  // column's first rows_written elements, hashed after the 32-byte zero block
+  if (enc < 2 || (enc & (enc - 1))) return fail(LCPC_ERR_INVALID_ARG, "encoded width must be a power of 2 (>= 2)");
+  if (!tree || (!porenc && rows_written)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (rows_written > row_capacity) return fail(LCPC_ERR_INVALID_ARG, "rows_written > row_capacity");
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  hipStream_t s = lease.s;
+  const int fid = POS_FID;
+  const size_t col_bytes = rows_written * POS_WB;
+  const size_t cpb = col_bytes ? std::max<size_t>(1, std::min(enc, POS_BATCH_BYTES / 2 / col_bytes)) : enc;
+  DBuf hashes, dcols, scratch, dbad;
+  HIP_TRY(hashes.alloc(dev, (2 * enc - 1) * 32));
+  HIP_TRY(dcols.alloc(dev, cpb * col_bytes));
+  HIP_TRY(scratch.alloc(dev, leaf_hash_scratch_bytes(fid, rows_written, cpb)));
+  HIP_TRY(dbad.alloc(dev, 4));
+  HIP_TRY(hipMemsetAsync(dbad.p, 0, 4, s));
+  PinnedBuf stg;
+  HIP_TRY(stg.alloc(cpb * col_bytes));
+  for (size_t c0 = 0; c0 < enc; c0 += cpb) {
+    const size_t nc = std::min(enc, c0 + cpb) - c0;
+    if (col_bytes) {
+      HIP_TRY(hipStreamSynchronize(s));  // the previous batch's upload has left the staging
+      parallel_for(nc, [&](size_t c) {
+        std::memcpy(stg.b() + c * col_bytes, porenc + (c0 + c) * row_capacity * POS_WB, col_bytes);
+      });
+      HIP_TRY(hipMemcpyAsync(dcols.p, stg.p, nc * col_bytes, hipMemcpyHostToDevice, s));
+      // raw_bytes_to_field_vec: from_repr(..).unwrap() (data_field.rs:72-81)
+      HIP_TRY(convert(fid, dcols.as<uint32_t>(), dcols.as<uint32_t>(), nc * rows_written, true, s,
+                      dbad.as<uint32_t>()));
+    }
+    HIP_TRY(leaf_hashes_cols(fid, dcols.as<uint32_t>(), rows_written, nc, hashes.as<uint8_t>() + c0 * 32,
+                             scratch.p, s));
+  }
+  HIP_TRY(merkle_tree(hashes.as<uint8_t>(), enc, s));
+  uint32_t bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, dbad.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(tree, hashes.p, (2 * enc - 1) * 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (bad) return fail(LCPC_ERR_INVALID_ARG, "encoded file holds a non-canonical element (from_repr fails)");
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_pos_decode_porenc(const uint8_t *porenc, size_t pre, size_t enc, size_t row_capacity,
+                                   size_t row_lo, size_t row_hi, uint8_t *out) {
+  // EncodedFileReader::get_unencoded_row_bytes / decode_to_target_file (encoded_file_reader.rs:
+  // 59-91): gather each row's enc elements from the columns, decode_row (ifft_oi), keep the
+  // first pre coefficients, 7 data bytes each
+  lcpc_status st = pos_dims_check(pre, enc);
+  if (st) return st;
+  if (row_lo > row_hi || row_hi > row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row range");
+  const size_t n = row_hi - row_lo;
+  if (!n) return LCPC_OK;
+  if (!porenc || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  hipStream_t s = lease.s;
+  const int fid = POS_FID;
+  const int log_n = (int)log2_np2(enc);
+  NttPlan plan;
+  hipError_t he = ntt_plan_init(plan, fid, log_n, true, s);
+  if (he != hipSuccess) {
+    ntt_plan_free(plan);
+    if (he == hipErrorInvalidValue) return fail(LCPC_ERR_UNSUPPORTED, "length beyond the NTT range");
+    HIP_TRY(he);
+  }
+  struct PlanGuard {
+    NttPlan &p;
+    hipStream_t s;
+    ~PlanGuard() {
+      (void)hipStreamSynchronize(s);
+      ntt_plan_free(p);
+    }
+  } guard{plan, s};
+  uint32_t inv[8] = {0};
+  inv_pow2_canon(fid, log_n, inv);
+  const size_t bmax = std::max<size_t>(1, std::min(n, POS_BATCH_BYTES / (3 * enc * POS_WB)));
+  DBuf a, b, dbytes, dbad;
+  HIP_TRY(a.alloc(dev, bmax * enc * POS_WB));
+  HIP_TRY(b.alloc(dev, bmax * enc * POS_WB));
+  HIP_TRY(dbytes.alloc(dev, bmax * pre * POS_DB + 64));
+  HIP_TRY(dbad.alloc(dev, 4));
+  HIP_TRY(hipMemsetAsync(dbad.p, 0, 4, s));
+  PinnedBuf stg, ostg;
+  HIP_TRY(stg.alloc(bmax * enc * POS_WB));
+  HIP_TRY(ostg.alloc(bmax * pre * POS_DB));
+  for (size_t r0 = row_lo; r0 < row_hi; r0 += bmax) {
+    const size_t B = std::min(row_hi, r0 + bmax) - r0;
+    HIP_TRY(hipStreamSynchronize(s));
+    parallel_for(enc, [&](size_t c) {
+      std::memcpy(stg.b() + c * B * POS_WB, porenc + (c * row_capacity + r0) * POS_WB, B * POS_WB);
+    });
+    HIP_TRY(hipMemcpyAsync(a.p, stg.p, enc * B * POS_WB, hipMemcpyHostToDevice, s));
+    // [enc][B] canonical -> [B][enc] Montgomery (get_encoded_row + raw_bytes_to_field_vec)
+    HIP_TRY(transpose_elems(fid, a.as<uint32_t>(), enc, B, B, B, b.as<uint32_t>(), enc, s, TR_TO_MONT,
+                            dbad.as<uint32_t>()));
+    HIP_TRY(bitrev_scale(fid, b.as<uint32_t>(), a.as<uint32_t>(), log_n, B, nullptr, s));
+    HIP_TRY(ntt_rows(plan, a.as<uint32_t>(), enc, enc, b.as<uint32_t>(), enc, B, s));
+    HIP_TRY(bitrev_scale(fid, b.as<uint32_t>(), a.as<uint32_t>(), log_n, B, inv, s));
+    // decoded_row.drain(pre..) then field_vec_to_byte_vec
+    HIP_TRY(hipMemcpy2DAsync(b.p, pre * POS_WB, a.p, enc * POS_WB, pre * POS_WB, B, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(pos_unpack7(b.as<uint64_t>(), B * pre, dbytes.as<uint8_t>(), B * pre * POS_DB, s));
+    HIP_TRY(hipMemcpyAsync(ostg.p, dbytes.p, B * pre * POS_DB, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(out + (r0 - row_lo) * pre * POS_DB, ostg.p, B * pre * POS_DB);
+  }
+  uint32_t bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, dbad.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (bad) return fail(LCPC_ERR_INVALID_ARG, "encoded file holds a non-canonical element (from_repr fails)");
   return LCPC_OK;
 }
 

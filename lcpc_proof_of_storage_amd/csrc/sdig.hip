@@ -61,22 +61,39 @@ __global__ __launch_bounds__(256) void k_reed_solomon(const uint32_t *__restrict
   fe_store<F>(out, t, r);
 }
 
-// 32 x 32 element tiles through LDS (padded row: no repeated bank pattern down a column)
-template <class F>
+// 32 x 32 element tiles through LDS (padded row: no repeated bank pattern down a column).
+// MODE: TR_PLAIN copies elements; TR_FROM_MONT writes canonical values (the PoS on-disk repr);
+// TR_TO_MONT reads canonical values, flags any that is not < p in *bad (from_repr's check).
+template <class F, int MODE>
 __global__ __launch_bounds__(256) void k_transpose(const uint32_t *__restrict__ src, size_t rows,
                                                    size_t cols, size_t ss, size_t nv,
-                                                   uint32_t *__restrict__ dst, size_t ds) {
+                                                   uint32_t *__restrict__ dst, size_t ds,
+                                                   uint32_t *__restrict__ bad) {
   __shared__ Fe<F> tile[32][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const size_t c0 = (size_t)blockIdx.x * 32, r0 = (size_t)blockIdx.y * 32;
+  bool ok = true;
   for (int i = ty; i < 32; i += 8) {
     const size_t r = r0 + i, c = c0 + tx;
-    tile[i][tx] = (r < rows && c < cols && c < nv) ? fe_load<F>(src, r * ss + c) : fe_zero<F>();
+    Fe<F> x = (r < rows && c < cols && c < nv) ? fe_load<F>(src, r * ss + c) : fe_zero<F>();
+    if constexpr (MODE == TR_TO_MONT) {
+      ok &= fe_is_canonical<F>(x);
+      x = fe_to_mont<F>(x);
+    }
+    tile[i][tx] = x;
+  }
+  if constexpr (MODE == TR_TO_MONT) {
+    if (!ok) atomicOr(bad, 1u);
   }
   __syncthreads();
   for (int i = ty; i < 32; i += 8) {
     const size_t c = c0 + i, r = r0 + tx;
-    if (c < cols && r < rows) fe_store<F>(dst, c * ds + r, tile[tx][i]);
+    if (c < cols && r < rows) {
+      if constexpr (MODE == TR_FROM_MONT)
+        fe_store<F>(dst, c * ds + r, fe_from_mont<F>(tile[tx][i]));
+      else
+        fe_store<F>(dst, c * ds + r, tile[tx][i]);
+    }
   }
 }
 
@@ -189,13 +206,21 @@ hipError_t sdig_encode_cm(const SdigPlan &plan, uint32_t *cw, size_t R, uint32_t
 
 hipError_t transpose_elems(int fid, const uint32_t *src, size_t rows, size_t cols,
                            size_t src_stride, size_t n_valid, uint32_t *dst, size_t dst_stride,
-                           hipStream_t s) {
+                           hipStream_t s, int mode, uint32_t *bad) {
   if (!rows || !cols) return hipSuccess;
+  if (mode == TR_TO_MONT && !bad) return hipErrorInvalidValue;
   return dispatch_field(fid, [&]<class F>() {
     prof::Scope ps("transpose", s);
     dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));
-    hipLaunchKernelGGL((k_transpose<F>), grid, dim3(256), 0, s, src, rows, cols, src_stride,
-                       n_valid, dst, dst_stride);
+    if (mode == TR_FROM_MONT)
+      hipLaunchKernelGGL((k_transpose<F, TR_FROM_MONT>), grid, dim3(256), 0, s, src, rows, cols,
+                         src_stride, n_valid, dst, dst_stride, bad);
+    else if (mode == TR_TO_MONT)
+      hipLaunchKernelGGL((k_transpose<F, TR_TO_MONT>), grid, dim3(256), 0, s, src, rows, cols,
+                         src_stride, n_valid, dst, dst_stride, bad);
+    else
+      hipLaunchKernelGGL((k_transpose<F, TR_PLAIN>), grid, dim3(256), 0, s, src, rows, cols,
+                         src_stride, n_valid, dst, dst_stride, bad);
     return hipGetLastError();
   });
 }

@@ -1,0 +1,425 @@
+"""Proof-of-storage encoded files over liblcpc_mi.so: the `.porenc` / `.portree` / `.meta`
+formats of the reference's proof-of-storage/src/lcpc_online (names kept):
+
+  EncodedFileWriter     encoded_file_writer.rs:24-501  (new, push_bytes, finalize_*,
+                        convert_unencoded_file, get_encoded_file_metadata)
+  EncodedFileReader     encoded_file_reader.rs:20-381  (get_encoded_row,
+                        get_encoded_column_without_path, get_unencoded_row[_bytes],
+                        decode_to_target_file, process_file_to_merkle_tree, set_new_capacity,
+                        resize_to_target_file, get_unencoded_file_len)
+  EncodedFileMetadata   encoded_file_metadata.rs:6-27  (serde_json)
+  MerkleTree            merkle_tree.rs:7-86             (digests = leaves || parents)
+  read_tree / write_tree_to_file                         file_handler.rs:714-735
+  get_encoded_file_size_from_rate / get_decoded_file_size_from_rate   reader.rs:384-407
+
+Layout of a `.porenc` file (WriteableFt63): column c occupies row_capacity * 8 bytes starting at
+byte c * row_capacity * 8; its first rows_written elements are the canonical little-endian repr
+of the encoded matrix's column c, the rest zero.  The writer starts with row_capacity = 2 * rows
+and doubles it when rows reach it.
+
+Every byte of encoding, hashing and decoding runs on the GPU (liblcpc_mi.so); this module maps
+the files and hands the library pointers into them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import mmap
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .lcpc2d import _raise
+
+WRITTEN_BYTES_WIDTH = 8   # size_of::<WriteableFt63>() (data_field.rs:24)
+DATA_BYTE_CAPACITY = 7    # CAPACITY / 8 (data_field.rs:22)
+DIGEST_BYTES = 32
+_NULL_ULID = "0" * 26     # Ulid::default() as serialized by the ulid crate's serde impl
+
+
+def _u8(a: np.ndarray):
+    return a.ctypes.data_as(N.u8p) if a.size else None
+
+
+def _bytes_ptr(b) -> Tuple[Optional[C.POINTER(C.c_uint8)], object]:
+    arr = np.frombuffer(b, dtype=np.uint8) if len(b) else np.zeros(0, np.uint8)
+    return _u8(arr), arr
+
+
+# ---------------------------------------------------------------- metadata / Merkle tree
+@dataclass
+class EncodedFileMetadata:
+    """encoded_file_metadata.rs:6-13 (serde_json, field order kept)."""
+    pre_encoded_size: int
+    encoded_size: int
+    rows_written: int
+    row_capacity: int
+    bytes_of_data: int
+    ulid: str = _NULL_ULID
+
+    def to_json(self) -> str:
+        return json.dumps({"ulid": self.ulid, "pre_encoded_size": self.pre_encoded_size,
+                           "encoded_size": self.encoded_size, "rows_written": self.rows_written,
+                           "row_capacity": self.row_capacity, "bytes_of_data": self.bytes_of_data},
+                          separators=(",", ":"))
+
+    def write_to_file(self, writable) -> None:
+        writable.write(self.to_json().encode())
+
+    @classmethod
+    def read_from_file(cls, readable) -> "EncodedFileMetadata":
+        d = json.loads(readable.read())
+        return cls(d["pre_encoded_size"], d["encoded_size"], d["rows_written"], d["row_capacity"],
+                   d["bytes_of_data"], d.get("ulid", _NULL_ULID))
+
+
+class MerkleTree:
+    """merkle_tree.rs:7-86: 2 w - 1 digests, the w leaves then every parent level, root last."""
+
+    def __init__(self, digests: np.ndarray):
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1, DIGEST_BYTES)
+        self.digests = d
+        self.width = (d.shape[0] + 1) // 2
+
+    @classmethod
+    def new(cls, children_leaves) -> "MerkleTree":
+        leaves = np.ascontiguousarray(np.frombuffer(bytes(children_leaves), np.uint8)
+                                      if isinstance(children_leaves, (bytes, bytearray))
+                                      else children_leaves, dtype=np.uint8).reshape(-1, DIGEST_BYTES)
+        w = leaves.shape[0]
+        if w < 2 or w & (w - 1):
+            raise ValueError("Input needs to be a power of two, at least two.")
+        d = np.zeros((2 * w - 1, DIGEST_BYTES), np.uint8)
+        d[:w] = leaves
+        _raise(N.load().lcpc_merkle_tree(_u8(d[:w]), w, _u8(d[w:])))
+        return cls(d)
+
+    def root(self) -> bytes:
+        return self.digests[-1].tobytes()
+
+    def get_path(self, index: int) -> Optional[List[bytes]]:
+        if index >= self.width:
+            return None
+        path, base, level_len = [], 0, self.width
+        while level_len > 1:
+            path.append(self.digests[base + (index ^ 1)].tobytes())
+            base += level_len
+            level_len //= 2
+            index >>= 1
+        return path
+
+    def __len__(self) -> int:
+        return self.digests.shape[0]
+
+    def __getitem__(self, i: int) -> bytes:
+        return self.digests[i].tobytes()
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, MerkleTree) and np.array_equal(self.digests, other.digests)
+
+    def to_bytes(self) -> bytes:
+        return self.digests.tobytes()
+
+    @classmethod
+    def from_bytes(cls, data: bytes) -> "MerkleTree":
+        n = len(data) // DIGEST_BYTES
+        if (n + 1) & n:
+            raise ValueError("input size must be a power of two")
+        if n <= 2:
+            raise ValueError("Merkle tree must be a non-trivial binary tree")
+        return cls(np.frombuffer(data[:n * DIGEST_BYTES], np.uint8).copy())
+
+
+def read_tree(tree_file) -> MerkleTree:
+    tree_file.seek(0)
+    return MerkleTree.from_bytes(tree_file.read())
+
+
+def write_tree_to_file(tree_file, tree: MerkleTree) -> None:
+    tree_file.write(tree.to_bytes())
+
+
+def get_encoded_file_size_from_rate(decoded_file_size: int, pre_encoded_len: int, encoded_len: int) -> int:
+    """reader.rs:384-395 (div_ceils first, in this order)."""
+    return (-(-(-(-decoded_file_size // DATA_BYTE_CAPACITY)) // pre_encoded_len)
+            * WRITTEN_BYTES_WIDTH * encoded_len)
+
+
+def get_decoded_file_size_from_rate(encoded_file_size: int, pre_encoded_len: int, encoded_len: int) -> int:
+    """reader.rs:397-407."""
+    return (-(-(-(-encoded_file_size // encoded_len)) // WRITTEN_BYTES_WIDTH)
+            * DATA_BYTE_CAPACITY * pre_encoded_len)
+
+
+# ---------------------------------------------------------------- mapped file images
+class _Image:
+    """A read/write mmap of a `.porenc` file (zero-length files map to nothing)."""
+
+    def __init__(self, f, size: int):
+        self.f = f
+        self.size = size
+        f.truncate(size)
+        f.flush()
+        self.mm = mmap.mmap(f.fileno(), size) if size else None
+        self.arr = np.frombuffer(self.mm, np.uint8) if size else np.zeros(0, np.uint8)
+
+    def ptr(self):
+        return _u8(self.arr)
+
+    def close(self):
+        if self.mm is not None:
+            self.mm.flush()
+            del self.arr
+            self.mm.close()
+            self.mm = None
+            self.arr = np.zeros(0, np.uint8)
+
+    def grow(self, old_rows: int, new_rows: int, n_cols: int) -> None:
+        """EncodedFileReader::set_new_capacity (reader.rs:348-381): columns move back to
+        front to their new stride, the space after each zeroed."""
+        wb = WRITTEN_BYTES_WIDTH
+        self.close()
+        self.__init__(self.f, new_rows * n_cols * wb)
+        a = self.arr
+        old_len, new_len = old_rows * wb, new_rows * wb
+        for c in range(n_cols - 1, 0, -1):
+            a[c * new_len:c * new_len + old_len] = a[c * old_len:(c + 1) * old_len].copy()
+            a[c * new_len + old_len:(c + 1) * new_len] = 0
+        a[old_len:new_len] = 0
+
+
+# ---------------------------------------------------------------- writer
+class EncodedFileWriter:
+    """EncodedFileWriter<WriteableFt63, Blake3, LigeroEncoding> (encoded_file_writer.rs)."""
+
+    def __init__(self, num_pre_encoded_columns: int, num_encoded_columns: int,
+                 original_file_size: int, target_file, batch_rows: int = 0):
+        # new (:53-105): the assertions, then the file preallocated to 2 * rows
+        if not (num_encoded_columns > 0 and num_encoded_columns & (num_encoded_columns - 1) == 0):
+            raise ValueError("num_encoded_columns must be a power of two")
+        if not num_pre_encoded_columns < num_encoded_columns:
+            raise ValueError("num_pre_encoded_columns must be less than num_encoded_columns")
+        if not num_pre_encoded_columns > 0:
+            raise ValueError("num_pre_encoded_columns must be > 0")
+        self.pre_encoded_size = num_pre_encoded_columns
+        self.encoded_size = num_encoded_columns
+        num_rows = -(-(-(-original_file_size // DATA_BYTE_CAPACITY)) // num_pre_encoded_columns)
+        self.row_capacity = num_rows * 2
+        self.bytes_received = 0
+        self.rows_written = 0
+        self._img = _Image(target_file, self.row_capacity * num_encoded_columns * WRITTEN_BYTES_WIDTH)
+        h = N.vp()
+        _raise(N.load().lcpc_pos_writer_new(num_pre_encoded_columns, num_encoded_columns,
+                                            self._img.ptr(), self.row_capacity, batch_rows, C.byref(h)))
+        self._h = h
+        self._done = False
+
+    def _rows_for(self, n_bytes: int) -> int:
+        return -(-(-(-n_bytes // DATA_BYTE_CAPACITY)) // self.pre_encoded_size)
+
+    def _ensure_capacity(self, rows: int) -> None:
+        # the reference doubles the capacity whenever the rows written reach it (:378-381)
+        new_cap = self.row_capacity
+        while rows >= new_cap > 0:
+            new_cap *= 2
+        if rows > new_cap:  # zero-capacity files (empty original)
+            new_cap = max(rows, 1) * 2
+        if new_cap == self.row_capacity:
+            return
+        self._img.grow(self.row_capacity, new_cap, self.encoded_size)
+        self.row_capacity = new_cap
+        _raise(N.load().lcpc_pos_writer_set_target(self._h, self._img.ptr(), new_cap))
+
+    def get_encoded_file_metadata(self) -> EncodedFileMetadata:
+        return EncodedFileMetadata(self.pre_encoded_size, self.encoded_size, self.rows_written,
+                                   self.row_capacity, self.bytes_received)
+
+    def push_bytes(self, data: bytes) -> None:
+        if self._done:
+            raise RuntimeError("writer already finalized")
+        self._ensure_capacity(self._rows_for(self.bytes_received + len(data)))
+        p, keep = _bytes_ptr(data)
+        _raise(N.load().lcpc_pos_writer_push_bytes(self._h, p, len(data)))
+        self.bytes_received += len(data)
+
+    def _finalize(self, want_digests: bool, want_tree: bool):
+        if self._done:
+            raise RuntimeError("writer already finalized")
+        self._ensure_capacity(self._rows_for(self.bytes_received))
+        w = self.encoded_size
+        digests = np.zeros((w, DIGEST_BYTES), np.uint8) if want_digests else None
+        tree = np.zeros((2 * w - 1, DIGEST_BYTES), np.uint8) if want_tree else None
+        rows, nbytes = C.c_size_t(), C.c_size_t()
+        try:
+            _raise(N.load().lcpc_pos_writer_finalize(
+                self._h, _u8(digests) if want_digests else None, _u8(tree) if want_tree else None,
+                C.byref(rows), C.byref(nbytes)))
+        finally:
+            self._done = True
+            N.load().lcpc_pos_writer_free(self._h)
+            self._img.close()
+        self.rows_written = rows.value
+        return digests, tree
+
+    def finalize_to_column_digest(self) -> Tuple[EncodedFileMetadata, List[bytes]]:
+        d, _ = self._finalize(True, False)
+        return self.get_encoded_file_metadata(), [r.tobytes() for r in d]
+
+    def finalize_to_commit(self) -> Tuple[EncodedFileMetadata, bytes]:
+        _, t = self._finalize(False, True)
+        return self.get_encoded_file_metadata(), t[-1].tobytes()
+
+    def finalize_to_merkle_tree(self) -> Tuple[EncodedFileMetadata, MerkleTree]:
+        _, t = self._finalize(False, True)
+        return self.get_encoded_file_metadata(), MerkleTree(t)
+
+    def __del__(self):
+        if getattr(self, "_done", True) is False:
+            try:
+                N.load().lcpc_pos_writer_free(self._h)
+                self._img.close()
+            except Exception:
+                pass
+
+    @staticmethod
+    def convert_unencoded_file(unencoded_file, target_encoded_file: str,
+                               target_digest_file: Optional[str], target_metadata_file: Optional[str],
+                               num_pre_encoded_columns: int, num_encoded_columns: int
+                               ) -> Tuple[EncodedFileMetadata, MerkleTree]:
+        """encoded_file_writer.rs:134-231: the whole file in one pass of the GPU writer."""
+        if num_pre_encoded_columns < 1:
+            raise ValueError("Number of pre-encoded columns must be greater than 0")
+        if num_encoded_columns < 2 or num_encoded_columns & (num_encoded_columns - 1):
+            raise ValueError("Number of encoded columns must be a power of 2")
+        if num_encoded_columns <= num_pre_encoded_columns:
+            raise ValueError("Number of encoded columns must be greater than the number of columns")
+        unencoded_file.seek(0, os.SEEK_END)
+        total = unencoded_file.tell()
+        unencoded_file.seek(0)
+        num_rows = -(-(-(-total // DATA_BYTE_CAPACITY)) // num_pre_encoded_columns)
+        cap = num_rows * 2
+        with open(target_encoded_file, "w+b") as tf:
+            img = _Image(tf, cap * num_encoded_columns * WRITTEN_BYTES_WIDTH)
+            src = mmap.mmap(unencoded_file.fileno(), total, access=mmap.ACCESS_READ) if total else None
+            try:
+                data = np.frombuffer(src, np.uint8) if total else np.zeros(0, np.uint8)
+                tree = np.zeros((2 * num_encoded_columns - 1, DIGEST_BYTES), np.uint8)
+                rows = C.c_size_t()
+                _raise(N.load().lcpc_pos_encode_file(_u8(data), total, num_pre_encoded_columns,
+                                                     num_encoded_columns, cap, img.ptr(), _u8(tree),
+                                                     C.byref(rows)))
+                del data
+            finally:
+                if src is not None:
+                    src.close()
+                img.close()
+        meta = EncodedFileMetadata(num_pre_encoded_columns, num_encoded_columns, rows.value, cap, total)
+        mt = MerkleTree(tree)
+        if target_metadata_file:
+            with open(target_metadata_file, "wb") as f:
+                meta.write_to_file(f)
+        if target_digest_file:
+            with open(target_digest_file, "wb") as f:
+                write_tree_to_file(f, mt)
+        return meta, mt
+
+
+# ---------------------------------------------------------------- reader
+class EncodedFileReader:
+    """EncodedFileReader<WriteableFt63, Blake3, LigeroEncoding> (encoded_file_reader.rs)."""
+
+    def __init__(self, file_to_read, pre_encoded_size: int, encoded_size: int, rows_written: int,
+                 row_capacity: int):
+        self.f = file_to_read
+        self.pre_encoded_size = pre_encoded_size
+        self.encoded_size = encoded_size
+        self.rows_written = rows_written
+        self.row_capacity = row_capacity
+
+    @classmethod
+    def new_ligero(cls, file_to_read, pre_encoded_size, encoded_size, rows_written, row_capacity):
+        return cls(file_to_read, pre_encoded_size, encoded_size, rows_written, row_capacity)
+
+    def _with_map(self, fn):
+        """fn(u8 array over a read-only mmap of the file); no view of it may escape fn."""
+        size = os.fstat(self.f.fileno()).st_size
+        need = self.row_capacity * self.encoded_size * WRITTEN_BYTES_WIDTH
+        if size < need:
+            raise ValueError("encoded file shorter than row_capacity * encoded_size elements")
+        if need == 0:
+            return fn(np.zeros(0, np.uint8))
+        mm = mmap.mmap(self.f.fileno(), need, access=mmap.ACCESS_READ)
+        try:
+            return fn(np.frombuffer(mm, np.uint8))
+        finally:
+            try:
+                mm.close()
+            except BufferError:  # an in-flight exception's traceback still holds the view
+                pass
+
+    def get_encoded_column_without_path(self, target_col: int) -> np.ndarray:
+        """Canonical u64 values of the column's rows_written elements (reader.rs:317-326)."""
+        wb = WRITTEN_BYTES_WIDTH
+        self.f.seek(target_col * self.row_capacity * wb)
+        raw = self.f.read(self.rows_written * wb)
+        return np.frombuffer(raw, "<u8").copy()
+
+    def get_encoded_row(self, target_row: int) -> np.ndarray:
+        """Canonical u64 values of the row's encoded_size elements (reader.rs:214-253)."""
+        return self._with_map(lambda a: a.view("<u8").reshape(self.encoded_size, self.row_capacity)
+                              [:, target_row].copy())
+
+    def get_unencoded_row_bytes(self, target_row: int) -> bytes:
+        if not target_row < self.rows_written:
+            raise IndexError("target row index is out of bounds")
+        return self._decode(target_row, target_row + 1)
+
+    def _decode(self, lo: int, hi: int) -> bytes:
+        out = np.zeros((hi - lo) * self.pre_encoded_size * DATA_BYTE_CAPACITY, np.uint8)
+        self._with_map(lambda a: _raise(N.load().lcpc_pos_decode_porenc(
+            _u8(a), self.pre_encoded_size, self.encoded_size, self.row_capacity, lo, hi, _u8(out))))
+        return out.tobytes()
+
+    def get_unencoded_row(self, target_row: int) -> np.ndarray:
+        """The row's pre_encoded_size elements, raw limbs (WriteableFt63 internal words)."""
+        b = self.get_unencoded_row_bytes(target_row)
+        return np.frombuffer(b"".join(b[i:i + 7] + b"\0" for i in range(0, len(b), 7)), "<u8").copy()
+
+    def decode_to_target_file(self, target_file) -> None:
+        """reader.rs:79-91: every written row's pre_encoded_size * 7 bytes, in order."""
+        if self.rows_written:
+            target_file.write(self._decode(0, self.rows_written))
+        target_file.flush()
+
+    def get_unencoded_file_len(self) -> int:
+        return os.fstat(self.f.fileno()).st_size // (self.encoded_size // self.pre_encoded_size)
+
+    def process_file_to_merkle_tree(self) -> MerkleTree:
+        w = self.encoded_size
+        tree = np.zeros((2 * w - 1, DIGEST_BYTES), np.uint8)
+        self._with_map(lambda a: _raise(N.load().lcpc_pos_porenc_tree(
+            _u8(a), w, self.rows_written, self.row_capacity, _u8(tree))))
+        return MerkleTree(tree)
+
+    def set_new_capacity(self, new_row_capacity: int) -> None:
+        if new_row_capacity < self.rows_written:
+            raise ValueError("Cannot set capacity to fewer than rows are written.")
+        img = _Image.__new__(_Image)
+        img.f, img.size = self.f, self.row_capacity * self.encoded_size * WRITTEN_BYTES_WIDTH
+        img.mm = None
+        img.arr = np.zeros(0, np.uint8)
+        img.grow(self.row_capacity, new_row_capacity, self.encoded_size)
+        img.close()
+        self.row_capacity = new_row_capacity
+
+    def resize_to_target_file(self, target_file, new_pre_encoded_size: int, new_encoded_size: int
+                              ) -> Tuple[EncodedFileMetadata, MerkleTree]:
+        """reader.rs:98-117: decode every row, push its bytes into a writer of the new shape."""
+        w = EncodedFileWriter(new_pre_encoded_size, new_encoded_size, self.get_unencoded_file_len(),
+                              target_file)
+        if self.rows_written:
+            w.push_bytes(self._decode(0, self.rows_written))
+        return w.finalize_to_merkle_tree()

@@ -535,3 +535,46 @@ def hash_columns(fid: int, m: np.ndarray, n_rows: int, n_cols: int) -> bytes:
     lib().of_hash_columns(fid, p64(np.ascontiguousarray(m, dtype=np.uint64)), n_rows, n_cols,
                           out.ctypes.data_as(u8p))
     return out.tobytes()
+
+
+# ---------------------------------------------------------------- proof-of-storage encoded files
+def pos_encode_file(data: bytes, pre: int, enc: int, row_capacity: int = None):
+    """EncodedFileWriter::convert_unencoded_file restated (encoded_file_writer.rs:134-231,
+    264-389; column_digest_accumulator.rs:62-118; merkle_tree.rs:14-27): the data's 7-byte
+    elements in rows of `pre` (the last row partial), each zero padded to `enc` and Ligero
+    encoded (fft_io); the file is column-major with `row_capacity` (default 2 * rows) canonical
+    8-byte LE elements per column; leaves = BLAKE3(32 zero bytes || column repr); the tree is
+    leaves || parents.  Returns (porenc bytes, tree bytes, rows, capacity)."""
+    elems = pos_bytes_to_field(data)
+    rows = -(-len(elems) // pre)
+    cap = 2 * rows if row_capacity is None else row_capacity
+    coder = Encoding.ligero(0, pre, enc, 1, 1)
+    comm = np.zeros((rows, enc), np.uint64)
+    for r in range(rows):
+        row = np.zeros(enc, np.uint64)
+        part = elems[r * pre:(r + 1) * pre]
+        row[:len(part)] = part
+        comm[r] = coder.encode(row)
+    canon = np.zeros(rows * enc, np.uint64)
+    if rows:
+        lib().of_to_canonical(0, p64(np.ascontiguousarray(comm.reshape(-1))), p64(canon), rows * enc)
+    img = np.zeros((enc, cap), "<u8")
+    img[:, :rows] = canon.reshape(rows, enc).T
+    leaves = np.frombuffer(hash_columns(0, comm.reshape(-1) if rows else np.zeros(1, np.uint64), rows, enc),
+                           np.uint8).copy()
+    parents = np.zeros(32 * (enc - 1), np.uint8)
+    lib().of_merkle_tree(leaves.ctypes.data_as(u8p), enc, parents.ctypes.data_as(u8p))
+    return img.tobytes(), leaves.tobytes() + parents.tobytes(), rows, cap
+
+
+def pos_decode_rows(img: bytes, pre: int, enc: int, cap: int, rows: int) -> bytes:
+    """EncodedFileReader::decode_to_target_file restated (encoded_file_reader.rs:59-91,
+    lcpc_online.rs:568-574): each row gathered from the columns, ifft_oi, first `pre`
+    coefficients, 7 data bytes each."""
+    a = np.frombuffer(img, "<u8").reshape(enc, cap)
+    out = []
+    for r in range(rows):
+        mont = to_mont(0, [int(v) for v in a[:, r]])
+        coeffs = ifft_oi(0, mont)
+        out.append(pos_field_to_bytes(coeffs[:pre], 7 * pre))
+    return b"".join(out)
