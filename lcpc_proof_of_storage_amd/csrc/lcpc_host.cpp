@@ -165,6 +165,33 @@ struct Device {
     if (it == sizes.end()) return;
     free_blocks.emplace(it->second, p);
   }
+  // page-locked host blocks for the file paths' staging (pinning is slow: blocks are reused)
+  std::multimap<size_t, void *> pinned_free;
+  std::map<void *, size_t> pinned_sizes;
+  void *pinned_get(size_t bytes) {
+    bytes = std::max<size_t>(bytes, 4096);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = pinned_free.lower_bound(bytes);
+      if (it != pinned_free.end() && it->first <= 2 * bytes) {
+        void *p = it->second;
+        pinned_free.erase(it);
+        return p;
+      }
+    }
+    const size_t want = (bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+    void *p = nullptr;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    pinned_sizes[p] = want;
+    return p;
+  }
+  void pinned_put(void *p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = pinned_sizes.find(p);
+    if (it != pinned_sizes.end()) pinned_free.emplace(it->second, p);
+  }
   void trim() {
     (void)hipDeviceSynchronize();
     std::lock_guard<std::mutex> lk(mu);
@@ -1830,13 +1857,14 @@ lcpc_status lcpc_transcript_append_field_elems(lcpc_transcript *tr, const uint8_
 // column-major file layout, BLAKE3 column digests, Merkle tree) runs on the GPU in row batches
 // that end on BLAKE3 chunk boundaries of the column messages, so each batch contributes whole
 // chunk chaining values and the file streams through bounded device memory.  The host only
-// moves bytes between the caller's buffers (typically mmaps of the files) and pinned staging.
+// moves bytes between the caller's buffers (typically mmaps of the files) and page-locked
+// staging, with the copies of one batch overlapping the GPU work of the next.
 namespace {
 
 constexpr int POS_FID = LCPC_FT63;  // WriteableFt63: Ft63's modulus (writable_ft63.rs:8-12)
 constexpr size_t POS_WB = 8;        // F::WRITTEN_BYTES_WIDTH = size_of::<F>() (data_field.rs:24)
 constexpr size_t POS_DB = 7;        // F::DATA_BYTE_CAPACITY (data_field.rs:22)
-constexpr size_t POS_BATCH_BYTES = (size_t)4 << 30;  // device working set per batch
+constexpr size_t POS_STAGE_BYTES = (size_t)256 << 20;  // encoded bytes per pipelined batch
 
 template <class Fn>
 void parallel_for(size_t n, Fn fn) {
@@ -1861,13 +1889,58 @@ void parallel_for(size_t n, Fn fn) {
   for (auto &t : th) t.join();
 }
 
-struct PinnedBuf {
-  void *p = nullptr;
-  ~PinnedBuf() {
-    if (p) (void)hipHostFree(p);
+// large memcpy split over host threads
+void par_memcpy(uint8_t *dst, const uint8_t *src, size_t n) {
+  constexpr size_t BLK = (size_t)8 << 20;
+  if (n <= BLK) {
+    if (n) std::memcpy(dst, src, n);
+    return;
   }
-  hipError_t alloc(size_t n) { return hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault); }
+  parallel_for((n + BLK - 1) / BLK, [&](size_t i) {
+    const size_t o = i * BLK;
+    std::memcpy(dst + o, src + o, std::min(BLK, n - o));
+  });
+}
+
+// a page-locked block from the device's pool, returned at scope exit
+struct Pinned {
+  Device *d = nullptr;
+  void *p = nullptr;
+  size_t n = 0;
+  Pinned() = default;
+  Pinned(const Pinned &) = delete;
+  Pinned &operator=(const Pinned &) = delete;
+  ~Pinned() { reset(); }
+  void reset() {
+    if (d && p) d->pinned_put(p);
+    p = nullptr;
+    n = 0;
+  }
+  bool get(Device *dev, size_t bytes) {
+    reset();
+    d = dev;
+    p = dev->pinned_get(bytes);
+    n = p ? bytes : 0;
+    return p != nullptr;
+  }
   uint8_t *b() const { return (uint8_t *)p; }
+};
+
+// events destroyed at scope exit
+struct Events {
+  hipEvent_t e[2] = {nullptr, nullptr};
+  ~Events() {
+    for (auto &x : e)
+      if (x) (void)hipEventDestroy(x);
+  }
+  hipError_t init() {
+    for (auto &x : e)
+      if (!x) {
+        hipError_t r = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+        if (r != hipSuccess) return r;
+      }
+    return hipSuccess;
+  }
 };
 
 lcpc_status pos_dims_check(size_t pre, size_t enc) {
@@ -1893,25 +1966,36 @@ struct lcpc_pos_writer {
   size_t cpb = 1, bmax = 1;        // chunks per batch, rows per batch (at most)
   size_t rows_done = 0, chunks_done = 0, bytes_received = 0;
   bool finalized = false;
-  std::vector<uint8_t> pending;   // data bytes from row rows_done on
-  std::vector<uint8_t> cvs;       // [chunk][column] chaining values of the chunks done
+  Pinned pend;                     // data bytes from row rows_done on (page-locked)
+  size_t pend_len = 0;
+  std::vector<uint8_t> cvs;        // [chunk][column] chaining values of the chunks done
+  size_t buf_rows = 0;             // rows the batch buffers below hold (grown on demand)
   DBuf dbytes, coeffs, comm, dout, dcv;
-  PinnedBuf stg[2];
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  ~lcpc_pos_writer() {
-    if (e && e->dev) {
-      (void)hipSetDevice(e->dev->id);
-      for (auto &x : ev)
-        if (x) (void)hipEventDestroy(x);
-    }
-  }
+  Pinned stg[2];
+  Events ev;
 };
 
 namespace {
 
 size_t pos_row_bytes(const lcpc_pos_writer *w) { return w->pre * POS_DB; }
 
-// Encode chunks [chunks_done, c_end) (rows from pending), n_rows_cv = the row count the chunk
+lcpc_status writer_append(lcpc_pos_writer *w, const uint8_t *bytes, size_t n) {
+  if (!n) return LCPC_OK;
+  if (w->pend_len + n > w->pend.n) {
+    Pinned bigger;
+    if (!bigger.get(w->e->dev, std::max(w->pend_len + n, std::max<size_t>(1 << 20, 2 * w->pend.n))))
+      return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+    par_memcpy(bigger.b(), w->pend.b(), w->pend_len);
+    std::swap(w->pend.p, bigger.p);
+    std::swap(w->pend.n, bigger.n);
+    std::swap(w->pend.d, bigger.d);
+  }
+  par_memcpy(w->pend.b() + w->pend_len, bytes, n);
+  w->pend_len += n;
+  return LCPC_OK;
+}
+
+// Encode chunks [chunks_done, c_end) (rows from pend), n_rows_cv = the row count the chunk
 // chaining values are computed for (exact at finalize; any larger-than-covered count before).
 lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_t n_rows_max) {
   if (c_end <= w->chunks_done) return LCPC_OK;
@@ -1929,7 +2013,7 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
   } pend;
   auto scatter = [&](const Pending &p) -> lcpc_status {
     if (p.slot < 0) return LCPC_OK;
-    HIP_TRY(hipEventSynchronize(w->ev[p.slot]));
+    HIP_TRY(hipEventSynchronize(w->ev.e[p.slot]));
     const uint8_t *src = w->stg[p.slot].b();
     uint8_t *dst = w->porenc;
     const size_t cap = w->row_capacity;
@@ -1939,6 +2023,17 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
     return LCPC_OK;
   };
   const size_t pend_row0 = w->rows_done;
+  // batch buffers sized for the largest batch of this run (small files stay small)
+  const size_t need_rows = std::min(w->bmax, std::max<size_t>(1, n_rows_max - std::min(n_rows_max, pend_row0)));
+  if (need_rows > w->buf_rows) {
+    HIP_TRY(w->dbytes.alloc(dev, need_rows * pre * POS_DB + 64));
+    HIP_TRY(w->coeffs.alloc(dev, need_rows * pre * POS_WB));
+    HIP_TRY(w->comm.alloc(dev, need_rows * enc * POS_WB));
+    HIP_TRY(w->dout.alloc(dev, need_rows * enc * POS_WB));
+    for (auto &x : w->stg)
+      if (!x.get(dev, need_rows * enc * POS_WB)) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+    w->buf_rows = need_rows;
+  }
   // chaining values land in w->cvs by async copies: no reallocation while they are queued
   w->cvs.reserve(c_end * w->enc * 32);
   int k = 0;
@@ -1948,14 +2043,14 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
     const size_t r1 = std::min(n_rows_max, lcpc_leaf_chunk_first_row((lcpc_field)fid, c_hi));
     const size_t rr1 = c_hi == leaf_n_chunks(fid, n_rows_cv) ? n_rows_max : r1;
     const size_t B = rr1 - r0;
-    if (B > w->bmax) return fail(LCPC_ERR_INVALID_ARG, "internal: batch larger than its buffers");
+    if (B > w->buf_rows) return fail(LCPC_ERR_INVALID_ARG, "internal: batch larger than its buffers");
     if (B) {
       if (r0 + B > w->row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row capacity exceeded");
-      // rows r0..r0+B are data bytes [rb (r0 - pend_row0), ...) of pending (the last may be short)
+      // rows r0..r0+B are data bytes [rb (r0 - pend_row0), ...) of pend (the last may be short)
       const size_t b0 = (r0 - pend_row0) * rb;
-      const size_t b1 = std::min(w->pending.size(), b0 + B * rb);
+      const size_t b1 = std::min(w->pend_len, b0 + B * rb);
       const size_t ne = (b1 - b0 + POS_DB - 1) / POS_DB;
-      HIP_TRY(hipMemcpyAsync(w->dbytes.p, w->pending.data() + b0, b1 - b0, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(w->dbytes.p, w->pend.b() + b0, b1 - b0, hipMemcpyHostToDevice, s));
       if (B * pre > ne)
         HIP_TRY(hipMemsetAsync(w->coeffs.as<uint8_t>() + ne * POS_WB, 0, (B * pre - ne) * POS_WB, s));
       HIP_TRY(pos_pack7(w->dbytes.as<uint8_t>(), b1 - b0, w->coeffs.as<uint64_t>(), s));
@@ -1973,8 +2068,8 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
     if (B) {
       const int slot = k & 1;
       HIP_TRY(hipMemcpyAsync(w->stg[slot].p, w->dout.p, B * enc * POS_WB, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipEventRecord(w->ev[slot], s));
-      if ((st = scatter(pend))) return st;
+      HIP_TRY(hipEventRecord(w->ev.e[slot], s));
+      if ((st = scatter(pend))) return st;  // overlaps this batch's GPU work
       pend = Pending{slot, r0, B};
     }
     w->chunks_done = c_hi;
@@ -1983,8 +2078,9 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
   if ((st = scatter(pend))) return st;
   HIP_TRY(hipStreamSynchronize(s));
   for (auto *b : {&w->dbytes, &w->coeffs, &w->comm, &w->dout, &w->dcv}) b->settle();
-  const size_t used = std::min(w->pending.size(), (w->rows_done - pend_row0) * rb);
-  w->pending.erase(w->pending.begin(), w->pending.begin() + used);
+  const size_t used = std::min(w->pend_len, (w->rows_done - pend_row0) * rb);
+  std::memmove(w->pend.b(), w->pend.b() + used, w->pend_len - used);
+  w->pend_len -= used;
   return LCPC_OK;
 }
 
@@ -2007,21 +2103,14 @@ lcpc_status lcpc_pos_writer_new(size_t pre, size_t enc, uint8_t *porenc, size_t 
   w->row_capacity = row_capacity;
   const size_t rows_per_chunk = 1024 / POS_WB;
   size_t want = batch_rows;
-  if (!want) want = POS_BATCH_BYTES / (2 * enc * POS_WB + pre * (POS_WB + POS_DB));
+  if (!want) want = std::max<size_t>(rows_per_chunk, POS_STAGE_BYTES / (enc * POS_WB));
   w->cpb = std::max<size_t>(1, want / rows_per_chunk);
   w->bmax = w->cpb * rows_per_chunk;
   Device *dev = w->e->dev;
   Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
-  HIP_TRY(w->dbytes.alloc(dev, w->bmax * pre * POS_DB + 64));
-  HIP_TRY(w->coeffs.alloc(dev, w->bmax * pre * POS_WB));
-  HIP_TRY(w->comm.alloc(dev, w->bmax * enc * POS_WB));
-  HIP_TRY(w->dout.alloc(dev, w->bmax * enc * POS_WB));
   HIP_TRY(w->dcv.alloc(dev, w->cpb * enc * 32));
-  for (int i = 0; i < 2; i++) {
-    HIP_TRY(w->stg[i].alloc(w->bmax * enc * POS_WB));
-    HIP_TRY(hipEventCreateWithFlags(&w->ev[i], hipEventDisableTiming));
-  }
+  HIP_TRY(w->ev.init());
   HIP_TRY(hipStreamSynchronize(lease.s));
   for (auto *b : {&w->dbytes, &w->coeffs, &w->comm, &w->dout, &w->dcv}) b->settle();
   *out = w.release();
@@ -2045,14 +2134,24 @@ lcpc_status lcpc_pos_writer_push_bytes(lcpc_pos_writer *w, const uint8_t *bytes,
   // push_bytes (encoded_file_writer.rs:233-262)
   if (!w || (!bytes && n)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   if (w->finalized) return fail(LCPC_ERR_INVALID_ARG, "writer already finalized");
-  w->pending.insert(w->pending.end(), bytes, bytes + n);
-  w->bytes_received += n;
-  // whole batches whose rows are followed by at least one more full row
-  const size_t full_rows = w->rows_done + w->pending.size() / pos_row_bytes(w);
-  size_t c_end = w->chunks_done;
-  while (lcpc_leaf_chunk_first_row(LCPC_FT63, c_end + w->cpb) < full_rows) c_end += w->cpb;
-  if (c_end == w->chunks_done) return LCPC_OK;
-  return writer_run(w, c_end, full_rows, lcpc_leaf_chunk_first_row(LCPC_FT63, c_end));
+  lcpc_status st;
+  const size_t rb = pos_row_bytes(w);
+  // large pushes are taken a batch at a time, so the staging stays about a batch
+  const size_t step = std::max<size_t>(1, w->bmax * rb);
+  for (size_t off = 0; off < n || (n == 0 && off == 0); off += step) {
+    const size_t m = std::min(step, n - off);
+    if ((st = writer_append(w, bytes + off, m))) return st;
+    w->bytes_received += m;
+    // whole batches whose rows are followed by at least one more full row
+    const size_t full_rows = w->rows_done + w->pend_len / rb;
+    size_t c_end = w->chunks_done;
+    while (lcpc_leaf_chunk_first_row(LCPC_FT63, c_end + w->cpb) < full_rows) c_end += w->cpb;
+    if (c_end > w->chunks_done &&
+        (st = writer_run(w, c_end, full_rows, lcpc_leaf_chunk_first_row(LCPC_FT63, c_end))))
+      return st;
+    if (n == 0) break;
+  }
+  return LCPC_OK;
 }
 
 lcpc_status lcpc_pos_writer_finalize(lcpc_pos_writer *w, uint8_t *digests, uint8_t *tree,
@@ -2063,7 +2162,7 @@ lcpc_status lcpc_pos_writer_finalize(lcpc_pos_writer *w, uint8_t *digests, uint8
   if (!w) return fail(LCPC_ERR_INVALID_ARG, "null writer");
   if (w->finalized) return fail(LCPC_ERR_INVALID_ARG, "writer already finalized");
   const size_t rb = pos_row_bytes(w);
-  const size_t n_rows = w->rows_done + (w->pending.size() + rb - 1) / rb;
+  const size_t n_rows = w->rows_done + (w->pend_len + rb - 1) / rb;
   if (n_rows > w->row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row capacity exceeded");
   const int fid = POS_FID;
   const size_t n_chunks = leaf_n_chunks(fid, n_rows);
@@ -2102,10 +2201,7 @@ lcpc_status lcpc_pos_encode_file_batched(const uint8_t *data, size_t n_bytes, si
   lcpc_pos_writer *w = nullptr;
   if ((st = lcpc_pos_writer_new(pre, enc, porenc, row_capacity, batch_rows, &w))) return st;
   std::unique_ptr<lcpc_pos_writer> guard(w);
-  // one batch of bytes per push keeps the writer's pending buffer at about a batch
-  const size_t step = w->bmax * pre * POS_DB;
-  for (size_t off = 0; off < n_bytes; off += step)
-    if ((st = lcpc_pos_writer_push_bytes(w, data + off, std::min(step, n_bytes - off)))) return st;
+  if ((st = lcpc_pos_writer_push_bytes(w, data, n_bytes))) return st;
   return lcpc_pos_writer_finalize(w, nullptr, tree, rows_written, nullptr);
 }
 
@@ -2130,29 +2226,38 @@ lcpc_status lcpc_pos_porenc_tree(const uint8_t *porenc, size_t enc, size_t rows_
   hipStream_t s = lease.s;
   const int fid = POS_FID;
   const size_t col_bytes = rows_written * POS_WB;
-  const size_t cpb = col_bytes ? std::max<size_t>(1, std::min(enc, POS_BATCH_BYTES / 2 / col_bytes)) : enc;
-  DBuf hashes, dcols, scratch, dbad;
+  const size_t cpb = col_bytes ? std::max<size_t>(1, std::min(enc, POS_STAGE_BYTES / col_bytes)) : enc;
+  DBuf hashes, dcols[2], scratch[2], dbad;
   HIP_TRY(hashes.alloc(dev, (2 * enc - 1) * 32));
-  HIP_TRY(dcols.alloc(dev, cpb * col_bytes));
-  HIP_TRY(scratch.alloc(dev, leaf_hash_scratch_bytes(fid, rows_written, cpb)));
+  for (int i = 0; i < 2; i++) {
+    HIP_TRY(dcols[i].alloc(dev, cpb * col_bytes));
+    HIP_TRY(scratch[i].alloc(dev, leaf_hash_scratch_bytes(fid, rows_written, cpb)));
+  }
   HIP_TRY(dbad.alloc(dev, 4));
   HIP_TRY(hipMemsetAsync(dbad.p, 0, 4, s));
-  PinnedBuf stg;
-  HIP_TRY(stg.alloc(cpb * col_bytes));
-  for (size_t c0 = 0; c0 < enc; c0 += cpb) {
+  Pinned stg[2];
+  Events ev;
+  HIP_TRY(ev.init());
+  if (col_bytes)
+    for (auto &x : stg)
+      if (!x.get(dev, cpb * col_bytes)) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  int k = 0;
+  for (size_t c0 = 0; c0 < enc; c0 += cpb, k++) {
     const size_t nc = std::min(enc, c0 + cpb) - c0;
+    const int slot = k & 1;
     if (col_bytes) {
-      HIP_TRY(hipStreamSynchronize(s));  // the previous batch's upload has left the staging
+      if (k >= 2) HIP_TRY(hipEventSynchronize(ev.e[slot]));  // its last upload has left it
       parallel_for(nc, [&](size_t c) {
-        std::memcpy(stg.b() + c * col_bytes, porenc + (c0 + c) * row_capacity * POS_WB, col_bytes);
+        std::memcpy(stg[slot].b() + c * col_bytes, porenc + (c0 + c) * row_capacity * POS_WB, col_bytes);
       });
-      HIP_TRY(hipMemcpyAsync(dcols.p, stg.p, nc * col_bytes, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(dcols[slot].p, stg[slot].p, nc * col_bytes, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipEventRecord(ev.e[slot], s));
       // raw_bytes_to_field_vec: from_repr(..).unwrap() (data_field.rs:72-81)
-      HIP_TRY(convert(fid, dcols.as<uint32_t>(), dcols.as<uint32_t>(), nc * rows_written, true, s,
+      HIP_TRY(convert(fid, dcols[slot].as<uint32_t>(), dcols[slot].as<uint32_t>(), nc * rows_written, true, s,
                       dbad.as<uint32_t>()));
     }
-    HIP_TRY(leaf_hashes_cols(fid, dcols.as<uint32_t>(), rows_written, nc, hashes.as<uint8_t>() + c0 * 32,
-                             scratch.p, s));
+    HIP_TRY(leaf_hashes_cols(fid, dcols[slot].as<uint32_t>(), rows_written, nc, hashes.as<uint8_t>() + c0 * 32,
+                             scratch[slot].p, s));
   }
   HIP_TRY(merkle_tree(hashes.as<uint8_t>(), enc, s));
   uint32_t bad = 0;
@@ -2198,23 +2303,40 @@ lcpc_status lcpc_pos_decode_porenc(const uint8_t *porenc, size_t pre, size_t enc
   } guard{plan, s};
   uint32_t inv[8] = {0};
   inv_pow2_canon(fid, log_n, inv);
-  const size_t bmax = std::max<size_t>(1, std::min(n, POS_BATCH_BYTES / (3 * enc * POS_WB)));
+  const size_t bmax = std::max<size_t>(1, std::min(n, POS_STAGE_BYTES / (enc * POS_WB)));
   DBuf a, b, dbytes, dbad;
   HIP_TRY(a.alloc(dev, bmax * enc * POS_WB));
   HIP_TRY(b.alloc(dev, bmax * enc * POS_WB));
   HIP_TRY(dbytes.alloc(dev, bmax * pre * POS_DB + 64));
   HIP_TRY(dbad.alloc(dev, 4));
   HIP_TRY(hipMemsetAsync(dbad.p, 0, 4, s));
-  PinnedBuf stg, ostg;
-  HIP_TRY(stg.alloc(bmax * enc * POS_WB));
-  HIP_TRY(ostg.alloc(bmax * pre * POS_DB));
-  for (size_t r0 = row_lo; r0 < row_hi; r0 += bmax) {
+  Pinned stg[2], ostg[2];
+  Events in_ev, out_ev;
+  HIP_TRY(in_ev.init());
+  HIP_TRY(out_ev.init());
+  for (int i = 0; i < 2; i++)
+    if (!stg[i].get(dev, bmax * enc * POS_WB) || !ostg[i].get(dev, bmax * pre * POS_DB))
+      return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  struct Done {
+    int slot = -1;
+    size_t r0 = 0, rows = 0;
+  } done;
+  auto copy_out = [&](const Done &d) -> lcpc_status {
+    if (d.slot < 0) return LCPC_OK;
+    HIP_TRY(hipEventSynchronize(out_ev.e[d.slot]));
+    par_memcpy(out + (d.r0 - row_lo) * pre * POS_DB, ostg[d.slot].b(), d.rows * pre * POS_DB);
+    return LCPC_OK;
+  };
+  int k = 0;
+  for (size_t r0 = row_lo; r0 < row_hi; r0 += bmax, k++) {
     const size_t B = std::min(row_hi, r0 + bmax) - r0;
-    HIP_TRY(hipStreamSynchronize(s));
+    const int slot = k & 1;
+    if (k >= 2) HIP_TRY(hipEventSynchronize(in_ev.e[slot]));  // its last upload has left it
     parallel_for(enc, [&](size_t c) {
-      std::memcpy(stg.b() + c * B * POS_WB, porenc + (c * row_capacity + r0) * POS_WB, B * POS_WB);
+      std::memcpy(stg[slot].b() + c * B * POS_WB, porenc + (c * row_capacity + r0) * POS_WB, B * POS_WB);
     });
-    HIP_TRY(hipMemcpyAsync(a.p, stg.p, enc * B * POS_WB, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(a.p, stg[slot].p, enc * B * POS_WB, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(in_ev.e[slot], s));
     // [enc][B] canonical -> [B][enc] Montgomery (get_encoded_row + raw_bytes_to_field_vec)
     HIP_TRY(transpose_elems(fid, a.as<uint32_t>(), enc, B, B, B, b.as<uint32_t>(), enc, s, TR_TO_MONT,
                             dbad.as<uint32_t>()));
@@ -2224,10 +2346,13 @@ lcpc_status lcpc_pos_decode_porenc(const uint8_t *porenc, size_t pre, size_t enc
     // decoded_row.drain(pre..) then field_vec_to_byte_vec
     HIP_TRY(hipMemcpy2DAsync(b.p, pre * POS_WB, a.p, enc * POS_WB, pre * POS_WB, B, hipMemcpyDeviceToDevice, s));
     HIP_TRY(pos_unpack7(b.as<uint64_t>(), B * pre, dbytes.as<uint8_t>(), B * pre * POS_DB, s));
-    HIP_TRY(hipMemcpyAsync(ostg.p, dbytes.p, B * pre * POS_DB, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    std::memcpy(out + (r0 - row_lo) * pre * POS_DB, ostg.p, B * pre * POS_DB);
+    if (k >= 2) HIP_TRY(hipEventSynchronize(out_ev.e[slot]));
+    HIP_TRY(hipMemcpyAsync(ostg[slot].p, dbytes.p, B * pre * POS_DB, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(out_ev.e[slot], s));
+    if ((st = copy_out(done))) return st;  // overlaps this batch's GPU work
+    done = Done{slot, r0, B};
   }
+  if ((st = copy_out(done))) return st;
   uint32_t bad = 0;
   HIP_TRY(hipMemcpyAsync(&bad, dbad.p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
