@@ -276,6 +276,22 @@ lcpc_status lcpc_open_columns(const lcpc_commit *c, const uint64_t *idx, size_t 
 /* CommitRequestType::ColumnsWithoutPath / Leaves (lcpc_online.rs:144-224): encode `len`
  * elements with e and return the requested columns (n x n_rows) and / or their BLAKE3 leaf
  * digests (n x 32 B) without building the Merkle tree; either output may be NULL */
+/* PoS client verification (lcpc_online.rs:251-452):
+ * hash_column_to_digest / hash_field_vec_to_digest for n_cols columns stored one after another
+ * ([n_cols][n_rows] elements) -> n_cols x 32 B */
+lcpc_status lcpc_hash_field_columns(lcpc_field f, const uint64_t *cols, size_t n_rows, size_t n_cols,
+                                    uint8_t *out);
+/* client_online_verify_column_paths_without_full_columns (:280-318): ok[k] = 1 iff leaf digest
+ * k with its path (path_len x 32 B) hashes up to root at column idx[k] */
+lcpc_status lcpc_verify_leaf_paths(const uint8_t *leaves, const uint8_t *paths, size_t n,
+                                   size_t path_len, const uint64_t *idx, const uint8_t root[32],
+                                   uint8_t *ok);
+/* verify_column_value (lcpc-2d/src/lib.rs:1014-1030) batched, and the check of
+ * verify_proper_partial_polynomial_evaluation (:487-516): ok[k] = 1 iff
+ * sum_r tensor[r] cols[k][r] == values[idx[k]] (cols [n][n_rows]) */
+lcpc_status lcpc_verify_column_values(lcpc_field f, const uint64_t *cols, size_t n, size_t n_rows,
+                                      const uint64_t *tensor, const uint64_t *values,
+                                      size_t n_values, const uint64_t *idx, uint8_t *ok);
 lcpc_status lcpc_pos_columns(const lcpc_encoding *e, const uint64_t *elems, size_t len,
                              const uint64_t *idx, size_t n, uint64_t *cols_out,
                              uint8_t *leaves_out);

@@ -110,6 +110,9 @@ SIGNATURES = {
     "lcpc_ifft_oi_rows": (i32, [i32, u64p, sz, sz]),
     "lcpc_open_columns": (i32, [vp, u64p, sz, u64p, u8p]),
     "lcpc_pos_columns": (i32, [vp, u64p, sz, u64p, sz, u64p, u8p]),
+    "lcpc_hash_field_columns": (i32, [i32, u64p, sz, sz, u8p]),
+    "lcpc_verify_leaf_paths": (i32, [u8p, u8p, sz, sz, u64p, u8p, u8p]),
+    "lcpc_verify_column_values": (i32, [i32, u64p, sz, sz, u64p, u64p, sz, u64p, u8p]),
     "lcpc_pos_encode_file": (i32, [u8p, sz, sz, sz, sz, u8p, u8p, szp]),
     "lcpc_pos_encode_file_batched": (i32, [u8p, sz, sz, sz, sz, u8p, u8p, szp, sz]),
     "lcpc_pos_writer_new": (i32, [sz, sz, u8p, sz, sz, C.POINTER(vp)]),

@@ -156,7 +156,12 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
 #pragma unroll
         for (int i = 0; i < N; i++) w[i] = 0;
       } else {
+#ifdef LCPC_EXP_RAW_REPR
+#pragma unroll
+        for (int i = 0; i < N; i++) w[i] = cur[k].v[i];
+#else
         fe_repr_words<F>(cur[k], w);
+#endif
       }
 #pragma unroll
       for (int i = 0; i < N; i++) msg[k * N + i] = w[i];

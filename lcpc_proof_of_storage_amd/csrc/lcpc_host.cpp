@@ -1277,6 +1277,88 @@ int lcpc_verify_column_path(lcpc_field f, const uint64_t *col, size_t n_rows, co
   return flag != 0;
 }
 
+lcpc_status lcpc_hash_field_columns(lcpc_field f, const uint64_t *cols, size_t n_rows, size_t n_cols,
+                                    uint8_t *out) {
+  // hash_field_vec_to_digest / hash_column_to_digest (lcpc_online.rs:431-452) for n_cols
+  // columns given one after another ([n_cols][n_rows])
+  if (!valid_field(f) || !field_gpu_supported(f)) return fail(LCPC_ERR_UNSUPPORTED, "field");
+  if ((!cols && n_rows * n_cols) || (!out && n_cols)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (!n_cols) return LCPC_OK;
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  const int wb = field_bytes(f);
+  DBuf dm, dl, scratch;
+  if ((st = upload(dev, dm, cols, n_rows * n_cols * wb))) return st;
+  HIP_TRY(dl.alloc(dev, n_cols * 32));
+  HIP_TRY(scratch.alloc(dev, leaf_hash_scratch_bytes(f, n_rows, n_cols)));
+  HIP_TRY(leaf_hashes_cols(f, dm.as<uint32_t>(), n_rows, n_cols, dl.as<uint8_t>(), scratch.p, lease.s));
+  HIP_TRY(hipMemcpyAsync(out, dl.p, n_cols * 32, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_verify_leaf_paths(const uint8_t *leaves, const uint8_t *paths, size_t n,
+                                   size_t path_len, const uint64_t *idx, const uint8_t root[32],
+                                   uint8_t *ok) {
+  // client_online_verify_column_paths_without_full_columns (lcpc_online.rs:280-318): ok[k] = 1
+  // iff the path of leaf digest k at column idx[k] hashes up to root
+  if ((!leaves || !paths || !idx || !ok) && n) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (!root) return fail(LCPC_ERR_INVALID_ARG, "null root");
+  if (!n) return LCPC_OK;
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf dl, dp, di, dr, dfl;
+  if ((st = upload(dev, dl, leaves, n * 32)) || (st = upload(dev, dp, paths, n * path_len * 32 + 32)) ||
+      (st = upload(dev, di, idx, n * 8)) || (st = upload(dev, dr, root, 32)))
+    return st;
+  HIP_TRY(dfl.alloc(dev, n * 4));
+  HIP_TRY(path_checks(dl.as<uint8_t>(), dp.as<uint8_t>(), n, path_len, di.as<uint64_t>(), dr.as<uint8_t>(),
+                      dfl.as<uint32_t>(), lease.s));
+  std::vector<uint32_t> fl(n);
+  HIP_TRY(hipMemcpyAsync(fl.data(), dfl.p, n * 4, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  for (size_t k = 0; k < n; k++) ok[k] = fl[k] ? 1 : 0;
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_verify_column_values(lcpc_field f, const uint64_t *cols, size_t n, size_t n_rows,
+                                      const uint64_t *tensor, const uint64_t *values, size_t n_values,
+                                      const uint64_t *idx, uint8_t *ok) {
+  // verify_column_value (lcpc-2d/src/lib.rs:1014-1030) for n columns at once, also
+  // verify_proper_partial_polynomial_evaluation's check (lcpc_online.rs:487-516): ok[k] = 1 iff
+  // sum_r tensor[r] cols[k][r] == values[idx[k]]
+  if (!valid_field(f) || !field_gpu_supported(f)) return fail(LCPC_ERR_UNSUPPORTED, "field");
+  if ((!cols || !idx || !ok) && n) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if ((!tensor && n_rows) || (!values && n_values)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  for (size_t k = 0; k < n; k++)
+    if (idx[k] >= n_values) return fail(LCPC_ERR_INVALID_ARG, "value index out of range");
+  if (!n) return LCPC_OK;
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  const int wb = field_bytes(f);
+  DBuf dc, dt, dv, di, dfl;
+  if ((st = upload(dev, dc, cols, n * n_rows * wb)) || (st = upload(dev, dt, tensor, n_rows * wb)) ||
+      (st = upload(dev, dv, values, n_values * wb)) || (st = upload(dev, di, idx, n * 8)))
+    return st;
+  HIP_TRY(dfl.alloc(dev, n * 4));
+  HIP_TRY(column_checks(f, dc.as<uint32_t>(), n, n_rows, dt.as<uint32_t>(), 1, dv.as<uint32_t>(), n_values,
+                        di.as<uint64_t>(), dfl.as<uint32_t>(), lease.s));
+  std::vector<uint32_t> fl(n);
+  HIP_TRY(hipMemcpyAsync(fl.data(), dfl.p, n * 4, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  for (size_t k = 0; k < n; k++) ok[k] = fl[k] ? 1 : 0;
+  return LCPC_OK;
+}
+
 int lcpc_verify_column_value(lcpc_field f, const uint64_t *col, const uint64_t *tensor,
                              size_t n_rows, const uint64_t *poly_eval) {
   if (!valid_field(f)) return 0;

@@ -10,7 +10,13 @@ commitment (names kept):
   lcpc_online::{convert_file_data_to_commit, verifiable_polynomial_evaluation, decode_row,
                 form_side_vectors_for_polynomial_evaluation_from_point,
                 server_retreive_columns, hash_column_to_digest,
-                client_online_verify_column_paths}       lcpc_online.rs:80-627
+                client_online_verify_column_paths[_without_full_columns],
+                client_online_verify_column_leaves, client_verify_commitment[_without_full_columns],
+                hash_column_to_digest, hash_field_vec_to_digest, _get_POS_soundness_n_cols,
+                verify_proper_partial_polynomial_evaluation, verifiable_full_polynomial_evaluation,
+                verify_full_polynomial_evaluation_wrapper_with_single_eval_point}
+                                                         lcpc_online.rs:80-627
+  lcpc_online::file_handler::left_multiply_unencoded_matrix_by_vector   file_handler.rs:614-638
 The field is WriteableFt63: the modulus, arithmetic and repr of FT63.
 """
 from __future__ import annotations
@@ -23,8 +29,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from . import _native as N
-from .lcpc2d import (FT63, LcColumn, LcCommit, LigeroEncoding, ProverError, _p64, _raise,
-                     limbs, verify_column_path)
+from .lcpc2d import (FT63, VERIFIER, LcColumn, LcCommit, LigeroEncoding, ProverError, VerifierError,
+                     _p64, _raise, collapse_columns, limbs, verify_column_path)
 
 WRITTEN_BYTES_WIDTH = 8   # size_of::<WriteableFt63>() (data_field.rs:24)
 DATA_BYTE_CAPACITY = 7    # CAPACITY / 8 (data_field.rs:22)
@@ -184,8 +190,201 @@ def server_retreive_columns(comm: LcCommit, requested_columns: Sequence[int]) ->
     return comm.open_columns(list(requested_columns))
 
 
+def field_dot(a, b, field: int = FT63) -> np.ndarray:
+    """fields::vector_multiply (fields.rs): sum_i a[i] b[i], on the GPU (a one-column collapse)."""
+    nl = limbs(field)
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.uint64).reshape(-1))
+    b = np.ascontiguousarray(np.asarray(b, dtype=np.uint64).reshape(-1))
+    n = min(a.size, b.size) // nl
+    if n == 0:
+        return np.zeros((1, nl), np.uint64)
+    return collapse_columns(field, a[:n * nl], b[:n * nl], n, 1)
+
+
+def _verifier_error(kind: str, msg: str) -> VerifierError:
+    code = {v: k for k, v in VERIFIER.items()}[kind]
+    return VerifierError(code, msg)
+
+
 def client_online_verify_column_paths(root: bytes, requested_columns: Sequence[int],
-                                      received_columns: Sequence[LcColumn], field: int = FT63) -> bool:
+                                      received_columns: Sequence[LcColumn], field: int = FT63) -> None:
+    """lcpc_online.rs:251-277: every received column's Merkle path leads to root.
+    Raises VerifierError(ColumnEval) otherwise, as the reference's Err."""
     if len(requested_columns) != len(received_columns):
-        return False
-    return all(verify_column_path(field, c, i, root) for i, c in zip(requested_columns, received_columns))
+        raise _verifier_error("ColumnEval", "column count")
+    if not received_columns:
+        return
+    leaves = hash_columns_to_digests(received_columns, field)
+    client_online_verify_column_paths_without_full_columns(
+        root, requested_columns, leaves, [c.path for c in received_columns])
+
+
+def client_online_verify_column_paths_without_full_columns(
+        root: bytes, requested_columns: Sequence[int], received_columns_digests: Sequence[bytes],
+        received_column_paths: Sequence[Sequence[bytes]]) -> None:
+    """lcpc_online.rs:280-318 (the paths checked on the GPU in one launch)."""
+    n = len(requested_columns)
+    if len(received_column_paths) != n or len(received_columns_digests) < n:
+        raise _verifier_error("ColumnEval", "column count")
+    if n == 0:
+        return
+    plen = len(received_column_paths[0])
+    if any(len(p) != plen for p in received_column_paths):
+        raise _verifier_error("ColumnEval", "path lengths differ")
+    leaves = np.frombuffer(b"".join(received_columns_digests[:n]), np.uint8).copy()
+    paths = np.frombuffer(b"".join(b"".join(p) for p in received_column_paths) or b"\0", np.uint8).copy()
+    idx = np.ascontiguousarray(np.array(requested_columns, dtype=np.uint64))
+    ok = np.zeros(n, np.uint8)
+    rp, keep = _u8p(root)
+    _raise(N.load().lcpc_verify_leaf_paths(leaves.ctypes.data_as(N.u8p), paths.ctypes.data_as(N.u8p), n, plen,
+                                           _p64(idx), rp, ok.ctypes.data_as(N.u8p)))
+    if not ok.all():
+        raise _verifier_error("ColumnEval", "Merkle path mismatch")
+
+
+def hash_field_vec_to_digest(column, field: int = FT63) -> bytes:
+    """lcpc_online.rs:439-452: BLAKE3(32 zero bytes || repr of every element)."""
+    return hash_columns_to_digests([column], field)[0]
+
+
+def hash_column_to_digest(column: LcColumn, field: int = FT63) -> bytes:
+    """lcpc_online.rs:431-437."""
+    return hash_field_vec_to_digest(column.col, field)
+
+
+def hash_columns_to_digests(columns, field: int = FT63) -> List[bytes]:
+    """hash_column_to_digest over many columns in one GPU launch."""
+    cols = [np.ascontiguousarray(getattr(c, "col", c), dtype=np.uint64).reshape(-1) for c in columns]
+    if not cols:
+        return []
+    n_rows = cols[0].size // limbs(field)
+    if any(c.size != cols[0].size for c in cols):
+        raise ValueError("columns of different lengths")
+    m = np.ascontiguousarray(np.concatenate(cols)) if n_rows else np.zeros(1, np.uint64)
+    out = np.zeros(32 * len(cols), np.uint8)
+    _raise(N.load().lcpc_hash_field_columns(field, _p64(m), n_rows, len(cols), out.ctypes.data_as(N.u8p)))
+    return [out[32 * i:32 * i + 32].tobytes() for i in range(len(cols))]
+
+
+def client_online_verify_column_leaves(locally_derived_column_leaves: Sequence[bytes],
+                                       requested_columns: Sequence[int],
+                                       received_column_leaves: Sequence[bytes]) -> None:
+    """lcpc_online.rs:321-356 (errors are NumColOpens there, kept)."""
+    if (len(locally_derived_column_leaves) != len(requested_columns)
+            or len(received_column_leaves) != len(requested_columns)):
+        raise _verifier_error("NumColOpens", "leaf count")
+    if any(bytes(a) != bytes(b) for a, b in zip(locally_derived_column_leaves, received_column_leaves)):
+        raise _verifier_error("NumColOpens", "leaf mismatch")
+
+
+def _get_POS_soundness_n_cols(pre_encoded_columns: int, encoded_columns: int) -> int:  # noqa: N802
+    """lcpc_online.rs:363-368 (f64 arithmetic as in Rust)."""
+    den = math.log2((1.0 + pre_encoded_columns / encoded_columns) / 2.0)
+    return min(math.ceil(-128.0 / den), encoded_columns)
+
+
+def get_PoS_soudness_n_cols(num_columns: int, num_encoded_columns: int) -> int:  # noqa: N802
+    """lcpc_online.rs:359-361 (FileMetadata's two widths passed directly)."""
+    return _get_POS_soundness_n_cols(num_columns, num_encoded_columns)
+
+
+def client_verify_commitment(root: bytes, locally_derived_column_leaves: Sequence[bytes],
+                             requested_columns: Sequence[int], received_columns: Sequence[LcColumn],
+                             required_columns_for_soundness: int, field: int = FT63) -> None:
+    """lcpc_online.rs:370-398: the received columns hash to the locally derived leaves and their
+    paths lead to root."""
+    if (required_columns_for_soundness < len(locally_derived_column_leaves)
+            or required_columns_for_soundness < len(requested_columns)
+            or required_columns_for_soundness < len(received_columns)):
+        raise _verifier_error("NumColOpens", "more columns than the soundness count")
+    received_leaves = hash_columns_to_digests(received_columns, field)
+    client_online_verify_column_leaves(locally_derived_column_leaves, requested_columns, received_leaves)
+    client_online_verify_column_paths(root, requested_columns, received_columns, field)
+
+
+def client_verify_commitment_without_full_columns(root: bytes, locally_derived_column_leaves: Sequence[bytes],
+                                                  requested_columns: Sequence[int],
+                                                  received_column_digests: Sequence[bytes],
+                                                  received_column_paths: Sequence[Sequence[bytes]],
+                                                  required_columns_for_soundness: int) -> None:
+    """lcpc_online.rs:400-429."""
+    if (required_columns_for_soundness < len(locally_derived_column_leaves)
+            or required_columns_for_soundness < len(requested_columns)
+            or required_columns_for_soundness < len(received_column_digests)):
+        raise _verifier_error("NumColOpens", "more columns than the soundness count")
+    client_online_verify_column_leaves(locally_derived_column_leaves, requested_columns, received_column_digests)
+    client_online_verify_column_paths_without_full_columns(root, requested_columns, received_column_digests,
+                                                           received_column_paths)
+
+
+def verify_proper_partial_polynomial_evaluation(left_evaluation_column, evaluation_result_vector,
+                                                requested_columns_indices: Sequence[int],
+                                                received_columns: Sequence[LcColumn],
+                                                field: int = FT63) -> None:
+    """lcpc_online.rs:487-516: vector_multiply(left, column) == the result entry of that column.
+    As in the reference, the result entries are taken in increasing column index (the filter
+    over the result vector) and zipped with the columns in the order received."""
+    nl = limbs(field)
+    res = np.ascontiguousarray(np.asarray(evaluation_result_vector, dtype=np.uint64).reshape(-1))
+    n_res = res.size // nl
+    wanted = set(int(i) for i in requested_columns_indices)
+    picked = [i for i in range(n_res) if i in wanted]
+    k = min(len(received_columns), len(picked))
+    if k == 0:
+        return
+    cols = np.ascontiguousarray(np.concatenate(
+        [np.asarray(getattr(c, "col", c), dtype=np.uint64).reshape(-1) for c in received_columns[:k]]))
+    n_rows = cols.size // nl // k
+    left = np.ascontiguousarray(np.asarray(left_evaluation_column, dtype=np.uint64).reshape(-1))
+    if left.size // nl < n_rows:
+        raise _verifier_error("ColumnEval", "left vector shorter than the columns")
+    idx = np.array(picked[:k], dtype=np.uint64)
+    ok = np.zeros(k, np.uint8)
+    _raise(N.load().lcpc_verify_column_values(field, _p64(cols), k, n_rows, _p64(left), _p64(res), n_res,
+                                              _p64(idx), ok.ctypes.data_as(N.u8p)))
+    if not ok.all():
+        raise _verifier_error("ColumnEval", "column value mismatch")
+
+
+def verifiable_full_polynomial_evaluation(left_evaluation_column, right_evaluation_column,
+                                          received_decoded_result_vector, requested_column_indices,
+                                          received_columns, pre_encoded_len: int, encoded_len: int,
+                                          field: int = FT63):
+    """lcpc_online.rs:519-543.  The reference body does not compile as written (it passes an
+    undefined `received_result_vector`); this restates its evident intent: the result is
+    <decoded u^T M, right>, and the decoded vector re-encoded (Enc(u^T M) = u^T Enc(M)) must
+    agree with u^T col at every opened column.  Parity unpinned (no reference output exists)."""
+    nl = limbs(field)
+    dec = np.ascontiguousarray(np.asarray(received_decoded_result_vector, dtype=np.uint64).reshape(-1, nl))
+    right = np.ascontiguousarray(np.asarray(right_evaluation_column, dtype=np.uint64).reshape(-1, nl))
+    result = field_dot(dec[:pre_encoded_len], right[:pre_encoded_len], field)
+    enc = LigeroEncoding.new_from_dims(field, pre_encoded_len, encoded_len)
+    row = np.zeros((encoded_len, nl), np.uint64)
+    row[:min(pre_encoded_len, dec.shape[0])] = dec[:pre_encoded_len]
+    encoded = enc.encode(row)
+    verify_proper_partial_polynomial_evaluation(left_evaluation_column, encoded, requested_column_indices,
+                                                received_columns, field)
+    return result
+
+
+def verify_full_polynomial_evaluation_wrapper_with_single_eval_point(
+        evaluation_point, received_result_vector, n_rows: int, n_cols: int, requested_column_indices,
+        received_columns, pre_encoded_len: int, field: int = FT63):
+    """lcpc_online.rs:545-566 (side vectors from the point, then the check above)."""
+    left, right = form_side_vectors_for_polynomial_evaluation_from_point(evaluation_point, n_rows, n_cols, field)
+    return verifiable_full_polynomial_evaluation(left, right, received_result_vector, requested_column_indices,
+                                                 received_columns, pre_encoded_len, n_cols, field)
+
+
+def left_multiply_unencoded_matrix_by_vector(data: bytes, pre_encoded_size: int, left_vector) -> np.ndarray:
+    """file_handler.rs:614-638: u^T M over the file's unencoded rows (7 bytes per element, rows of
+    pre_encoded_size).  The reference returns an empty vector (its result is `with_capacity`
+    and never resized); this returns the sum it is written to accumulate."""
+    el = convert_byte_vec_to_field_elements_vec(data).reshape(-1)
+    n_rows = -(-el.size // pre_encoded_size)
+    left = np.ascontiguousarray(np.asarray(left_vector, dtype=np.uint64).reshape(-1))
+    if left.size != n_rows:
+        raise ValueError(f"left_vector incorrect size, expected {n_rows} and received {left.size}")
+    m = np.zeros(n_rows * pre_encoded_size, np.uint64)
+    m[:el.size] = el
+    return collapse_columns(FT63, m, left, n_rows, pre_encoded_size)

@@ -578,3 +578,13 @@ def pos_decode_rows(img: bytes, pre: int, enc: int, cap: int, rows: int) -> byte
         coeffs = ifft_oi(0, mont)
         out.append(pos_field_to_bytes(coeffs[:pre], 7 * pre))
     return b"".join(out)
+
+
+def verify_path(leaf: bytes, col: int, path: bytes, root: bytes) -> bool:
+    """lcpc-2d verify_column_path's climb (lib.rs:985-1012) from a leaf digest."""
+    h = leaf
+    for i in range(0, len(path), 32):
+        sib = path[i:i + 32]
+        h = blake3(h + sib) if col % 2 == 0 else blake3(sib + h)
+        col >>= 1
+    return h == root

@@ -116,8 +116,9 @@ def test_request_types(gpu, pos, oracle):
     for k, c in enumerate(cols):
         assert np.array_equal(got[k].reshape(-1), m[:, c])
     opened = pos.convert_file_data_to_commit(coeffs, pos.ColumnsWithPath(cols), pos.Specified(np_, nc))
-    assert pos.client_online_verify_column_paths(ocomm.root(), cols, opened)
-    assert not pos.client_online_verify_column_paths(ocomm.root(), cols[::-1], opened)
+    pos.client_online_verify_column_paths(ocomm.root(), cols, opened)
+    with pytest.raises(pos.VerifierError):
+        pos.client_online_verify_column_paths(ocomm.root(), cols[::-1], opened)
     comm = pos.convert_file_data_to_commit(coeffs, pos.Commit(), pos.Specified(np_, nc))
     for k, c in enumerate(cols):
         one = comm.open_column(c)
@@ -133,3 +134,77 @@ def test_test_txt_golden(gpu, pos):
     assert [comm.get_n_rows(), comm.get_n_per_row(), comm.get_n_cols()] == g["dims"]
     assert comm.get_root().hex() == g["root"]
     assert hashlib.sha256(comm.comm.tobytes()).hexdigest() == g["comm_sha256"]
+
+
+def test_client_verification(gpu, pos, oracle):
+    """The PoS client side (lcpc_online.rs:251-452): leaves recomputed locally (Leaves request),
+    columns with and without paths, soundness counts, and each failure's error kind."""
+    coeffs = oracle.random_coeffs(FT63, 7000, 4)
+    np_, nc = 64, 128
+    ocomm = oracle.Commit(oracle.Encoding.ligero(FT63, np_, nc), coeffs)
+    root = ocomm.root()
+    need = pos._get_POS_soundness_n_cols(np_, nc)
+    cols = oracle.pos_column_indices(99, 20, nc)
+    local = pos.convert_file_data_to_commit(coeffs, pos.Leaves(cols), pos.Specified(np_, nc))
+    opened = pos.convert_file_data_to_commit(coeffs, pos.ColumnsWithPath(cols), pos.Specified(np_, nc))
+    # hash_column_to_digest == the commitment's leaves
+    assert pos.hash_columns_to_digests(opened) == [ocomm.hashes[32 * c:32 * c + 32] for c in cols]
+    assert pos.hash_column_to_digest(opened[3]) == ocomm.hashes[32 * cols[3]:32 * cols[3] + 32]
+    pos.client_verify_commitment(root, local, cols, opened, need)
+    digests = [pos.hash_column_to_digest(c) for c in opened]
+    pos.client_verify_commitment_without_full_columns(root, local, cols, digests, [c.path for c in opened], need)
+    with pytest.raises(pos.VerifierError) as e:  # soundness count below the opened columns
+        pos.client_verify_commitment(root, local, cols, opened, len(cols) - 1)
+    assert e.value.kind == "NumColOpens"
+    bad = [pos.LcColumn(c.col.copy(), c.path) for c in opened]
+    bad[5].col[7, 0] ^= 1
+    with pytest.raises(pos.VerifierError) as e:  # leaves differ from the local ones
+        pos.client_verify_commitment(root, local, cols, bad, need)
+    assert e.value.kind == "NumColOpens"
+    bad_paths = [list(c.path) for c in opened]
+    bad_paths[2][1] = bytes(32)
+    with pytest.raises(pos.VerifierError) as e:
+        pos.client_online_verify_column_paths_without_full_columns(root, cols, digests, bad_paths)
+    assert e.value.kind == "ColumnEval"
+    # the same check against the oracle's path verification
+    for k, c in enumerate(cols):
+        assert oracle.verify_path(digests[k], c, b"".join(opened[k].path), root)
+
+
+def test_partial_and_full_polynomial_evaluation(gpu, pos, oracle):
+    """verify_proper_partial_polynomial_evaluation / verifiable_full_polynomial_evaluation /
+    left_multiply_unencoded_matrix_by_vector on a small file (lcpc_online.rs:454-566)."""
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, 7 * 64 * 40 - 11, dtype=np.uint8).tobytes()
+    np_, nc = 64, 128
+    el = oracle.pos_bytes_to_field(data)
+    n_rows = -(-el.size // np_)
+    comm = pos.convert_file_data_to_commit(el.reshape(-1, 1), pos.Commit(), pos.Specified(np_, nc))
+    x = oracle.ChaCha(seed_u64=77).field_random(FT63, 1)
+    # side vectors over the unencoded width: p(x) = <u^T M, right> with u = left
+    left, right_np = pos.form_side_vectors_for_polynomial_evaluation_from_point(x, n_rows, np_)
+    result = pos.verifiable_polynomial_evaluation(comm, left)            # u^T Enc(M), n_cols
+    decoded = pos.left_multiply_unencoded_matrix_by_vector(data, np_, left)  # u^T M, n_per_row
+    m = np.zeros(n_rows * np_, np.uint64)
+    m[:el.size] = el
+    assert np.array_equal(decoded.reshape(-1), oracle.collapse(FT63, m, left.reshape(-1), n_rows, np_))
+    cols = sorted(oracle.pos_column_indices(5, 12, nc))
+    opened = comm.open_columns(cols)
+    pos.verify_proper_partial_polynomial_evaluation(left, result, cols, opened)
+    tampered = result.copy().reshape(-1)
+    tampered[cols[4]] ^= 1
+    with pytest.raises(pos.VerifierError):
+        pos.verify_proper_partial_polynomial_evaluation(left, tampered, cols, opened)
+    # the full check: <u^T M, right> is p(x) for the file's polynomial, and Enc(u^T M) agrees
+    # with the opened columns
+    got = pos.verifiable_full_polynomial_evaluation(left, right_np, decoded, cols, opened, np_, nc)
+    p = oracle.modulus(FT63)
+    xv = oracle.from_mont(FT63, x)[0]
+    want = 0
+    for c in reversed(oracle.from_mont(FT63, m)):
+        want = (want * xv + c) % p
+    assert oracle.from_mont(FT63, got.reshape(-1))[0] == want
+    bad = decoded.copy()
+    bad[3, 0] = (int(bad[3, 0]) + 1) % p
+    with pytest.raises(pos.VerifierError):
+        pos.verifiable_full_polynomial_evaluation(left, right_np, bad, cols, opened, np_, nc)

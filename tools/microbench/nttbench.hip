@@ -38,7 +38,7 @@ struct Variant {
 };
 
 template <class F>
-void bench(const char *fname, int log_n, size_t rows) {
+void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
   const size_t n = (size_t)1 << log_n, np = n / 2;
   const size_t W = F::N;
   uint32_t *coeffs, *ref, *out, *tw;
@@ -46,6 +46,8 @@ void bench(const char *fname, int log_n, size_t rows) {
   CK(hipMalloc(&ref, rows * n * W * 4));
   CK(hipMalloc(&out, rows * n * W * 4));
   CK(hipMalloc(&tw, n * W * 4));
+  uint32_t *cpy = nullptr;
+  if (with_copy) CK(hipMalloc(&cpy, rows * np * W * 4));
   hipLaunchKernelGGL(k_fill<F>, dim3((rows * np * W + 255) / 256), dim3(256), 0, 0, coeffs, rows * np * W, 12345u);
   hipLaunchKernelGGL((ntt_detail::k_tw_table<F>), dim3((n + 255) / 256), dim3(256), 0, 0, tw, log_n, 0);
   CK(hipDeviceSynchronize());
@@ -66,7 +68,7 @@ void bench(const char *fname, int log_n, size_t rows) {
 #define V2(LA, CWA, TA, LB, CWB, TB)                                                           \
   vs.push_back({"v2 A(S=2^" #LA ",CW=2^" #CWA ",T=2^" #TA ") B(S=2^" #LB ",CW=2^" #CWB ",T=2^" #TB ")", \
                 [&](const uint32_t *c, uint32_t *o, hipStream_t st) {                          \
-                  CK((ntt_v2::launch_a<F, LA, CWA, TA, true>(c, np, np, o, n, tw, log_n, rows, st, nullptr, 0))); \
+                  CK((ntt_v2::launch_a<F, LA, CWA, TA, true>(c, np, np, o, n, tw, log_n, rows, st, cpy, np))); \
                   CK((ntt_v2::launch_b<F, LB, CWB, TB>(o, n, tw, log_n, rows, st)));           \
                 }});
   if constexpr (F::ID == 1) {
@@ -87,11 +89,27 @@ void bench(const char *fname, int log_n, size_t rows) {
       V2(7, 2, 6, 7, 2, 6)
     }
   } else if constexpr (F::ID == 0) {
-    V2(8, 4, 8, 8, 4, 8)
-    V2(8, 3, 8, 8, 3, 8)
-    V2(8, 4, 9, 8, 4, 9)
-    V2(8, 5, 9, 8, 5, 9)
-    V2(8, 3, 7, 8, 3, 7)
+    if (log_n == 15) {  // PoS default dims: l1 = 7, l2 = 8; pass-A shapes at a fixed pass B, then B
+      V2(7, 5, 9, 8, 4, 9)
+      V2(7, 3, 7, 8, 4, 9)
+      V2(7, 3, 8, 8, 4, 9)
+      V2(7, 4, 8, 8, 4, 9)
+      V2(7, 4, 9, 8, 4, 9)
+      V2(7, 5, 10, 8, 4, 9)
+      V2(7, 6, 10, 8, 4, 9)
+      V2(7, 2, 7, 8, 4, 9)
+      V2(7, 5, 9, 8, 3, 8)
+      V2(7, 5, 9, 8, 2, 7)
+      V2(7, 5, 9, 8, 3, 9)
+      V2(7, 5, 9, 8, 2, 8)
+      V2(7, 5, 9, 8, 1, 7)
+    } else {
+      V2(8, 4, 8, 8, 4, 8)
+      V2(8, 3, 8, 8, 3, 8)
+      V2(8, 4, 9, 8, 4, 9)
+      V2(8, 5, 9, 8, 5, 9)
+      V2(8, 3, 7, 8, 3, 7)
+    }
   } else {
     V2(8, 2, 8, 9, 1, 8)
     V2(8, 3, 8, 9, 2, 8)
@@ -137,6 +155,7 @@ int main(int argc, char **argv) {
   const int which = argc > 1 ? atoi(argv[1]) : 1;
   if (which == 1) { bench<Ft127>("Ft127", 16, 512); bench<Ft127>("Ft127", 14, 128); }
   if (which == 0) bench<Ft63>("Ft63", 16, 512);
+  if (which == 5) bench<Ft63>("Ft63 PoS 1 GiB (copy)", 15, 9363, true);
   if (which == 3) bench<Ft255>("Ft255", 17, 256);
   return 0;
 }
