@@ -38,8 +38,8 @@ SEED = 0x1CDC2024       # coefficients = F::random(ChaCha20Rng
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=24)
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--log-len", type=int, default=24)
     ap.add_argument("--field", default="Ft127")
     ap.add_argument("--code", choices=["ligero", "sdig", "pos"], default="ligero",

@@ -174,6 +174,10 @@ lcpc_status lcpc_commit_copy_hashes(const lcpc_commit *c, uint8_t *out);
  * for Ligero and element-major [n_cols][n_rows] for SDIG (lcpc_commit_col_major() == 1), where
  * every Merkle leaf is one contiguous column; copy_comm always returns the row-major layout. */
 int lcpc_commit_col_major(const lcpc_commit *c);
+/* 1 if the device codeword (lcpc_commit_device_comm) holds canonical values rather than
+ * Montgomery words (R-S / Ligero commitments: the encode writes them so, and the Merkle leaves
+ * hash canonical bytes); copy_comm and the opened columns are Montgomery either way. */
+int lcpc_commit_comm_canonical(const lcpc_commit *c);
 const void *lcpc_commit_device_comm(const lcpc_commit *c);
 const void *lcpc_commit_device_coeffs(const lcpc_commit *c);
 /* check_comm (:703-718) */

@@ -73,6 +73,7 @@ SIGNATURES = {
     "lcpc_commit_copy_hashes": (i32, [vp, u8p]),
     "lcpc_commit_col_major": (i32, [vp]),
     "lcpc_commit_device_comm": (vp, [vp]),
+    "lcpc_commit_comm_canonical": (i32, [vp]),
     "lcpc_commit_device_coeffs": (vp, [vp]),
     "lcpc_check_comm": (i32, [vp, vp]),
     "lcpc_open_column": (i32, [vp, sz, u64p, u8p]),

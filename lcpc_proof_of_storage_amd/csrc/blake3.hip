@@ -111,7 +111,7 @@ __device__ __forceinline__ void store8(uint32_t *p, const uint32_t v[8]) {
 // every 16-word block holds whole elements.  The launch covers chunks [chunk0, chunk_end) of
 // messages of n_rows rows; m holds rows [row0, ...) (a row shard: every row those chunks read
 // is present), and chaining values go to cvs[chunk - chunk0][col].
-template <class F>
+template <class F, bool CANON>
 __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict__ m,
                                                      size_t n_rows, size_t n_cols,
                                                      size_t row_stride, size_t col_stride,
@@ -155,13 +155,10 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
       if (ew < 0 || (size_t)ew / N >= n_rows) {
 #pragma unroll
         for (int i = 0; i < N; i++) w[i] = 0;
+      } else if constexpr (CANON) {
+        fe_canon_repr_words<F>(cur[k], w);
       } else {
-#ifdef LCPC_EXP_RAW_REPR
-#pragma unroll
-        for (int i = 0; i < N; i++) w[i] = cur[k].v[i];
-#else
         fe_repr_words<F>(cur[k], w);
-#endif
       }
 #pragma unroll
       for (int i = 0; i < N; i++) msg[k * N + i] = w[i];
@@ -253,12 +250,13 @@ __global__ __launch_bounds__(256) void k_merkle(uint8_t *__restrict__ hashes, si
 template <class F>
 __global__ void k_gather_cols(const uint32_t *__restrict__ m, size_t n_rows, size_t n_cols,
                               const uint64_t *__restrict__ idx, size_t n_idx,
-                              uint32_t *__restrict__ cols, int col_major) {
+                              uint32_t *__restrict__ cols, int col_major, int canon) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_idx * n_rows) return;
   const size_t k = t / n_rows, r = t % n_rows;
   const size_t at = col_major ? idx[k] * n_rows + r : r * n_cols + idx[k];
-  fe_store<F>(cols, t, fe_load<F>(m, at));
+  const Fe<F> x = fe_load<F>(m, at);
+  fe_store<F>(cols, t, canon ? fe_to_mont<F>(x) : x);
 }
 
 __global__ void k_gather_paths(const uint8_t *__restrict__ hashes, size_t np2,
@@ -311,7 +309,7 @@ size_t leaf_hash_scratch_bytes(int fid, size_t n_rows, size_t n_cols) {
 
 static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
                                       size_t row_stride, size_t col_stride, uint8_t *leaves,
-                                      void *scratch, hipStream_t s) {
+                                      void *scratch, hipStream_t s, bool canon) {
   if (n_cols == 0) return hipSuccess;
   const size_t words = 8 + n_rows * (size_t)field_words(fid);
   const int n_chunks = (int)((words + 255) / 256);
@@ -319,8 +317,12 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
   hipError_t e = dispatch_field(fid, [&]<class F>() {
     if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
       prof::Scope ps("leaf_chunks", s);
-      hipLaunchKernelGGL((k_leaf_chunks<F>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
-                         col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
+      if (canon)
+        hipLaunchKernelGGL((k_leaf_chunks<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
+                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
+      else
+        hipLaunchKernelGGL((k_leaf_chunks<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
+                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
       return hipGetLastError();
     } else {
       return hipErrorInvalidValue;
@@ -339,16 +341,21 @@ size_t leaf_n_chunks(int fid, size_t n_rows) {
 
 hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows, size_t n_cols,
                           size_t stride, size_t chunk_lo, size_t chunk_hi, uint32_t *cvs,
-                          hipStream_t s) {
+                          hipStream_t s, bool canon) {
   if (n_cols == 0 || chunk_hi <= chunk_lo) return hipSuccess;
   const int n_chunks = (int)leaf_n_chunks(fid, n_rows);
   dim3 grid((unsigned)((n_cols + 63) / 64), (unsigned)((chunk_hi - chunk_lo + 3) / 4));
   return dispatch_field(fid, [&]<class F>() {
     if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
       prof::Scope ps("leaf_chunks", s);
-      hipLaunchKernelGGL((k_leaf_chunks<F>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
-                         (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
-                         (int)chunk_hi);
+      if (canon)
+        hipLaunchKernelGGL((k_leaf_chunks<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
+                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
+                           (int)chunk_hi);
+      else
+        hipLaunchKernelGGL((k_leaf_chunks<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
+                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
+                           (int)chunk_hi);
       return hipGetLastError();
     } else {
       return hipErrorInvalidValue;
@@ -367,14 +374,14 @@ hipError_t leaves_from_cvs(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t *
 }
 
 hipError_t leaf_hashes(int fid, const uint32_t *m, size_t n_rows, size_t n_cols, size_t stride,
-                       uint8_t *leaves, void *scratch, hipStream_t s) {
-  return leaf_hashes_strided(fid, m, n_rows, n_cols, stride, 1, leaves, scratch, s);
+                       uint8_t *leaves, void *scratch, hipStream_t s, bool canon) {
+  return leaf_hashes_strided(fid, m, n_rows, n_cols, stride, 1, leaves, scratch, s, canon);
 }
 
 hipError_t leaf_hashes_cols(int fid, const uint32_t *cols, size_t n_rows, size_t n_cols,
-                            uint8_t *leaves, void *scratch, hipStream_t s) {
+                            uint8_t *leaves, void *scratch, hipStream_t s, bool canon) {
   // cols laid out [column][row]
-  return leaf_hashes_strided(fid, cols, n_rows, n_cols, 1, n_rows, leaves, scratch, s);
+  return leaf_hashes_strided(fid, cols, n_rows, n_cols, 1, n_rows, leaves, scratch, s, canon);
 }
 
 hipError_t merkle_tree(uint8_t *hashes, size_t np2, hipStream_t s) {
@@ -402,13 +409,13 @@ hipError_t merkle_tree_io(const uint8_t *ins, size_t n_ins, uint8_t *outs, hipSt
 
 hipError_t gather_columns(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
                           const uint64_t *idx, size_t n_idx, uint32_t *cols, hipStream_t s,
-                          bool col_major) {
+                          bool col_major, bool canon) {
   const size_t n = n_idx * n_rows;
   if (!n) return hipSuccess;
   return dispatch_field(fid, [&]<class F>() {
     prof::Scope ps("gather_cols", s);
     hipLaunchKernelGGL((k_gather_cols<F>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, m,
-                       n_rows, n_cols, idx, n_idx, cols, col_major ? 1 : 0);
+                       n_rows, n_cols, idx, n_idx, cols, col_major ? 1 : 0, canon ? 1 : 0);
     return hipGetLastError();
   });
 }

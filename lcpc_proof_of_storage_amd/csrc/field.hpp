@@ -430,6 +430,18 @@ __device__ __forceinline__ void fe_repr_words(const Fe<F>& a, uint32_t* w) {
   }
 }
 
+// repr words of a value already in canonical form (no Montgomery conversion)
+template <class F>
+__device__ __forceinline__ void fe_canon_repr_words(const Fe<F>& c, uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {
+    if constexpr (F::BE_REPR)
+      w[i] = __builtin_bswap32(c.v[F::N - 1 - i]);
+    else
+      w[i] = c.v[i];
+  }
+}
+
 // ---------------------------------------------------------------- memory
 // Elements are 8/16/24/32 bytes; move them with the widest aligned vector loads.
 template <class F>

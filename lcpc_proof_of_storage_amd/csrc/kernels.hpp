@@ -21,7 +21,8 @@ bool field_gpu_supported(int fid);
 struct NttPlan {
   int fid = -1;
   int log_n = 0, l1 = 0, l2 = 0;
-  uint32_t *d_tw = nullptr;  // w^e, e in [0, n): n elements (Montgomery)
+  uint32_t *d_tw = nullptr;        // w^e, e in [0, n): n elements (Montgomery)
+  uint32_t *d_tw_canon = nullptr;  // forward plans: the same values' canonical words (below)
 };
 hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream_t s);
 void ntt_plan_free(NttPlan &p);
@@ -31,29 +32,35 @@ void ntt_plan_free(NttPlan &p);
 // copy (optional): the n_valid input coefficients of row r are also written to
 // copy + r * copy_stride by the first pass, which reads them anyway (commit keeps its own
 // coefficient matrix without a separate device-to-device copy).
+// canon_out: the outputs are written in canonical form instead of Montgomery form.  The
+// transform is linear, so pass A multiplies by w^e R^-1 -- whose Montgomery words are the
+// canonical words of w^e (d_tw_canon) -- at no extra cost, and every output's Montgomery words
+// become its canonical value: commitments hash their codeword without a per-element
+// conversion (the Merkle leaves are over canonical bytes).
 hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
                     uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s,
-                    uint32_t *copy = nullptr, size_t copy_stride = 0);
+                    uint32_t *copy = nullptr, size_t copy_stride = 0, bool canon_out = false);
 
 // ------------------------------------------------------------------ BLAKE3 / Merkle
 // leaf[j] = BLAKE3(32 zero bytes || repr(m[0][j]) || ... || repr(m[n_rows-1][j]))
 // for j in [0, n_cols); m is row-major with row stride `stride` elements.
+// canon: the matrix holds canonical values (ntt_rows canon_out) instead of Montgomery form.
 size_t leaf_hash_scratch_bytes(int fid, size_t n_rows, size_t n_cols);
 hipError_t leaf_hashes(int fid, const uint32_t *m, size_t n_rows, size_t n_cols, size_t stride,
-                       uint8_t *leaves, void *scratch, hipStream_t s);
+                       uint8_t *leaves, void *scratch, hipStream_t s, bool canon = false);
 // Row shards: chaining values of chunks [chunk_lo, chunk_hi) of every column's leaf message
 // (messages of n_rows rows in total) from a row-major shard m holding rows [row0, ...);
 // cvs[(chunk - chunk_lo) * n_cols + col] (8 words).  Chunk c starts at message byte 1024 c.
 size_t leaf_n_chunks(int fid, size_t n_rows);
 hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows, size_t n_cols,
                           size_t stride, size_t chunk_lo, size_t chunk_hi, uint32_t *cvs,
-                          hipStream_t s);
+                          hipStream_t s, bool canon = false);
 // leaf digests from all n_chunks chaining values ([chunk][col] layout; cvs is clobbered)
 hipError_t leaves_from_cvs(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t *leaves,
                            hipStream_t s);
 // same, for a [column][row] matrix (opened columns of a proof)
 hipError_t leaf_hashes_cols(int fid, const uint32_t *cols, size_t n_rows, size_t n_cols,
-                            uint8_t *leaves, void *scratch, hipStream_t s);
+                            uint8_t *leaves, void *scratch, hipStream_t s, bool canon = false);
 // hashes = [leaves (np2) | level 1 (np2/2) | ... | root]; fills every level above the leaves
 hipError_t merkle_tree(uint8_t *hashes, size_t np2, hipStream_t s);
 // generic Merkle over ins (n_ins = outs + 1 nodes, power of two) -> outs
@@ -68,11 +75,12 @@ hipError_t collapse_rows(int fid, const uint32_t *coeffs, size_t n_rows, size_t 
 // out[c] = sum_k vecs[k][c] (n_vecs vectors of len elements)
 hipError_t collapse_fold_rows(int fid, const uint32_t *vecs, size_t n_vecs, size_t len, uint32_t *out,
                               hipStream_t s);
-// cols[k][r] = m[r][idx[k]] (m row-major) or m[idx[k]][r] (col_major);
+// cols[k][r] = m[r][idx[k]] (m row-major) or m[idx[k]][r] (col_major); canon: m holds
+// canonical values and the gathered columns are converted to Montgomery form;
 // paths[k][i] = sibling digests of leaf idx[k]
 hipError_t gather_columns(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
                           const uint64_t *idx, size_t n_idx, uint32_t *cols, hipStream_t s,
-                          bool col_major = false);
+                          bool col_major = false, bool canon = false);
 hipError_t gather_paths(const uint8_t *hashes, size_t n_hashes, const uint64_t *idx,
                         size_t n_idx, size_t path_len, uint8_t *paths, hipStream_t s);
 

@@ -357,6 +357,7 @@ struct lcpc_commit {
   Device *dev = nullptr;
   size_t n_rows = 0, n_cols = 0, n_per_row = 0, n_hashes = 0;
   bool col_major = false;  // comm stored [n_cols][n_rows] (SDIG) instead of [n_rows][n_cols]
+  bool canon = false;      // comm holds canonical values (R-S: ntt_rows canon_out), not Montgomery
   DBuf coeffs, comm, hashes;
   uint8_t root[32];
 };
@@ -567,22 +568,24 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
     HIP_TRY(tmp.alloc(dev, e->sdig.tmp_elems * n_rows * wb));
     HIP_TRY(sdig_encode_cm(e->sdig, (uint32_t *)cm, n_rows, tmp.as<uint32_t>(), s));
   } else if (src_is_host) {
+    c->canon = true;
     HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb, hipMemcpyHostToDevice, s));
     if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
-    HIP_TRY(ntt_rows(e->plan, (const uint32_t *)cf, np, np, (uint32_t *)cm, nc, n_rows, s));
+    HIP_TRY(ntt_rows(e->plan, (const uint32_t *)cf, np, np, (uint32_t *)cm, nc, n_rows, s, nullptr, 0, true));
   } else {
     // full rows are encoded straight from the caller's buffer; the first NTT pass writes the
     // commitment's own coefficient copy as it reads them (no separate D2D copy)
+    c->canon = true;
     const size_t full = len / np, tail = len - full * np;
     HIP_TRY(ntt_rows(e->plan, (const uint32_t *)d_src, np, np, (uint32_t *)cm, nc, full, s,
-                     (uint32_t *)cf, np));
+                     (uint32_t *)cf, np, true));
     if (tail) {
       uint8_t *last = cf + full * np * wb;
       HIP_TRY(hipMemcpyAsync(last, (const uint8_t *)d_src + full * np * wb, tail * wb,
                              hipMemcpyDeviceToDevice, s));
       HIP_TRY(hipMemsetAsync(last + tail * wb, 0, (np - tail) * wb, s));
       HIP_TRY(ntt_rows(e->plan, (const uint32_t *)last, np, np, (uint32_t *)(cm + full * nc * wb),
-                       nc, 1, s));
+                       nc, 1, s, nullptr, 0, true));
     }
   }
   // Merkle tree (:685-697, merkleize :720-734); leaves past n_cols stay zero digests
@@ -593,7 +596,8 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   if (c->col_major)
     HIP_TRY(leaf_hashes_cols(fid, c->comm.as<uint32_t>(), n_rows, nc, c->hashes.as<uint8_t>(), scratch.p, s));
   else
-    HIP_TRY(leaf_hashes(fid, c->comm.as<uint32_t>(), n_rows, nc, nc, c->hashes.as<uint8_t>(), scratch.p, s));
+    HIP_TRY(leaf_hashes(fid, c->comm.as<uint32_t>(), n_rows, nc, nc, c->hashes.as<uint8_t>(), scratch.p, s,
+                        c->canon));
   HIP_TRY(merkle_tree(c->hashes.as<uint8_t>(), np2, s));
   HIP_TRY(hipMemcpyAsync(c->root, c->hashes.as<uint8_t>() + (c->n_hashes - 1) * 32, 32,
                          hipMemcpyDeviceToHost, s));
@@ -865,6 +869,16 @@ static lcpc_status copy_out(const lcpc_commit *c, void *dst, const void *src, si
 }
 lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out) {
   const size_t bytes = c->n_rows * c->n_cols * field_bytes(c->fid);
+  if (c->canon) {  // canonical on the device -> the reference's Montgomery words
+    Lease lease(c->dev);
+    HIP_TRY(hipSetDevice(c->dev->id));
+    DBuf mm;
+    HIP_TRY(mm.alloc(c->dev, bytes));
+    HIP_TRY(convert(c->fid, c->comm.as<uint32_t>(), mm.as<uint32_t>(), c->n_rows * c->n_cols, true, lease.s));
+    HIP_TRY(hipMemcpyAsync(out, mm.p, bytes, hipMemcpyDeviceToHost, lease.s));
+    HIP_TRY(hipStreamSynchronize(lease.s));
+    return LCPC_OK;
+  }
   if (!c->col_major) return copy_out(c, out, c->comm.p, bytes);
   // element-major on the device -> the reference's row-major Vec<F>
   Lease lease(c->dev);
@@ -878,6 +892,7 @@ lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out) {
   return LCPC_OK;
 }
 int lcpc_commit_col_major(const lcpc_commit *c) { return c->col_major ? 1 : 0; }
+int lcpc_commit_comm_canonical(const lcpc_commit *c) { return c->canon ? 1 : 0; }
 lcpc_status lcpc_commit_copy_coeffs(const lcpc_commit *c, uint64_t *out) {
   return copy_out(c, out, c->coeffs.p, c->n_rows * c->n_per_row * field_bytes(c->fid));
 }
@@ -911,7 +926,7 @@ lcpc_status lcpc_open_column(const lcpc_commit *c, size_t column, uint64_t *col_
   HIP_TRY(dcol.alloc(dev, c->n_rows * wb));
   HIP_TRY(dpath.alloc(dev, path_len * 32));
   HIP_TRY(gather_columns(c->fid, c->comm.as<uint32_t>(), c->n_rows, c->n_cols, didx.as<uint64_t>(), 1,
-                         dcol.as<uint32_t>(), lease.s, c->col_major));
+                         dcol.as<uint32_t>(), lease.s, c->col_major, c->canon));
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), 1, path_len,
                        dpath.as<uint8_t>(), lease.s));
   if (col_out) HIP_TRY(hipMemcpyAsync(col_out, dcol.p, c->n_rows * wb, hipMemcpyDeviceToHost, lease.s));
@@ -1031,7 +1046,7 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   HIP_TRY(dcols.alloc(dev, nco * nr * wb));
   HIP_TRY(dpaths.alloc(dev, nco * p->path_len * 32));
   HIP_TRY(gather_columns(fid, c->comm.as<uint32_t>(), nr, c->n_cols, didx.as<uint64_t>(), nco,
-                         dcols.as<uint32_t>(), s, c->col_major));
+                         dcols.as<uint32_t>(), s, c->col_major, c->canon));
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), nco, p->path_len,
                        dpaths.as<uint8_t>(), s));
   if (nco) {
@@ -1590,6 +1605,8 @@ lcpc_status lcpc_pos_eval_encoded(const lcpc_commit *c, const uint64_t *left, si
   HIP_TRY(scratch.alloc(dev, collapse_scratch_bytes(c->fid, n_rows, c->n_cols, 1)));
   HIP_TRY(collapse_rows(c->fid, c->comm.as<uint32_t>(), n_rows, c->n_cols, dt.as<uint32_t>(), 1,
                         dout.as<uint32_t>(), scratch.p, lease.s));
+  // over a canonical matrix the Montgomery products come out as canonical values
+  if (c->canon) HIP_TRY(convert(c->fid, dout.as<uint32_t>(), dout.as<uint32_t>(), c->n_cols, true, lease.s));
   HIP_TRY(hipMemcpyAsync(out, dout.p, c->n_cols * wb, hipMemcpyDeviceToHost, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
@@ -1656,7 +1673,7 @@ lcpc_status lcpc_open_columns(const lcpc_commit *c, const uint64_t *idx, size_t 
   HIP_TRY(dcol.alloc(dev, n * c->n_rows * wb));
   HIP_TRY(dpath.alloc(dev, n * path_len * 32 + 32));
   HIP_TRY(gather_columns(c->fid, c->comm.as<uint32_t>(), c->n_rows, c->n_cols, didx.as<uint64_t>(), n,
-                         dcol.as<uint32_t>(), lease.s, c->col_major));
+                         dcol.as<uint32_t>(), lease.s, c->col_major, c->canon));
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), n, path_len,
                        dpath.as<uint8_t>(), lease.s));
   if (cols_out) HIP_TRY(hipMemcpyAsync(cols_out, dcol.p, n * c->n_rows * wb, hipMemcpyDeviceToHost, lease.s));
@@ -1758,11 +1775,11 @@ static lcpc_status shard_new_impl(const lcpc_encoding *e, const void *coeffs, bo
   HIP_TRY(sh->comm.alloc(dev, n_shard_rows * nc * wb + 16));
   if (n_shard_rows && on_device) {  // encode straight from the caller's rows; pass A copies them
     HIP_TRY(ntt_rows(e->plan, (const uint32_t *)coeffs, np, np, sh->comm.as<uint32_t>(), nc, n_shard_rows,
-                     lease.s, sh->coeffs.as<uint32_t>(), np));
+                     lease.s, sh->coeffs.as<uint32_t>(), np, true));
   } else if (n_shard_rows) {
     HIP_TRY(hipMemcpyAsync(sh->coeffs.p, coeffs, n_shard_rows * np * wb, hipMemcpyHostToDevice, lease.s));
     HIP_TRY(ntt_rows(e->plan, sh->coeffs.as<uint32_t>(), np, np, sh->comm.as<uint32_t>(), nc, n_shard_rows,
-                     lease.s));
+                     lease.s, nullptr, 0, true));
   }
   HIP_TRY(hipStreamSynchronize(lease.s));
   sh->coeffs.settle();
@@ -1799,7 +1816,7 @@ lcpc_status lcpc_shard_chunk_cvs(const lcpc_shard *s, size_t chunk_lo, size_t ch
   DBuf cvs;
   HIP_TRY(cvs.alloc(dev, (chunk_hi - chunk_lo) * nc * 32));
   HIP_TRY(leaf_chunk_cvs(fid, s->comm.as<uint32_t>(), s->row0, s->n_rows_total, nc, nc, chunk_lo, chunk_hi,
-                         cvs.as<uint32_t>(), lease.s));
+                         cvs.as<uint32_t>(), lease.s, true));
   HIP_TRY(hipMemcpyAsync(out, cvs.p, (chunk_hi - chunk_lo) * nc * 32, hipMemcpyDeviceToHost, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
@@ -1864,7 +1881,7 @@ lcpc_status lcpc_shard_gather_columns(const lcpc_shard *s, const uint64_t *idx, 
   if ((st = upload(dev, didx, idx, n * 8))) return st;
   HIP_TRY(dcol.alloc(dev, n * s->n_rows * wb));
   HIP_TRY(gather_columns(fid, s->comm.as<uint32_t>(), s->n_rows, nc, didx.as<uint64_t>(), n,
-                         dcol.as<uint32_t>(), lease.s));
+                         dcol.as<uint32_t>(), lease.s, false, true));
   HIP_TRY(hipMemcpyAsync(out, dcol.p, n * s->n_rows * wb, hipMemcpyDeviceToHost, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
@@ -2136,13 +2153,14 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
       if (B * pre > ne)
         HIP_TRY(hipMemsetAsync(w->coeffs.as<uint8_t>() + ne * POS_WB, 0, (B * pre - ne) * POS_WB, s));
       HIP_TRY(pos_pack7(w->dbytes.as<uint8_t>(), b1 - b0, w->coeffs.as<uint64_t>(), s));
-      HIP_TRY(ntt_rows(w->e->plan, w->coeffs.as<uint32_t>(), pre, pre, w->comm.as<uint32_t>(), enc, B, s));
-      HIP_TRY(transpose_elems(fid, w->comm.as<uint32_t>(), B, enc, enc, enc, w->dout.as<uint32_t>(), B, s,
-                              TR_FROM_MONT));
+      // canonical codeword: the file's repr words and the leaves' input without conversion
+      HIP_TRY(ntt_rows(w->e->plan, w->coeffs.as<uint32_t>(), pre, pre, w->comm.as<uint32_t>(), enc, B, s,
+                       nullptr, 0, true));
+      HIP_TRY(transpose_elems(fid, w->comm.as<uint32_t>(), B, enc, enc, enc, w->dout.as<uint32_t>(), B, s));
     }
     // column-digest chunks of these rows (ColumnDigestAccumulator::update, :62-87)
     HIP_TRY(leaf_chunk_cvs(fid, w->comm.as<uint32_t>(), r0, n_rows_cv, enc, enc, c_lo, c_hi,
-                           w->dcv.as<uint32_t>(), s));
+                           w->dcv.as<uint32_t>(), s, true));
     const size_t cv_bytes = (c_hi - c_lo) * enc * 32;
     const size_t cv_off = w->cvs.size();
     w->cvs.resize(cv_off + cv_bytes);

@@ -6,7 +6,7 @@ namespace lcpc {
 
 #define DECL(n)                                                                                   \
   hipError_t ntt_rows_##n(const NttPlan &, const uint32_t *, size_t, size_t, uint32_t *, size_t, \
-                          size_t, hipStream_t, uint32_t *, size_t);                               \
+                          size_t, hipStream_t, uint32_t *, size_t, bool);                         \
   hipError_t ntt_tw_table_##n(uint32_t *, int, bool, hipStream_t);
 DECL(ft63)
 DECL(ft127)
@@ -33,26 +33,33 @@ hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream
   hipError_t e = hipMalloc(&p.d_tw, n * field_bytes(fid));
   if (e != hipSuccess) return e;
   switch (fid) {
-    case 0: return ntt_tw_table_ft63(p.d_tw, log_n, inverse, s);
-    case 1: return ntt_tw_table_ft127(p.d_tw, log_n, inverse, s);
-    case 3: return ntt_tw_table_ft255(p.d_tw, log_n, inverse, s);
-    default: return ntt_tw_table_ft253(p.d_tw, log_n, inverse, s);
+    case 0: e = ntt_tw_table_ft63(p.d_tw, log_n, inverse, s); break;
+    case 1: e = ntt_tw_table_ft127(p.d_tw, log_n, inverse, s); break;
+    case 3: e = ntt_tw_table_ft255(p.d_tw, log_n, inverse, s); break;
+    default: e = ntt_tw_table_ft253(p.d_tw, log_n, inverse, s); break;
   }
+  if (e != hipSuccess || inverse) return e;
+  // canonical words of w^e = Montgomery words of w^e R^-1 (canon_out encodes)
+  e = hipMalloc(&p.d_tw_canon, n * field_bytes(fid));
+  if (e != hipSuccess) return e;
+  return convert(fid, p.d_tw, p.d_tw_canon, n, false, s);
 }
 
 void ntt_plan_free(NttPlan &p) {
   if (p.d_tw) (void)hipFree(p.d_tw);
+  if (p.d_tw_canon) (void)hipFree(p.d_tw_canon);
   p.d_tw = nullptr;
+  p.d_tw_canon = nullptr;
 }
 
 hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
                     uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s, uint32_t *copy,
-                    size_t copy_stride) {
+                    size_t copy_stride, bool canon) {
   switch (p.fid) {
-    case 0: return ntt_rows_ft63(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride);
-    case 1: return ntt_rows_ft127(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride);
-    case 3: return ntt_rows_ft255(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride);
-    case 4: return ntt_rows_ft253(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride);
+    case 0: return ntt_rows_ft63(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
+    case 1: return ntt_rows_ft127(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
+    case 3: return ntt_rows_ft255(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
+    case 4: return ntt_rows_ft253(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
     default: return hipErrorInvalidValue;
   }
 }

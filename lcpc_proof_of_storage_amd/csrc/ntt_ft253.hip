@@ -3,8 +3,8 @@
 
 namespace lcpc {
 hipError_t ntt_rows_ft253(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst,
-                      size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
-  return ntt_detail::ntt_rows_t<Ft253_192>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs);
+                      size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
+  return ntt_detail::ntt_rows_t<Ft253_192>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, canon);
 }
 hipError_t ntt_tw_table_ft253(uint32_t *tw, int log_n, bool inverse, hipStream_t s) {
   const size_t n = (size_t)1 << log_n;

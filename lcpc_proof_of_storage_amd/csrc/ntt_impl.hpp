@@ -54,7 +54,7 @@ __global__ __launch_bounds__(NTHREADS) void k_ntt_small(const uint32_t *__restri
                                                         size_t dst_stride,
                                                         const uint32_t *__restrict__ twn,
                                                         int log_n, uint32_t *__restrict__ copy,
-                                                        size_t copy_stride) {
+                                                        size_t copy_stride, int canon) {
   __shared__ __align__(16) uint32_t smem[4096 * F::N];
   Fe<F> *buf = reinterpret_cast<Fe<F> *>(smem);
   const size_t row = blockIdx.x;
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(NTHREADS) void k_ntt_small(const uint32_t *__restri
   }
   __syncthreads();
   uint32_t *out = dst + row * dst_stride * F::N;
-  for (int i = threadIdx.x; i < n; i += NTHREADS) fe_store<F>(out, i, buf[i]);
+  for (int i = threadIdx.x; i < n; i += NTHREADS) fe_store<F>(out, i, canon ? fe_from_mont<F>(buf[i]) : buf[i]);
 }
 
 // Per-field tile shapes for the v2 passes (tools/microbench/nttbench.hip sweep on MI355X):
@@ -127,9 +127,16 @@ hipError_t dispatch_logs(int l, Fn &&fn) {
 }
 
 template <class F>
+__global__ void k_from_mont_rows(uint32_t *__restrict__ m, size_t stride, size_t n_rows) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < n_rows) fe_store<F>(m, r * stride, fe_from_mont<F>(fe_load<F>(m, r * stride)));
+}
+
+template <class F>
 hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst,
-                      size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
+                      size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
   if (n_rows == 0) return hipSuccess;
+  if (canon && !p.d_tw_canon) return hipErrorInvalidValue;
   if (p.log_n == 0) {  // length-1 transform is the identity (fffft returns early)
     if (cp && nv) {
       hipError_t e = hipMemcpy2DAsync(cp, cs * F::N * 4, src, ss * F::N * 4, F::N * 4, n_rows,
@@ -137,13 +144,17 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
       if (e != hipSuccess) return e;
     }
     if (!nv) return hipMemset2DAsync(dst, ds * F::N * 4, 0, F::N * 4, n_rows, s);
-    return hipMemcpy2DAsync(dst, ds * F::N * 4, src, ss * F::N * 4, F::N * 4, n_rows,
-                            hipMemcpyDeviceToDevice, s);
+    hipError_t e = hipMemcpy2DAsync(dst, ds * F::N * 4, src, ss * F::N * 4, F::N * 4, n_rows,
+                                    hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess || !canon) return e;
+    hipLaunchKernelGGL((k_from_mont_rows<F>), dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s, dst, ds,
+                       n_rows);
+    return hipGetLastError();
   }
   if (p.log_n <= 12) {
     prof::Scope ps("ntt_small", s);
     hipLaunchKernelGGL((k_ntt_small<F>), dim3(n_rows), dim3(NTHREADS), 0, s, src, ss, nv, dst, ds,
-                       p.d_tw, p.log_n, cp, cs);
+                       p.d_tw, p.log_n, cp, cs, canon ? 1 : 0);
     return hipGetLastError();
   }
   constexpr int R = Shape<F>::R, E = Shape<F>::E;
@@ -152,8 +163,13 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
   hipError_t e = dispatch_logs<F, 6, HI>(p.l1, [&]<int L>() {
     constexpr int CW = log_cw<L, E>();
     constexpr int T = L + CW - R;
+    const uint32_t *tc = p.d_tw_canon;
+    if (halfz && canon)
+      return ntt_v2::launch_a<F, L, CW, T, true, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, tc);
     if (halfz)
       return ntt_v2::launch_a<F, L, CW, T, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs);
+    if (canon)
+      return ntt_v2::launch_a<F, L, CW, T, false, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, tc);
     return ntt_v2::launch_a<F, L, CW, T, false>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs);
   });
   if (e != hipSuccess) return e;

@@ -91,12 +91,16 @@ constexpr int last_s0() {  // first stage of the last round
   return s0;
 }
 
-template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ>
+// CANON: the inter-pass multiplier is w^e R^-1 (twc: the canonical words of w^e), applied to
+// every element including e = 0, so the whole transform comes out scaled by R^-1 -- i.e. in
+// canonical form (see ntt_rows' canon_out).
+template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ, bool CANON>
 __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restrict__ src,
                                                        size_t src_stride, size_t n_valid,
                                                        uint32_t *__restrict__ dst,
                                                        size_t dst_stride,
                                                        const uint32_t *__restrict__ twn,
+                                                       const uint32_t *__restrict__ twc,
                                                        int log_n, uint32_t *__restrict__ copy,
                                                        size_t copy_stride) {
   constexpr int S = 1 << LOG_S, CW = 1 << LOG_CW, LD = CW > 1 ? CW + 1 : 1, T = 1 << LOG_T;
@@ -146,7 +150,10 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
         const int t = q + j * GL;  // GL == 1 here
         const size_t e = c * (size_t)brev(t, LOG_S);
         Fe<F> y = x[j];
-        if (e) y = fe_mul<F>(y, fe_load<F>(twn, e));
+        if (CANON)
+          y = fe_mul<F>(y, fe_load<F>(twc, e));
+        else if (e)
+          y = fe_mul<F>(y, fe_load<F>(twn, e));
         fe_store<F>(out, c + ((size_t)t << log_m), y);
       }
       return;
@@ -175,7 +182,10 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
         const int t = b + j;
         const size_t e = c * (size_t)brev(t, LOG_S);
         Fe<F> y = x[j];
-        if (e) y = fe_mul<F>(y, fe_load<F>(twn, e));
+        if (CANON)
+          y = fe_mul<F>(y, fe_load<F>(twc, e));
+        else if (e)
+          y = fe_mul<F>(y, fe_load<F>(twn, e));
         fe_store<F>(out, c + ((size_t)t << log_m), y);
       }
     }
@@ -220,14 +230,14 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_b(uint32_t *__restrict__ da
   }
 }
 
-template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ>
+template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ, bool CANON = false>
 hipError_t launch_a(const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                     const uint32_t *tw, int log_n, size_t n_rows, hipStream_t s, uint32_t *cp,
-                    size_t cs) {
+                    size_t cs, const uint32_t *twc = nullptr) {
   const size_t groups = (size_t)1 << (log_n - LOG_S - LOG_CW);
   prof::Scope ps("ntt_pass_a", s);
-  hipLaunchKernelGGL((k_pass_a<F, LOG_S, LOG_CW, LOG_T, HALFZ>), dim3((unsigned)(n_rows * groups)),
-                     dim3(1 << LOG_T), 0, s, src, ss, nv, dst, ds, tw, log_n, cp, cs);
+  hipLaunchKernelGGL((k_pass_a<F, LOG_S, LOG_CW, LOG_T, HALFZ, CANON>), dim3((unsigned)(n_rows * groups)),
+                     dim3(1 << LOG_T), 0, s, src, ss, nv, dst, ds, tw, twc, log_n, cp, cs);
   return hipGetLastError();
 }
 

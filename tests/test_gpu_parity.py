@@ -109,6 +109,14 @@ def test_commit_device_matches_oracle(gpu, oracle, hipmem, fid, n_per_row, n_col
         assert g.get_root() == o.root()
         # the caller's buffer is only read
         assert np.array_equal(hipmem.to_host(d, np.zeros_like(coeffs)), coeffs)
+        # the device codeword holds the canonical values of the reference's comm
+        from lcpc_proof_of_storage_amd import _native as N
+        assert N.load().lcpc_commit_comm_canonical(g._h) == 1
+        dev = hipmem.to_host(N.load().lcpc_commit_device_comm(g._h), np.zeros_like(o.comm))
+        nl = oracle.limbs(fid)
+        canon = np.zeros_like(o.comm)
+        oracle.lib().of_to_canonical(fid, oracle.p64(o.comm), oracle.p64(canon), o.comm.size // nl)
+        assert np.array_equal(dev, canon)
         del g
     finally:
         hipmem.free(d)

@@ -60,7 +60,7 @@ void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
 
   std::vector<Variant> vs;
   vs.push_back({"product (ntt_rows_t)", [&](const uint32_t *c, uint32_t *o, hipStream_t st) {
-                  CK(ntt_detail::ntt_rows_t<F>(plan, c, np, np, o, n, rows, st, nullptr, 0));
+                  CK(ntt_detail::ntt_rows_t<F>(plan, c, np, np, o, n, rows, st, nullptr, 0, false));
                 }});
   vs.push_back({"v1 (256thr, 3 LDS trips)", [&](const uint32_t *c, uint32_t *o, hipStream_t st) {
                   CK(ntt_v1::ntt_rows_v1<F>(plan, c, np, np, o, n, rows, st));
