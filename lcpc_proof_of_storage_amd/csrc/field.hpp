@@ -100,6 +100,23 @@ __device__ __forceinline__ Fe<F> fe_sub(const Fe<F>& a, const Fe<F>& b) {
   return r;
 }
 
+// a - b + p as an integer in [1, 2p) (no conditional correction): only as a MULTIPLICAND.
+// With p < R/2 a Montgomery product of a value < 2p and one < p is < p (1 + 2p/R) < 2p before
+// its final conditional subtraction, so fe_mul(fe_sub_lazy(a, b), w) == fe_mul(fe_sub(a, b), w)
+// bit for bit; the DIF butterfly's twiddled output saves the select of fe_sub.
+template <class F>
+__device__ __forceinline__ Fe<F> fe_sub_lazy(const Fe<F>& a, const Fe<F>& b) {
+  static_assert(F::P[F::N - 1] < 0x80000000u, "needs p < R / 2");
+  Fe<F> t;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) t.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) t.v[i] = __builtin_addc(t.v[i], F::P[i], c, &c);
+  return t;  // mod 2^(32N): a - b + p whether or not a - b borrowed
+}
+
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   return (uint64_t)a * (uint64_t)b + c;
 }

@@ -77,8 +77,8 @@ __global__ __launch_bounds__(NTHREADS) void k_ntt_small(const uint32_t *__restri
       const int base = chunk * 2 * gap;
       const Fe<F> a = buf[base + j], b = buf[base + j + gap];
       buf[base + j] = fe_add<F>(a, b);
-      const Fe<F> d = fe_sub<F>(a, b);
-      buf[base + j + gap] = j ? fe_mul<F>(d, fe_load<F>(twn, (size_t)nchunks * j)) : d;
+      buf[base + j + gap] = j ? fe_mul<F>(fe_sub_lazy<F>(a, b), fe_load<F>(twn, (size_t)nchunks * j))
+                              : fe_sub<F>(a, b);
     }
   }
   __syncthreads();

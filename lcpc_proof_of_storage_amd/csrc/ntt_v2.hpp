@@ -46,8 +46,7 @@ __device__ __forceinline__ void dif_regs(Fe<F> *x, int b_lo, const Fe<F> *tw) {
       } else {
         const Fe<F> a = x[j], c = x[j + h];
         x[j] = fe_add<F>(a, c);
-        const Fe<F> d = fe_sub<F>(a, c);
-        x[j + h] = triv ? d : fe_mul<F>(d, tw[(b_lo + jm * GL) << s]);
+        x[j + h] = triv ? fe_sub<F>(a, c) : fe_mul<F>(fe_sub_lazy<F>(a, c), tw[(b_lo + jm * GL) << s]);
       }
     }
   }
