@@ -11,9 +11,17 @@
 // all tensors accumulated from ONE read of each coefficient; the tensor entries of a row are
 // wave-uniform (scalar loads).  Rows are split over blockIdx.y so the grid fills 256 CUs; the
 // per-split partials are folded by a second kernel.
+//
+// Ft127 with up to 3 tensors (every prove launch of the Ligero / Brakedown commitments over
+// Ft127) runs the contraction on the int8 matrix cores instead (collapse_mfma.hpp): there the
+// kernel streams the coefficient matrix at the HBM rate instead of being bound by 64-bit
+// multiply-adds.
+#include "collapse_mfma.hpp"
 #include "field.hpp"
 #include "kernels.hpp"
 #include "prof.hpp"
+
+#include <cstdlib>
 
 namespace lcpc {
 
@@ -153,6 +161,51 @@ hipError_t collapse_t(const uint32_t *coeffs, size_t n_rows, size_t n_per_row,
   return hipGetLastError();
 }
 
+// MFMA path (Ft127, T <= 3): row splits of at most MAX_SPLIT_ROWS rows, about 512 blocks
+size_t mfma_splits_for(size_t n_rows, size_t n_per_row) {
+  const size_t blocks_x = (n_per_row + 4 * cmfma::COLS_PER_WAVE - 1) / (4 * cmfma::COLS_PER_WAVE);
+  size_t splits = (512 + blocks_x - 1) / blocks_x;
+  const size_t max_splits = (n_rows + 15) / 16;
+  if (splits > max_splits) splits = max_splits;
+  const size_t min_splits = (n_rows + cmfma::MAX_SPLIT_ROWS - 1) / cmfma::MAX_SPLIT_ROWS;
+  if (splits < min_splits) splits = min_splits;
+  return splits < 1 ? 1 : splits;
+}
+
+// LCPC_COLLAPSE_VALU=1 selects the VALU kernels for every field (A/B measurements)
+bool use_mfma(int fid, int n_tensors) {
+  static const bool valu_only = [] {
+    const char *e = getenv("LCPC_COLLAPSE_VALU");
+    return e && *e && *e != '0';
+  }();
+  return !valu_only && fid == Ft127::ID && n_tensors >= 1 && n_tensors <= 3;
+}
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+template <int T>
+hipError_t collapse_mfma_t(const uint32_t *coeffs, size_t n_rows, size_t n_per_row, const uint32_t *tensors,
+                           uint32_t *out, void *scratch, hipStream_t s) {
+  using F = Ft127;
+  const size_t splits = mfma_splits_for(n_rows, n_per_row);
+  const size_t rps = (n_rows + splits - 1) / splits;
+  uint32_t *partial = (uint32_t *)scratch;
+  uint8_t *hdig = (uint8_t *)scratch + round_up(splits * T * n_per_row * 16, 256);
+  const size_t nd = (size_t)T * n_rows * 16;
+  prof::Scope ps("collapse_partial", s);
+  hipLaunchKernelGGL((cmfma::k_tensor_digits<F>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, tensors,
+                     n_rows, T, hdig);
+  dim3 grid((unsigned)((n_per_row + 4 * cmfma::COLS_PER_WAVE - 1) / (4 * cmfma::COLS_PER_WAVE)), (unsigned)splits);
+  hipLaunchKernelGGL((cmfma::k_collapse_mfma<F, T>), grid, dim3(256), 0, s, coeffs, n_rows, n_per_row,
+                     (const uint8_t *)hdig, partial, rps);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  prof::Scope ps2("collapse_fold", s);
+  hipLaunchKernelGGL((k_collapse_fold<F, T>), dim3((unsigned)((n_per_row + 255) / 256)), dim3(256), 0, s,
+                     (const uint32_t *)partial, splits, n_per_row, out);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t collapse_fold_rows(int fid, const uint32_t *vecs, size_t n_vecs, size_t len, uint32_t *out,
@@ -165,7 +218,11 @@ hipError_t collapse_fold_rows(int fid, const uint32_t *vecs, size_t n_vecs, size
 }
 
 size_t collapse_scratch_bytes(int fid, size_t n_rows, size_t n_per_row, int n_tensors) {
-  return n_splits_for(n_rows, n_per_row) * (size_t)n_tensors * n_per_row * field_bytes(fid);
+  const size_t valu = n_splits_for(n_rows, n_per_row) * (size_t)n_tensors * n_per_row * field_bytes(fid);
+  if (!use_mfma(fid, n_tensors)) return valu;
+  const size_t mfma = round_up(mfma_splits_for(n_rows, n_per_row) * n_tensors * n_per_row * 16, 256) +
+                      (size_t)n_tensors * n_rows * 256;
+  return mfma > valu ? mfma : valu;
 }
 
 hipError_t collapse_rows(int fid, const uint32_t *coeffs, size_t n_rows, size_t n_per_row,
@@ -173,6 +230,14 @@ hipError_t collapse_rows(int fid, const uint32_t *coeffs, size_t n_rows, size_t 
                          hipStream_t s) {
   if (n_tensors < 1 || n_tensors > MAXT) return hipErrorInvalidValue;
   if (n_per_row == 0) return hipSuccess;
+  if (n_rows == 0) return hipMemsetAsync(out, 0, (size_t)n_tensors * n_per_row * field_bytes(fid), s);
+  if (use_mfma(fid, n_tensors)) {
+    switch (n_tensors) {
+      case 1: return collapse_mfma_t<1>(coeffs, n_rows, n_per_row, tensors, out, scratch, s);
+      case 2: return collapse_mfma_t<2>(coeffs, n_rows, n_per_row, tensors, out, scratch, s);
+      default: return collapse_mfma_t<3>(coeffs, n_rows, n_per_row, tensors, out, scratch, s);
+    }
+  }
   return dispatch_field(fid, [&]<class F>() {
     switch (n_tensors) {
       case 1: return collapse_t<F, 1>(coeffs, n_rows, n_per_row, tensors, out, scratch, s);
