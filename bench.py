@@ -199,12 +199,19 @@ def shard_workload(args, L, torch, rank, local_rank, dist):
     rows = rows.reshape(n_rows, n_per_row * nl)
     outer = L.field_random(fid, n_rows, 7)
     be = GpuBackend(enc)
-    comm = Comm(dist, f"cuda:{local_rank}" if dist is not None else "cpu")
+    # device-resident exchanges (RCCL at N > 1); every pipeline slot has a process group of its
+    # own, so the collectives of commitments in flight never interleave within one communicator
+    dev = f"cuda:{local_rank}"
+    groups = [dist.new_group(list(range(dist.get_world_size()))) for _ in range(max(1, args.pipeline))] \
+        if dist is not None else [None] * max(1, args.pipeline)
+    comms = [Comm(dist, dev, group=g) for g in groups]
+    comm = comms[0]
     sc0 = RowShardedCommit(be, comm, n_rows, 8 * nl)
     mine = np.ascontiguousarray(rows[sc0.r_lo:sc0.r_hi])  # this rank's rows stay resident in HBM
     d_mine = torch.from_numpy(mine.view(np.int64)).to(f"cuda:{local_rank}")
 
     def step(slot):
+        comm = comms[slot]
         sc = RowShardedCommit(be, comm, n_rows, 8 * nl)
         root = sc.commit((d_mine.data_ptr(), sc.r_hi - sc.r_lo))
         tr = None
@@ -311,7 +318,6 @@ def main():
 
     L.set_device(local_rank)
     if args.shard == "rows":
-        args.pipeline = 1  # the ranks' collectives must be issued in one order
         wl = shard_workload(args, L, torch, rank, local_rank, dist)
     else:
         wl = (pos_workload if args.code == "pos" else ligero_or_sdig)(args, L, torch, rank, local_rank)
@@ -339,11 +345,19 @@ def main():
             errors.append(e)
         ready.wait()
         start.wait()
+        # row shards: a static schedule (slot i runs steps i, i + P, ...), so that every rank
+        # issues the same collectives on each slot's process group
+        mine = len(range(slot, args.steps, n_workers)) if args.shard == "rows" else None
         while not errors:
             with lock:
-                if todo[0] <= 0:
+                if mine is not None:
+                    if mine <= 0:
+                        return
+                    mine -= 1
+                elif todo[0] <= 0:
                     return
-                todo[0] -= 1
+                else:
+                    todo[0] -= 1
             try:
                 roots.append(wl.step(slot))
             except Exception as e:

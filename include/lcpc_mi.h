@@ -377,6 +377,20 @@ lcpc_status lcpc_shard_gather_columns(const lcpc_shard *s, const uint64_t *idx, 
 /* out[i] = sum_k vecs[k][i] mod p */
 lcpc_status lcpc_field_sum(lcpc_field f, const uint64_t *vecs, size_t n_vecs, size_t len,
                            uint64_t *out);
+/* Device-resident variants for exchanges over RCCL (shard.py with the "nccl" backend): the
+ * exchanged buffers are device pointers (torch tensors); host memory only for idx and the
+ * folded row combination the transcript absorbs.  Same semantics as the host forms above. */
+lcpc_status lcpc_shard_chunk_cvs_device(const lcpc_shard *s, size_t chunk_lo, size_t chunk_hi,
+                                        void *d_out);
+/* leaf digests of n_cols (a power of two) columns from d_cvs [chunk][col][32] (clobbered) and
+ * their Merkle tree: d_hashes = leaves || level 1 || ... || root (2 n_cols - 1 digests) */
+lcpc_status lcpc_leaves_tree_device(void *d_cvs, size_t n_chunks, size_t n_cols, void *d_hashes);
+lcpc_status lcpc_shard_collapse_device(const lcpc_shard *s, const void *d_tensors,
+                                       size_t n_tensors, void *d_out);
+lcpc_status lcpc_shard_gather_columns_device(const lcpc_shard *s, const uint64_t *idx, size_t n,
+                                             void *d_out);
+lcpc_status lcpc_field_sum_device(lcpc_field f, const void *d_vecs, size_t n_vecs, size_t len,
+                                  uint64_t *out);
 /* the Fiat-Shamir steps of prove: degree-test tensor ("$l//DT" -> ChaCha20 -> Field::random,
  * lib.rs:1056-1062), absorbing field elements as their repr (lib.rs:1075-1077, 1096-1098) and
  * the column choice ("$l//CO" -> ChaCha20 -> Uniform(0, n_cols), lib.rs:1101-1110) */

@@ -134,6 +134,11 @@ SIGNATURES = {
     "lcpc_shard_collapse": (i32, [vp, u64p, sz, u64p]),
     "lcpc_shard_gather_columns": (i32, [vp, u64p, sz, u64p]),
     "lcpc_field_sum": (i32, [i32, u64p, sz, sz, u64p]),
+    "lcpc_shard_chunk_cvs_device": (i32, [vp, sz, sz, vp]),
+    "lcpc_leaves_tree_device": (i32, [vp, sz, sz, vp]),
+    "lcpc_shard_collapse_device": (i32, [vp, vp, sz, vp]),
+    "lcpc_shard_gather_columns_device": (i32, [vp, u64p, sz, vp]),
+    "lcpc_field_sum_device": (i32, [i32, vp, sz, sz, u64p]),
     "lcpc_challenge_tensor": (i32, [vp, i32, sz, u64p]),
     "lcpc_transcript_append_field_elems": (i32, [vp, u8p, sz, i32, u64p, sz]),
     "lcpc_challenge_columns": (i32, [vp, sz, sz, u64p]),
@@ -157,6 +162,14 @@ def load(path: str = LIB_PATH):
     if _lib is None:
         if not os.path.exists(path):
             raise OSError(f"{path} not built: run `make -C {PKG_DIR}` (or __graft_entry__.build())")
+        # torch-ROCm bundles its own libamdhip64.so (soname libamdhip64.so.7, as ours).  Loaded
+        # first, it satisfies this library's dependency, so torch tensors and RCCL (shard.py)
+        # share one HIP runtime with the kernels here; loaded after us, torch would bring a
+        # second runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = C.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

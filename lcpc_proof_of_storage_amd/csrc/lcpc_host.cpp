@@ -1911,6 +1911,107 @@ lcpc_status lcpc_field_sum(lcpc_field f, const uint64_t *vecs, size_t n_vecs, si
   return LCPC_OK;
 }
 
+// ---- device-resident exchanges: the same steps with the exchanged buffers in device memory
+// (torch tensors that RCCL moves over xGMI), so nothing crosses PCIe but the transcript inputs.
+// Each call runs on a leased library stream and returns once its results are in memory.
+lcpc_status lcpc_shard_chunk_cvs_device(const lcpc_shard *s, size_t chunk_lo, size_t chunk_hi, void *d_out) {
+  if (!s || (!d_out && chunk_hi > chunk_lo)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  const int fid = s->e->fid;
+  const size_t nc = s->e->n_cols;
+  if (chunk_hi > leaf_n_chunks(fid, s->n_rows_total) || chunk_lo > chunk_hi)
+    return fail(LCPC_ERR_INVALID_ARG, "chunk range");
+  const size_t need_lo = lcpc_leaf_chunk_first_row((lcpc_field)fid, chunk_lo);
+  const size_t need_hi = chunk_hi >= leaf_n_chunks(fid, s->n_rows_total)
+                             ? s->n_rows_total
+                             : lcpc_leaf_chunk_first_row((lcpc_field)fid, chunk_hi);
+  if (chunk_hi > chunk_lo && (need_lo < s->row0 || need_hi > s->row0 + s->n_rows))
+    return fail(LCPC_ERR_INVALID_ARG, "the shard does not hold every row of those chunks");
+  if (chunk_hi == chunk_lo) return LCPC_OK;
+  Device *dev = s->e->dev;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  HIP_TRY(leaf_chunk_cvs(fid, s->comm.as<uint32_t>(), s->row0, s->n_rows_total, nc, nc, chunk_lo, chunk_hi,
+                         (uint32_t *)d_out, lease.s, true));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_leaves_tree_device(void *d_cvs, size_t n_chunks, size_t n_cols, void *d_hashes) {
+  // d_cvs [chunk][col][32] (consumed as scratch) -> d_hashes = leaves || merkle levels || root
+  if ((!d_cvs || !d_hashes) && n_cols) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (n_chunks == 0 || n_cols == 0 || (n_cols & (n_cols - 1)))
+    return fail(LCPC_ERR_INVALID_ARG, "n_chunks >= 1, n_cols a power of two");
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  HIP_TRY(leaves_from_cvs((uint32_t *)d_cvs, n_cols, (int)n_chunks, (uint8_t *)d_hashes, lease.s));
+  if (n_cols > 1) HIP_TRY(merkle_tree((uint8_t *)d_hashes, n_cols, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_shard_collapse_device(const lcpc_shard *s, const void *d_tensors, size_t n_tensors, void *d_out) {
+  if (!s || !d_out || (!d_tensors && s->n_rows)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (n_tensors < 1 || n_tensors > 4) return fail(LCPC_ERR_INVALID_ARG, "1..4 tensors");
+  const int fid = s->e->fid, wb = field_bytes(fid);
+  const size_t np = s->e->n_per_row;
+  Device *dev = s->e->dev;
+  Lease lease(dev, true);
+  HIP_TRY(hipSetDevice(dev->id));
+  if (s->n_rows == 0) {
+    HIP_TRY(hipMemsetAsync(d_out, 0, n_tensors * np * wb, lease.s));
+  } else {
+    DBuf scratch;
+    HIP_TRY(scratch.alloc(dev, collapse_scratch_bytes(fid, s->n_rows, np, (int)n_tensors)));
+    HIP_TRY(collapse_rows(fid, s->coeffs.as<uint32_t>(), s->n_rows, np, (const uint32_t *)d_tensors,
+                          (int)n_tensors, (uint32_t *)d_out, scratch.p, lease.s));
+  }
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_shard_gather_columns_device(const lcpc_shard *s, const uint64_t *idx, size_t n, void *d_out) {
+  if (!s || (!idx && n) || (!d_out && n)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  const size_t nc = s->e->n_cols;
+  for (size_t k = 0; k < n; k++)
+    if (idx[k] >= nc) return fail(LCPC_PROVER_COLUMN_NUMBER, "ProverError::ColumnNumber");
+  if (!n || !s->n_rows) return LCPC_OK;
+  const int fid = s->e->fid;
+  Device *dev = s->e->dev;
+  Lease lease(dev, true);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf didx;
+  lcpc_status st;
+  if ((st = upload(dev, didx, idx, n * 8))) return st;
+  HIP_TRY(gather_columns(fid, s->comm.as<uint32_t>(), s->n_rows, nc, didx.as<uint64_t>(), n, (uint32_t *)d_out,
+                         lease.s, false, true));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_field_sum_device(lcpc_field f, const void *d_vecs, size_t n_vecs, size_t len, uint64_t *out) {
+  if (!valid_field(f) || (!d_vecs && n_vecs * len) || (!out && len)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  if (!len) return LCPC_OK;
+  const int wb = field_bytes(f);
+  if (n_vecs == 0) {
+    std::memset(out, 0, len * wb);
+    return LCPC_OK;
+  }
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  DBuf dout;
+  HIP_TRY(dout.alloc(dev, len * wb));
+  HIP_TRY(collapse_fold_rows(f, (const uint32_t *)d_vecs, n_vecs, len, dout.as<uint32_t>(), lease.s));
+  HIP_TRY(hipMemcpyAsync(out, dout.p, len * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
 lcpc_status lcpc_challenge_tensor(lcpc_transcript *tr, lcpc_field f, size_t n, uint64_t *out) {
   // prove / verify degree-test tensor (lcpc-2d/src/lib.rs:1056-1062, 899-907)
   if (!tr || !valid_field(f) || (!out && n)) return fail(LCPC_ERR_INVALID_ARG, "arguments");

@@ -505,6 +505,27 @@ class LcEvalProof:
                                               path_len, _p64(pe), _p64(pr), _p64(cols), pp, C.byref(h)))
         return cls(h.value)
 
+    @classmethod
+    def from_arrays(cls, field: int, n_cols: int, p_eval, p_random_vec, cols, paths):
+        """from_parts with the columns as one (n_col_opens, n_rows, limbs) array and the paths
+        as one (n_col_opens, path_len, 32) byte array."""
+        nl = limbs(field)
+        pe = _elems(p_eval, field)
+        pr = np.ascontiguousarray(np.concatenate([_elems(x, field) for x in p_random_vec]) if p_random_vec
+                                  else np.zeros((1, nl), np.uint64))
+        cols = np.ascontiguousarray(cols, dtype=np.uint64)
+        paths = np.ascontiguousarray(paths, dtype=np.uint8)
+        nco, n_rows = cols.shape[0], (cols.shape[1] if cols.ndim > 1 else 0)
+        path_len = paths.shape[1] if paths.ndim > 1 else 0
+        if nco == 0:
+            cols = np.zeros((1, nl), np.uint64)
+            paths = np.zeros(1, np.uint8)
+        h = C.c_void_p()
+        _raise(N.load().lcpc_proof_from_parts(field, n_cols, pe.shape[0], n_rows, len(p_random_vec), nco, path_len,
+                                              _p64(pe), _p64(pr), _p64(cols), paths.ctypes.data_as(N.u8p),
+                                              C.byref(h)))
+        return cls(h.value)
+
     def verify(self, root: bytes, outer_tensor, inner_tensor, enc: LcEncoding, tr: Transcript) -> np.ndarray:
         o = _elems(outer_tensor, self.field)
         i = _elems(inner_tensor, self.field)

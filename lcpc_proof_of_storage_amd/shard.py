@@ -18,6 +18,12 @@ hashes what it can of the column leaves; the exchanges are small and go over RCC
     them mod p and absorbs the result, and so on; the opened columns are assembled from every
     rank's rows and the Merkle paths from the owners' subtrees and the shared top tree.
 
+With the GPU backend and a device communicator (Comm(dist, "cuda:k"), backend "nccl") the
+exchanged buffers never leave HBM: the chaining values, partial row combinations and opened
+column pieces are torch tensors the library writes through device pointers
+(lcpc_*_device), and RCCL moves them over xGMI; only the folded row combinations (which the
+transcript absorbs on rank 0) and the 2B - 1 digests of each rank's subtree reach the host.
+
 The proof is bit-identical to the single-GPU LcCommit.prove (tests/test_shard.py runs the
 protocol over gloo at world_size 2 against a single-process commit).
 """
@@ -62,11 +68,12 @@ class Comm:
     """torch.distributed on numpy buffers: gloo keeps them on the CPU, nccl (RCCL) stages them
     through the rank's GPU."""
 
-    def __init__(self, dist=None, device: str = "cpu"):
+    def __init__(self, dist=None, device: str = "cpu", group=None):
         self.dist = dist
         self.device = device
-        self.rank = dist.get_rank() if dist else 0
-        self.world = dist.get_world_size() if dist else 1
+        self.group = group  # a process group of its own lets several commitments run concurrently
+        self.rank = dist.get_rank(group) if dist else 0
+        self.world = dist.get_world_size(group) if dist else 1
 
     def _t(self, a: np.ndarray):
         import torch
@@ -78,7 +85,7 @@ class Comm:
         import torch
         nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
         t = self._t(a) if self.rank == src else torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
-        self.dist.broadcast(t, src)
+        self.dist.broadcast(t, src, group=self.group)
         return t.cpu().numpy().view(dtype).reshape(shape)
 
     def all_gather(self, a: np.ndarray) -> List[np.ndarray]:
@@ -87,7 +94,7 @@ class Comm:
             return [a]
         t = self._t(a)
         outs = [t.clone() for _ in range(self.world)]
-        self.dist.all_gather(outs, t)
+        self.dist.all_gather(outs, t, group=self.group)
         return [o.cpu().numpy().view(a.dtype).reshape(a.shape) for o in outs]
 
     def all_gather_v(self, a: np.ndarray) -> List[np.ndarray]:
@@ -100,6 +107,41 @@ class Comm:
         pad[:a.shape[0]] = a
         got = self.all_gather(pad)
         return [g[:int(n[0])] for g, n in zip(got, lens)]
+
+    # -- device tensors (torch, on self.device): RCCL moves them in place; gloo stages via host
+    @property
+    def on_device(self) -> bool:
+        return self.device != "cpu"
+
+    def _nccl(self) -> bool:
+        return self.dist is not None and self.dist.get_backend(self.group) == "nccl"
+
+    def t_all_to_all(self, send, in_splits: Sequence[int], out_splits: Sequence[int]):
+        """1-D byte tensors: send[sum(in_splits[:k]) ...] goes to rank k; returns the pieces
+        received, concatenated in rank order."""
+        if self.world == 1:
+            return send
+        import torch
+        if self._nccl():
+            out = torch.empty(int(sum(out_splits)), dtype=send.dtype, device=send.device)
+            self.dist.all_to_all_single(out, send, list(map(int, out_splits)), list(map(int, in_splits)),
+                                        group=self.group)
+            return out
+        h = send.cpu().numpy()
+        offs = np.cumsum([0] + list(in_splits))
+        got = self.all_to_all([h[offs[k]:offs[k + 1]] for k in range(self.world)])
+        return torch.from_numpy(np.concatenate(got)).to(send.device)
+
+    def t_all_gather(self, t):
+        """Same-shaped device tensors from every rank, in rank order."""
+        if self.world == 1:
+            return [t]
+        import torch
+        if self._nccl():
+            outs = [torch.empty_like(t) for _ in range(self.world)]
+            self.dist.all_gather(outs, t.contiguous(), group=self.group)
+            return outs
+        return [torch.from_numpy(a.copy()).to(t.device) for a in self.all_gather(t.cpu().numpy())]
 
     def all_to_all(self, parts: Sequence[np.ndarray]) -> List[np.ndarray]:
         """parts[k] goes to rank k; returns what every rank sent here, in rank order.  Parts
@@ -194,6 +236,53 @@ class GpuBackend:
             self._raise(self.L.lcpc_shard_gather_columns(sh[0], self._p64(idx), len(idx), self._p64(out)))
         return out
 
+    # -- device-resident forms (torch tensors in, the library writes through data_ptr())
+    def chunk_cvs_dev(self, sh, c_lo, c_hi, device):
+        import torch
+        out = torch.empty((max(c_hi - c_lo, 0), self.n_cols, 32), dtype=torch.uint8, device=device)
+        if c_hi > c_lo:
+            _sync(out)
+            self._raise(self.L.lcpc_shard_chunk_cvs_device(sh[0], c_lo, c_hi, C.c_void_p(out.data_ptr())))
+        return out
+
+    def leaves_tree_dev(self, cvs, n_chunks, n_cols):
+        """cvs: [n_chunks][n_cols][32] device bytes (clobbered) -> leaves || levels || root."""
+        import torch
+        _sync(cvs)
+        out = torch.empty((2 * n_cols - 1, 32), dtype=torch.uint8, device=cvs.device)
+        _sync(out)
+        self._raise(self.L.lcpc_leaves_tree_device(C.c_void_p(cvs.data_ptr()), n_chunks, n_cols,
+                                                   C.c_void_p(out.data_ptr())))
+        return out
+
+    def collapse_dev(self, sh, tensors):
+        import torch
+        _sync(tensors)
+        nt = tensors.shape[0]
+        out = torch.empty((nt, self.n_per_row, self.limbs), dtype=torch.int64, device=tensors.device)
+        self._raise(self.L.lcpc_shard_collapse_device(sh[0], C.c_void_p(tensors.data_ptr()), nt,
+                                                      C.c_void_p(out.data_ptr())))
+        return out
+
+    def gather_columns_dev(self, sh, idx: np.ndarray, device):
+        import torch
+        idx = np.ascontiguousarray(idx, dtype=np.uint64)
+        out = torch.zeros((len(idx), sh[1], self.limbs), dtype=torch.int64, device=device)
+        if sh[1] and len(idx):
+            _sync(out)
+            self._raise(self.L.lcpc_shard_gather_columns_device(sh[0], self._p64(idx), len(idx),
+                                                                C.c_void_p(out.data_ptr())))
+        return out
+
+    def field_sum_dev(self, vecs) -> np.ndarray:
+        """vecs: [n_vecs][len][limbs] device tensor -> host sum mod p."""
+        v = vecs.contiguous()
+        _sync(v)
+        out = np.zeros(v.shape[1:], np.uint64)
+        self._raise(self.L.lcpc_field_sum_device(self.field, C.c_void_p(v.data_ptr()), v.shape[0], v.shape[1],
+                                                 self._p64(out)))
+        return out
+
     def field_sum(self, vecs: np.ndarray) -> np.ndarray:
         v = np.ascontiguousarray(vecs, dtype=np.uint64)
         out = np.zeros(v.shape[1:], np.uint64)
@@ -217,10 +306,14 @@ class GpuBackend:
         return out
 
     def proof_from_parts(self, p_eval, p_random, cols, paths):
-        from .lcpc2d import LcColumn, LcEvalProof
-        columns = [LcColumn(cols[k], [bytes(paths[k, i]) for i in range(paths.shape[1])])
-                   for k in range(cols.shape[0])]
-        return LcEvalProof.from_parts(self.field, self.n_cols, p_eval, list(p_random), columns)
+        from .lcpc2d import LcEvalProof
+        return LcEvalProof.from_arrays(self.field, self.n_cols, p_eval, list(p_random), cols, paths)
+
+
+def _sync(t):
+    """The library's streams are not torch's: let torch's work on t finish before it is read."""
+    import torch
+    torch.cuda.current_stream(t.device).synchronize()
 
 
 LABEL_PR = b"$l//PR"
@@ -250,6 +343,8 @@ class RowShardedCommit:
         array, or (device pointer, n_rows) with the GPU backend)."""
         b, comm, G = self.b, self.comm, self.comm.world
         self.sh = b.shard_new(coeff_rows, self.r_lo, self.n_rows)
+        if self.device_mode:
+            return self._commit_dev()
         cvs = b.chunk_cvs(self.sh, self.c_lo, self.c_hi)                 # (my chunks, n_cols, 32)
         B = self.block
         recv = comm.all_to_all([cvs[:, k * B:(k + 1) * B] for k in range(G)])
@@ -262,30 +357,56 @@ class RowShardedCommit:
         self.root = bytes(self.top[-1] if G > 1 else self.roots[0])
         return self.root
 
-    def _lower_path(self, j: int) -> np.ndarray:
-        """Sibling digests of column j below the subtree root (j in my block)."""
-        B = self.block
-        lvls = B.bit_length() - 1
-        out = np.zeros((lvls, 32), np.uint8)
-        jl = j - self.comm.rank * B
-        for lvl in range(lvls):
-            sib = (jl >> lvl) ^ 1
-            out[lvl] = self.leaves[sib] if lvl == 0 else self.sub[_level_offset(B, lvl) + sib]
-        return out
+    @property
+    def device_mode(self) -> bool:
+        return self.comm.on_device and hasattr(self.b, "chunk_cvs_dev")
 
-    def _upper_path(self, j: int) -> np.ndarray:
-        G, B = self.comm.world, self.block
-        lvls = G.bit_length() - 1
-        out = np.zeros((lvls, 32), np.uint8)
-        jb = j // B
-        for lvl in range(lvls):
-            sib = (jb >> lvl) ^ 1
-            out[lvl] = self.roots[sib] if lvl == 0 else self.top[_level_offset(G, lvl) + sib]
-        return out
+    def _commit_dev(self) -> bytes:
+        """commit with the chaining values exchanged as device tensors (RCCL all-to-all)."""
+        b, comm, G, B = self.b, self.comm, self.comm.world, self.block
+        nch = self.c_hi - self.c_lo
+        cvs = b.chunk_cvs_dev(self.sh, self.c_lo, self.c_hi, comm.device)        # [nch][n_cols][32]
+        # column block k of every chunk goes to rank k: [k][chunk][B][32], contiguous per k
+        send = cvs.view(nch, G, B, 32).transpose(0, 1).contiguous().view(-1)
+        out_splits = [(p[1] - p[0]) * B * 32 for p in self.part]
+        recv = comm.t_all_to_all(send, [nch * B * 32] * G, out_splits)           # [all chunks][B][32]
+        tree = b.leaves_tree_dev(recv.view(self.n_chunks, B, 32), self.n_chunks, B)
+        tree = tree.cpu().numpy()                                               # 2B - 1 digests
+        self.leaves, self.sub = tree[:B], tree[B:]
+        sub_root = tree[-1]
+        self.roots = np.stack(comm.all_gather(sub_root))                         # (G, 32)
+        self.top = b.merkle(self.roots)
+        self.root = bytes(self.top[-1] if G > 1 else self.roots[0])
+        return self.root
+
+    @staticmethod
+    def _tree_paths(tree: np.ndarray, width: int, idx: np.ndarray) -> np.ndarray:
+        """Sibling digests of positions idx in a Merkle tree stored as leaves || level 1 || ...
+        (width leaves): level l of the tree starts at 2 width - 2 (width >> l)."""
+        lvls = width.bit_length() - 1
+        idx = np.asarray(idx, dtype=np.int64).reshape(-1)
+        if lvls == 0 or idx.size == 0:
+            return np.zeros((idx.size, lvls, 32), np.uint8)
+        lv = np.arange(lvls)
+        base = 2 * width - 2 * (width >> lv)
+        sib = (idx[:, None] >> lv[None, :]) ^ 1
+        return tree[base[None, :] + sib]
+
+    def _lower_paths(self, js: np.ndarray) -> np.ndarray:
+        """Sibling digests of columns js (in my block) below the subtree root."""
+        tree = np.concatenate([self.leaves, self.sub]) if len(self.sub) else self.leaves
+        return self._tree_paths(tree, self.block, np.asarray(js, dtype=np.int64) - self.comm.rank * self.block)
+
+    def _upper_paths(self, js: np.ndarray) -> np.ndarray:
+        G = self.comm.world
+        tree = np.concatenate([self.roots, self.top]) if G > 1 else self.roots
+        return self._tree_paths(tree, G, np.asarray(js, dtype=np.int64) // self.block)
 
     # -- prove
     def prove(self, outer: np.ndarray, tr=None):
         """Every rank calls this; rank 0 passes the transcript and gets the LcEvalProof."""
+        if self.device_mode:
+            return self._prove_dev(outer, tr)
         b, comm = self.b, self.comm
         rank0 = comm.rank == 0
         nl = b.limbs
@@ -318,17 +439,69 @@ class RowShardedCommit:
         idx = comm.bcast(idx, (nco,), np.uint64)
         cols = comm.all_gather_v(b.gather_columns(self.sh, idx).transpose(1, 0, 2).copy())
         lower = np.zeros((nco, self.block.bit_length() - 1, 32), np.uint8)
-        for k, j in enumerate(idx):
-            if int(j) // self.block == comm.rank:
-                lower[k] = self._lower_path(int(j))
+        own = (idx.astype(np.int64) // self.block) == comm.rank
+        lower[own] = self._lower_paths(idx[own])
         lowers = comm.all_gather(lower)
         if not rank0:
             return None
         cols = np.concatenate(cols, axis=0).transpose(1, 0, 2)          # (nco, n_rows, limbs)
-        paths = np.zeros((nco, b.path_len, 32), np.uint8)
-        for k, j in enumerate(idx):
-            owner = int(j) // self.block
-            paths[k] = np.concatenate([lowers[owner][k], self._upper_path(int(j))], axis=0)
+        owner = idx.astype(np.int64) // self.block
+        low = np.stack(lowers)[owner, np.arange(nco)]                         # (nco, lower levels, 32)
+        paths = np.concatenate([low, self._upper_paths(idx)], axis=1)
+        return b.proof_from_parts(p_eval, p_random, np.ascontiguousarray(cols), paths)
+
+    def _prove_dev(self, outer: np.ndarray, tr=None):
+        """prove with the partial row combinations and opened column pieces as device tensors
+        (RCCL all-gathers); rank 0 folds the partials on its GPU and runs the transcript."""
+        import torch
+        b, comm = self.b, self.comm
+        dev = comm.device
+        rank0 = comm.rank == 0
+        nl = b.limbs
+        n_rows, lo, hi = self.n_rows, self.r_lo, self.r_hi
+        outer = np.ascontiguousarray(outer, dtype=np.uint64).reshape(n_rows, nl)
+        ndt = b.n_degree_tests
+        p_random = []
+        p_eval = None
+        for i in range(max(ndt, 1)):
+            tens = []
+            if i < ndt:
+                t = b.challenge_tensor(tr, n_rows) if rank0 else None
+                t = comm.bcast(t, (n_rows, nl), np.uint64)   # the challenge vector
+                tens.append(t[lo:hi])
+            if i == 0:
+                tens.append(outer[lo:hi])                     # the evaluation tensor rides along
+            dt = torch.from_numpy(np.ascontiguousarray(np.stack(tens)).view(np.int64)).to(dev)
+            parts = b.collapse_dev(self.sh, dt)                # (len(tens), n_per_row, limbs)
+            allp = torch.stack(comm.t_all_gather(parts))     # (G, len(tens), n_per_row, limbs)
+            if rank0:
+                sums = [b.field_sum_dev(allp[:, k]) for k in range(len(tens))]
+                if i < ndt:
+                    p_random.append(sums[0])
+                    b.append_field_elems(tr, LABEL_PR, sums[0])
+                if i == 0:
+                    p_eval = sums[-1]
+        if rank0:
+            b.append_field_elems(tr, LABEL_PE, p_eval)
+        nco = b.n_col_opens
+        idx = b.challenge_columns(tr, nco) if rank0 else None
+        idx = comm.bcast(idx, (nco,), np.uint64)
+        rows = [p[3] - p[2] for p in self.part]
+        mine = b.gather_columns_dev(self.sh, idx, dev)        # (nco, my rows, limbs)
+        pad = torch.zeros((nco, max(rows), nl), dtype=torch.int64, device=dev)
+        pad[:, :mine.shape[1]] = mine
+        got = comm.t_all_gather(pad)
+        lower = np.zeros((nco, self.block.bit_length() - 1, 32), np.uint8)
+        own = (idx.astype(np.int64) // self.block) == comm.rank
+        lower[own] = self._lower_paths(idx[own])
+        lowers = comm.all_gather(lower)
+        if not rank0:
+            return None
+        cols = torch.cat([g[:, :r] for g, r in zip(got, rows)], dim=1)        # (nco, n_rows, limbs)
+        cols = cols.cpu().numpy().view(np.uint64)
+        owner = idx.astype(np.int64) // self.block
+        low = np.stack(lowers)[owner, np.arange(nco)]                         # (nco, lower levels, 32)
+        paths = np.concatenate([low, self._upper_paths(idx)], axis=1)
         return b.proof_from_parts(p_eval, p_random, np.ascontiguousarray(cols), paths)
 
     def close(self):

@@ -49,14 +49,16 @@ def _run_sharded(L, dist, device, fid, n):
                 paths=all(a.path == b.path for a, b in zip(scols, cols)))
 
 
+@pytest.mark.parametrize("device", ["cpu", "cuda:0"])
 @pytest.mark.parametrize("case", sorted(CASES))
-def test_sharded_world1(gpu, case):
+def test_sharded_world1(gpu, case, device):
+    """device "cuda:0": the device-resident exchange path (lcpc_*_device, torch tensors)"""
     fid, n = CASES[case]
-    res = _run_sharded(gpu, None, "cpu", fid, n)
+    res = _run_sharded(gpu, None, device, fid, n)
     assert all(res.values()), res
 
 
-def _worker(rank, world, port, case, q):
+def _worker(rank, world, port, case, q, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
@@ -65,7 +67,7 @@ def _worker(rank, world, port, case, q):
     try:
         L.set_device(0)
         fid, n = CASES[case]
-        q.put((rank, _run_sharded(L, dist, "cpu", fid, n)))
+        q.put((rank, _run_sharded(L, dist, device, fid, n)))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, {"error": repr(e)}))
     finally:
@@ -73,15 +75,19 @@ def _worker(rank, world, port, case, q):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("device", ["cpu", "cuda:0"])
 @pytest.mark.parametrize("case", ["ft127", "ft63"])
-def test_sharded_world2_one_gpu(gpu, case):
+def test_sharded_world2_one_gpu(gpu, case, device):
+    """two ranks on the one GPU over gloo; with device "cuda:0" the exchanged buffers are device
+    tensors (gloo stages them through the host; RCCL, which needs one GPU per rank, moves them in
+    place) -- the device path's buffer layouts at world size 2."""
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q, device)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=280) for _ in range(2))

@@ -206,3 +206,59 @@ def test_row_sharded_protocol_world2(case):
         assert p.exitcode == 0
     r0 = res[0]
     assert r0["root"] and r0["p_eval"] and r0["p_random"] and r0["cols"] and r0["paths"], r0
+
+
+def _worker_concurrent(rank, world, port, case, q):
+    """two commitments in flight per rank, each on a process group of its own (bench.py's
+    pipelined --shard rows): both must reproduce the single-process proof"""
+    import threading
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import oracle_ffi as O
+    from lcpc_proof_of_storage_amd.shard import Comm, RowShardedCommit
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = CASES[case]
+        comm_ref, outer, pf_ref = reference(case)
+        groups = [dist.new_group([0, 1]) for _ in range(2)]
+        be = OracleBackend(O, c["fid"], c["n_per_row"], c["n_cols"], c["nco"], c["ndt"])
+        rows = comm_ref.coeffs.reshape(comm_ref.n_rows, -1)
+        out = [None, None]
+
+        def slot(i):
+            sc = RowShardedCommit(be, Comm(dist, "cpu", group=groups[i]), comm_ref.n_rows, be.wb)
+            root = sc.commit(rows[sc.r_lo:sc.r_hi])
+            tr = O.standard_transcript(c["nco"], root) if rank == 0 else None
+            pf = sc.prove(outer, tr)
+            if rank == 0:
+                out[i] = (root == comm_ref.root() and np.array_equal(pf["p_eval"], pf_ref.p_eval)
+                          and np.array_equal(pf["cols"], pf_ref.cols) and pf["paths"] == pf_ref.paths.tobytes())
+
+        ts = [threading.Thread(target=slot, args=(i,)) for i in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_row_sharded_concurrent_groups_world2():
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_concurrent, args=(r, 2, port, "ft127", q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=280) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[0] == [True, True], res[0]
