@@ -16,7 +16,7 @@ import json
 import os
 
 KERNELS = {"ntt_pass_a": "k_pass_a", "ntt_pass_b": "k_pass_b", "leaf_chunks": "k_leaf_chunks",
-           "collapse_partial": "k_collapse_partial"}
+           "collapse_partial": "k_collapse_partial", "collapse_mfma": "k_collapse_mfma"}
 
 
 def per_kernel(path):
