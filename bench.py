@@ -52,6 +52,8 @@ def parse():
                          "ranks (shard.py; RCCL exchanges; strong scaling)")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the cores available (max 16)")
+    ap.add_argument("--cpu-baseline-1core", choices=["auto", "on", "off"], default="auto",
+                    help="also time the oracle on one thread (auto: the ligero workload)")
     ap.add_argument("--no-prof", action="store_true", help="disable HIP-event kernel timing")
     ap.add_argument("--stream-mode", choices=["pool", "serial"], default="pool",
                     help="pool: each call leases its own HIP stream (kernels of different "
@@ -486,6 +488,20 @@ def main():
         }
         if oroot is not None:
             out["parity_root_vs_oracle"] = oroot == root if root is not None else None
+        # the CPU path on all host cores (above) and on one core
+        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and args.code == "ligero"
+                                                and args.shard == "none"):
+            O.lib().of_set_threads(1)
+            cpu1_s, oroot1, sample1 = wl.cpu_baseline(O)
+            out["cpu_baseline_1core"] = {
+                "value": wl.units / cpu1_s,
+                "unit": wl.unit,
+                "cores": 1,
+                "kind": "port",
+                "sample": f"{sample1} ({cpu1_s:.2f} s on 1 thread)",
+            }
+            if oroot1 is not None and root is not None:
+                out["parity_root_vs_oracle"] = out.get("parity_root_vs_oracle", True) and oroot1 == root
 
     if rank == 0:
         print(json.dumps(out))

@@ -17,6 +17,7 @@ through the C ABI; nothing here does field arithmetic.
 from __future__ import annotations
 
 import ctypes as C
+import struct
 from dataclasses import dataclass, field as dc_field
 from typing import List, Optional
 
@@ -504,6 +505,72 @@ class LcEvalProof:
         _raise(N.load().lcpc_proof_from_parts(field, n_cols, pe.shape[0], n_rows, len(p_random_vec), len(columns),
                                               path_len, _p64(pe), _p64(pr), _p64(cols), pp, C.byref(h)))
         return cls(h.value)
+
+    # ---- serialization: bincode 1.3 (fixed-width little-endian integers, u64 lengths) of the
+    # reference's WrappedLcEvalProof (lcpc-2d/src/lib.rs:576-590, 457-463, 377-381), the bytes
+    # `bincode::serialize(&pf)` produces (lcpc-ligero-pc/src/tests.rs:137): n_cols as u64;
+    # p_eval and each p_random as Vec<F>, an element being the serde newtype of ff_derive's
+    # [u64; N] (its Montgomery limbs); each column as Vec<F> plus a Vec of serde_bytes digests.
+    @staticmethod
+    def serialized_size_for(field: int, n_rows: int, n_per_row: int, n_cols: int, n_col_opens: int,
+                            n_degree_tests: int) -> int:
+        fb = 8 * limbs(field)
+        path_len = log2(n_cols)
+        return (8 + (8 + n_per_row * fb) + 8 + n_degree_tests * (8 + n_per_row * fb) + 8
+                + n_col_opens * ((8 + n_rows * fb) + 8 + path_len * (8 + 32)))
+
+    def to_bincode(self) -> bytes:
+        nl = limbs(self.field)
+        q = struct.Struct("<Q").pack
+
+        def vec_f(a):
+            a = np.ascontiguousarray(a, dtype="<u8").reshape(-1, nl)
+            return q(a.shape[0]) + a.tobytes()
+
+        parts = [q(self.n_cols), vec_f(self.p_eval), q(self.n_degree_tests)]
+        parts += [vec_f(x) for x in self.p_random_vec]
+        cols = self.columns
+        parts.append(q(len(cols)))
+        for c in cols:
+            parts.append(vec_f(c.col))
+            parts.append(q(len(c.path)))
+            parts += [q(len(d)) + bytes(d) for d in c.path]
+        return b"".join(parts)
+
+    @classmethod
+    def from_bincode(cls, field: int, data: bytes) -> "LcEvalProof":
+        """Inverse of to_bincode (the reference's bincode::deserialize of a proof)."""
+        nl = limbs(field)
+        off = 0
+
+        def u64():
+            nonlocal off
+            v = struct.unpack_from("<Q", data, off)[0]
+            off += 8
+            return v
+
+        def vec_f():
+            nonlocal off
+            n = u64()
+            a = np.frombuffer(data, dtype="<u8", count=n * nl, offset=off).astype(np.uint64).reshape(n, nl)
+            off += 8 * n * nl
+            return a
+
+        n_cols = u64()
+        p_eval = vec_f()
+        p_random = [vec_f() for _ in range(u64())]
+        columns = []
+        for _ in range(u64()):
+            col = vec_f()
+            path = []
+            for _ in range(u64()):
+                ln = u64()
+                path.append(bytes(data[off:off + ln]))
+                off += ln
+            columns.append(LcColumn(col, path))
+        if off != len(data):
+            raise LcpcError(30, "trailing bytes after a serialized proof")  # LCPC_ERR_INVALID_ARG
+        return cls.from_parts(field, n_cols, p_eval, p_random, columns)
 
     @classmethod
     def from_arrays(cls, field: int, n_cols: int, p_eval, p_random_vec, cols, paths):
