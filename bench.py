@@ -60,10 +60,15 @@ def parse():
                          "commitments overlap); serial: one in-order stream per GPU")
     ap.add_argument("--roofline-steps", type=int, default=3,
                     help="serial steps after the timed region whose encode launches give the roofline")
-    ap.add_argument("--pipeline", type=int, default=16,
+    ap.add_argument("--pipeline", type=int, default=0,
                     help="independent commitments in flight per GPU (host threads); the serial "
-                         "Merlin transcript of one overlaps the kernels of the others")
-    return ap.parse_args()
+                         "Merlin transcript of one overlaps the kernels of the others.  0: 16, or "
+                         "4 for --code pos (a 1 GiB request's 2.3 GiB codeword per slot: deeper "
+                         "pipelines only contend for HBM)")
+    args = ap.parse_args()
+    if args.pipeline <= 0:
+        args.pipeline = 4 if args.code == "pos" else 16
+    return args
 
 
 # ---------------------------------------------------------------- multi-process plumbing
