@@ -340,6 +340,13 @@ lcpc_status lcpc_pos_writer_finalize(lcpc_pos_writer *w, uint8_t *digests, uint8
  * LCPC_ERR_INVALID_ARG if an element is not canonical (from_repr(..).unwrap() panics there). */
 lcpc_status lcpc_pos_porenc_tree(const uint8_t *porenc, size_t enc, size_t rows_written,
                                  size_t row_capacity, uint8_t *tree);
+/* FileHandler::reencode_row (file_handler.rs:380-402) for a range of rows: bytes are the raw
+ * data of rows [row_lo, row_lo + ceil(n_bytes / (7 pre))) (the last row may be short and is
+ * zero-padded); each row is packed, encoded and written into the column-major .porenc image
+ * (column stride row_capacity), as replace_encoded_row does (encoded_file_reader.rs:255-315).
+ * edit_bytes / append_bytes (:279-366) re-encode the touched rows this way. */
+lcpc_status lcpc_pos_reencode_rows(const uint8_t *bytes, size_t n_bytes, size_t pre, size_t enc,
+                                   size_t row_lo, uint8_t *porenc, size_t row_capacity);
 /* EncodedFileReader::get_unencoded_row_bytes / decode_to_target_file (encoded_file_reader.rs:
  * 59-91) for rows [row_lo, row_hi): (row_hi - row_lo) * pre * 7 bytes into out */
 lcpc_status lcpc_pos_decode_porenc(const uint8_t *porenc, size_t pre, size_t enc,

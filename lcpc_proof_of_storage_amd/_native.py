@@ -139,6 +139,7 @@ SIGNATURES = {
     "lcpc_shard_collapse_device": (i32, [vp, vp, sz, vp]),
     "lcpc_shard_gather_columns_device": (i32, [vp, u64p, sz, vp]),
     "lcpc_field_sum_device": (i32, [i32, vp, sz, sz, u64p]),
+    "lcpc_pos_reencode_rows": (i32, [u8p, sz, sz, sz, sz, u8p, sz]),
     "lcpc_challenge_tensor": (i32, [vp, i32, sz, u64p]),
     "lcpc_transcript_append_field_elems": (i32, [vp, u8p, sz, i32, u64p, sz]),
     "lcpc_challenge_columns": (i32, [vp, sz, sz, u64p]),

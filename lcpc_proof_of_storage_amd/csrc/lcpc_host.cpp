@@ -2412,6 +2412,56 @@ lcpc_status lcpc_pos_encode_file(const uint8_t *data, size_t n_bytes, size_t pre
   return lcpc_pos_encode_file_batched(data, n_bytes, pre, enc, row_capacity, porenc, tree, rows_written, 0);
 }
 
+lcpc_status lcpc_pos_reencode_rows(const uint8_t *bytes, size_t n_bytes, size_t pre, size_t enc,
+                                   size_t row_lo, uint8_t *porenc, size_t row_capacity) {
+  // FileHandler::reencode_row / EncodedFileReader::replace_row_with_decoded_bytes +
+  // replace_encoded_row (file_handler.rs:380-402, encoded_file_reader.rs:196-315) for the rows
+  // [row_lo, row_lo + ceil(n_bytes / (7 pre))): pack each row's bytes (the last row may be
+  // short: zero-padded), encode, and write the canonical repr into the column-major image at
+  // column stride row_capacity.  Batches of rows go through the GPU like the writer's.
+  lcpc_status st = pos_dims_check(pre, enc);
+  if (st) return st;
+  if ((!bytes || !porenc) && n_bytes) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  const size_t rb = pre * POS_DB;
+  const size_t n_rows = (n_bytes + rb - 1) / rb;
+  if (!n_rows) return LCPC_OK;
+  if (row_lo + n_rows > row_capacity) return fail(LCPC_ERR_INVALID_ARG, "rows beyond row_capacity");
+  lcpc_encoding *ep = nullptr;
+  if ((st = make_rs_encoding(POS_FID, pre, enc, 0, 0, &ep))) return st;
+  std::unique_ptr<lcpc_encoding> eg(ep);
+  Device *dev = ep->dev;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  hipStream_t s = lease.s;
+  const size_t bmax = std::min(n_rows, std::max<size_t>(1, POS_STAGE_BYTES / (enc * POS_WB)));
+  DBuf dbytes, coeffs, comm, dout;
+  for (auto *b : {&dbytes, &coeffs, &comm, &dout}) b->s = s;
+  HIP_TRY(dbytes.alloc(dev, bmax * rb + 64));
+  HIP_TRY(coeffs.alloc(dev, bmax * pre * POS_WB));
+  HIP_TRY(comm.alloc(dev, bmax * enc * POS_WB));
+  HIP_TRY(dout.alloc(dev, bmax * enc * POS_WB));
+  Pinned stg;
+  if (!stg.get(dev, bmax * enc * POS_WB)) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  for (size_t r0 = 0; r0 < n_rows; r0 += bmax) {
+    const size_t B = std::min(bmax, n_rows - r0);
+    const size_t b0 = r0 * rb, b1 = std::min(n_bytes, b0 + B * rb);
+    const size_t ne = (b1 - b0 + POS_DB - 1) / POS_DB;
+    HIP_TRY(hipMemcpyAsync(dbytes.p, bytes + b0, b1 - b0, hipMemcpyHostToDevice, s));
+    if (B * pre > ne) HIP_TRY(hipMemsetAsync(coeffs.as<uint8_t>() + ne * POS_WB, 0, (B * pre - ne) * POS_WB, s));
+    HIP_TRY(pos_pack7(dbytes.as<uint8_t>(), b1 - b0, coeffs.as<uint64_t>(), s));
+    HIP_TRY(ntt_rows(ep->plan, coeffs.as<uint32_t>(), pre, pre, comm.as<uint32_t>(), enc, B, s, nullptr, 0, true));
+    HIP_TRY(transpose_elems(POS_FID, comm.as<uint32_t>(), B, enc, enc, enc, dout.as<uint32_t>(), B, s));
+    HIP_TRY(hipMemcpyAsync(stg.p, dout.p, B * enc * POS_WB, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint8_t *src = stg.b();
+    parallel_for(enc, [&](size_t c) {
+      std::memcpy(porenc + (c * row_capacity + row_lo + r0) * POS_WB, src + c * B * POS_WB, B * POS_WB);
+    });
+  }
+  for (auto *b : {&dbytes, &coeffs, &comm, &dout}) b->settle();
+  return LCPC_OK;
+}
+
 lcpc_status lcpc_pos_porenc_tree(const uint8_t *porenc, size_t enc, size_t rows_written,
                                  size_t row_capacity, uint8_t *tree) {
   // EncodedFileReader::process_file_to_merkle_tree (encoded_file_reader.rs:328-346): every

@@ -423,3 +423,301 @@ class EncodedFileReader:
         if self.rows_written:
             w.push_bytes(self._decode(0, self.rows_written))
         return w.finalize_to_merkle_tree()
+
+
+# ---------------------------------------------------------------- file handler
+SERVER_FILE_FOLDER = "PoR_server_files"   # databases/constants.rs:1-5
+UNENCODED_FILE_EXTENSION, ENCODED_FILE_EXTENSION = "porraw", "porenc"
+MERKLE_FILE_EXTENSION, METADATA_FILE_EXTENSION = "portree", "meta"
+
+
+def _location(directory: Optional[str], ulid: str, ext: str) -> str:
+    """file_formatter.rs get_*_file_location_from_id: <dir>/<ulid>.<ext>, dir created on demand
+    (the reference's dir is <cwd>/PoR_server_files)."""
+    d = directory if directory is not None else os.path.join(os.getcwd(), SERVER_FILE_FOLDER)
+    os.makedirs(d, exist_ok=True)
+    return os.path.join(d, f"{ulid}.{ext}")
+
+
+class FileHandler:
+    """FileHandler<Blake3, WriteableFt63, LigeroEncoding> (lcpc_online/file_handler.rs:29-712).
+
+    The server-side owner of one stored file: the raw `.porraw` bytes, the column-major
+    `.porenc` codeword, the `.portree` Merkle tree and the `.meta` JSON.  Edits and appends
+    re-encode only the touched rows (lcpc_pos_reencode_rows: pack, NTT and transpose on the GPU,
+    written into the mapped `.porenc`), then rebuild the tree from the file on the GPU
+    (lcpc_pos_porenc_tree), as the reference's edit_bytes / append_bytes do.
+    """
+
+    def __init__(self, ulid: str, unencoded: str, encoded: str, merkle: str, metadata: str):
+        # new_attach_to_existing_files (:73-143)
+        with open(metadata, "rb") as f:
+            m = EncodedFileMetadata.read_from_file(f)
+        if m.ulid != ulid:
+            raise ValueError("supplied metadata file ulid does not match!")
+        self.file_ulid = ulid
+        self.pre_encoded_size, self.encoded_size = m.pre_encoded_size, m.encoded_size
+        self.rows_written, self.row_capacity = m.rows_written, m.row_capacity
+        self.total_data_bytes = m.bytes_of_data
+        self.unencoded_file_handle, self.encoded_file_handle = unencoded, encoded
+        self.merkle_tree_file_handle, self.metadata_file_handle = merkle, metadata
+        with open(merkle, "rb") as f:
+            self.merkle_tree = MerkleTree.from_bytes(f.read())
+
+    # -- construction
+    @classmethod
+    def new_attach_to_existing_ulid(cls, file_directory: str, ulid: str) -> "FileHandler":
+        paths = [os.path.join(file_directory, f"{ulid}.{e}") for e in
+                 (UNENCODED_FILE_EXTENSION, ENCODED_FILE_EXTENSION, MERKLE_FILE_EXTENSION, METADATA_FILE_EXTENSION)]
+        for p, what in zip(paths, ("unencoded", "encoded", "merkle", "metadata")):
+            if not os.path.isfile(p):
+                raise FileNotFoundError(f"no {what} file found!")
+        return cls(ulid, *paths)
+
+    @classmethod
+    def new_attach_to_existing_files(cls, ulid, unencoded, encoded, merkle, metadata) -> "FileHandler":
+        return cls(ulid, unencoded, encoded, merkle, metadata)
+
+    @classmethod
+    def create_from_unencoded_file(cls, ulid: str, file_handle_if_not_already_ulid: Optional[str],
+                                   pre_encoded_size: int, encoded_size: int,
+                                   directory: Optional[str] = None) -> "FileHandler":
+        """:145-199 -- the raw file is moved to <ulid>.porraw, then encoded (GPU writer)."""
+        if encoded_size <= 0 or encoded_size & (encoded_size - 1):
+            raise ValueError("encoded file size must be a power of two!")
+        raw = _location(directory, ulid, UNENCODED_FILE_EXTENSION)
+        enc = _location(directory, ulid, ENCODED_FILE_EXTENSION)
+        tree = _location(directory, ulid, MERKLE_FILE_EXTENSION)
+        meta = _location(directory, ulid, METADATA_FILE_EXTENSION)
+        if file_handle_if_not_already_ulid is not None:
+            os.rename(file_handle_if_not_already_ulid, raw)
+        with open(raw, "r+b") as f:
+            m, _ = EncodedFileWriter.convert_unencoded_file(f, enc, tree, meta, pre_encoded_size, encoded_size)
+        m.ulid = ulid
+        with open(meta, "wb") as f:
+            m.write_to_file(f)
+        return cls(ulid, raw, enc, tree, meta)
+
+    # -- accessors
+    def get_encoded_file_handle(self) -> str:
+        return self.encoded_file_handle
+
+    def get_raw_file_handle(self) -> str:
+        return self.unencoded_file_handle
+
+    def get_merkle_file_handle(self) -> str:
+        return self.merkle_tree_file_handle
+
+    def get_dimensions(self) -> Tuple[int, int, int]:
+        return self.pre_encoded_size, self.encoded_size, self.rows_written
+
+    def get_encoded_metadata(self) -> EncodedFileMetadata:
+        return EncodedFileMetadata(self.pre_encoded_size, self.encoded_size, self.rows_written,
+                                   self.row_capacity, self.total_data_bytes, self.file_ulid)
+
+    def get_total_data_bytes(self) -> int:
+        return self.total_data_bytes
+
+    get_total_unencoded_bytes = get_total_data_bytes
+
+    def get_merkle_tree(self) -> MerkleTree:
+        return self.merkle_tree
+
+    def get_commit_root(self) -> bytes:
+        """LcRoot::new_from_root_digest(tree.root()) (:648-651)."""
+        return self.merkle_tree.root()
+
+    def _reader(self, f) -> EncodedFileReader:
+        return EncodedFileReader.new_ligero(f, self.pre_encoded_size, self.encoded_size, self.rows_written,
+                                            self.row_capacity)
+
+    def _row_bytes(self) -> int:
+        return self.pre_encoded_size * DATA_BYTE_CAPACITY
+
+    # -- raw data
+    def get_unencoded_bytes(self, byte_start: int, byte_end: int) -> bytes:
+        with open(self.unencoded_file_handle, "rb") as f:
+            f.seek(byte_start)
+            b = f.read(byte_end - byte_start)
+        if len(b) != byte_end - byte_start:
+            raise EOFError("failed to fill whole buffer")
+        return b
+
+    def get_unencoded_row(self, row_index: int) -> bytes:
+        """:585-602"""
+        if not row_index < self.rows_written:
+            raise IndexError("row_index out of bounds")
+        rb = self._row_bytes()
+        return self.get_unencoded_bytes(row_index * rb, min((row_index + 1) * rb, self.total_data_bytes))
+
+    # -- encoded data
+    def get_encoded_row(self, row_index: int) -> np.ndarray:
+        with open(self.encoded_file_handle, "rb") as f:
+            return self._reader(f).get_encoded_row(row_index)
+
+    def get_decoded_row(self, row_index: int) -> np.ndarray:
+        """:368-373 (decode_row of the encoded row, first pre_encoded_size elements)."""
+        with open(self.encoded_file_handle, "rb") as f:
+            return self._reader(f).get_unencoded_row(row_index)
+
+    def get_decoded_row_bytes(self, row_index: int) -> bytes:
+        with open(self.encoded_file_handle, "rb") as f:
+            return self._reader(f).get_unencoded_row_bytes(row_index)
+
+    def read_only_digests(self, columns=None) -> List[bytes]:
+        """:550-564 (columns None = ColumnsToCareAbout::All)."""
+        cols = range(self.encoded_size) if columns is None else columns
+        return [self.merkle_tree[c] for c in cols]
+
+    def read_full_columns(self, columns=None):
+        """:566-583: LcColumn(col = the column's canonical values, path = its Merkle path)."""
+        from .lcpc2d import LcColumn
+        cols = range(self.encoded_size) if columns is None else columns
+        with open(self.encoded_file_handle, "rb") as f:
+            r = self._reader(f)
+            out = []
+            for c in cols:
+                if not 0 <= c < self.encoded_size:
+                    raise IndexError("column index out of bounds")
+                out.append(LcColumn(r.get_encoded_column_without_path(c), self.merkle_tree.get_path(c)))
+        return out
+
+    # -- re-encoding
+    def _reencode_rows(self, row_lo: int, row_hi: int) -> None:
+        """Rows [row_lo, row_hi) from the raw file into the .porenc (one batched GPU pass)."""
+        if row_hi <= row_lo:
+            return
+        rb = self._row_bytes()
+        data = self.get_unencoded_bytes(row_lo * rb, min(row_hi * rb, self.total_data_bytes))
+        img_bytes = self.row_capacity * self.encoded_size * WRITTEN_BYTES_WIDTH
+        with open(self.encoded_file_handle, "r+b") as f:
+            if os.fstat(f.fileno()).st_size < img_bytes:
+                raise ValueError("encoded file shorter than row_capacity * encoded_size elements")
+            mm = mmap.mmap(f.fileno(), img_bytes)
+            try:
+                arr = np.frombuffer(mm, np.uint8)
+                p, keep = _bytes_ptr(data)
+                _raise(N.load().lcpc_pos_reencode_rows(p, len(data), self.pre_encoded_size, self.encoded_size,
+                                                       row_lo, _u8(arr), self.row_capacity))
+                del arr
+                mm.flush()
+            finally:
+                mm.close()
+
+    def reencode_row(self, row_index: int) -> None:
+        """:380-402"""
+        if not row_index < self.rows_written:
+            raise IndexError("cannot reencode a row that is out of bounds")
+        self._reencode_rows(row_index, row_index + 1)
+
+    def reencode_unencoded_file(self) -> None:
+        """:406-462 -- the whole raw file through the GPU writer again."""
+        self.total_data_bytes = os.path.getsize(self.unencoded_file_handle)
+        with open(self.unencoded_file_handle, "rb") as raw, open(self.encoded_file_handle, "w+b") as tf:
+            w = EncodedFileWriter(self.pre_encoded_size, self.encoded_size, self.total_data_bytes, tf)
+            if self.total_data_bytes:
+                w.push_bytes(raw.read())
+            m, tree = w.finalize_to_merkle_tree()
+        self.write_tree(tree)
+        self.pre_encoded_size, self.encoded_size = m.pre_encoded_size, m.encoded_size
+        self.total_data_bytes, self.row_capacity, self.rows_written = m.bytes_of_data, m.row_capacity, m.rows_written
+        self._write_metadata()
+        self.merkle_tree = tree
+
+    def edit_bytes(self, byte_start: int, unencoded_bytes_to_add: bytes) -> Tuple[bytes, MerkleTree]:
+        """:279-333 -- returns the bytes that were replaced and the new tree."""
+        if not os.path.isfile(self.unencoded_file_handle):
+            raise FileNotFoundError("no unencoded file found!")
+        n = len(unencoded_bytes_to_add)
+        if byte_start + n > self.total_data_bytes:
+            raise ValueError("can't edit more bytes than there are in the file!")
+        with open(self.unencoded_file_handle, "r+b") as f:
+            f.seek(byte_start)
+            original = f.read(n)
+            f.seek(byte_start)
+            f.write(unencoded_bytes_to_add)
+        rb = self._row_bytes()
+        self._reencode_rows(byte_start // rb, -(-(byte_start + n) // rb))
+        return original, self.recalculate_merkle_tree()
+
+    def append_bytes(self, bytes_to_add: bytes) -> MerkleTree:
+        """:335-366"""
+        with open(self.unencoded_file_handle, "ab") as f:
+            f.write(bytes_to_add)
+        rb = self._row_bytes()
+        start_row = self.total_data_bytes // rb
+        end_row = -(-(self.total_data_bytes + len(bytes_to_add)) // rb)
+        if end_row > self.row_capacity:
+            with open(self.encoded_file_handle, "r+b") as f:
+                self._reader(f).set_new_capacity(end_row * 2)
+            self.row_capacity = end_row * 2
+        self.total_data_bytes += len(bytes_to_add)
+        self.rows_written = end_row
+        self._reencode_rows(start_row, end_row)
+        tree = self.recalculate_merkle_tree()
+        self._write_metadata()
+        return tree
+
+    def reshape(self, new_pre_encoded_columns: int, new_encoded_columns: int
+                ) -> Tuple[EncodedFileMetadata, MerkleTree]:
+        """:224-276 (convert_unencoded_file with the new shape)."""
+        with open(self.unencoded_file_handle, "r+b") as f:
+            m, tree = EncodedFileWriter.convert_unencoded_file(
+                f, self.encoded_file_handle, self.merkle_tree_file_handle, self.metadata_file_handle,
+                new_pre_encoded_columns, new_encoded_columns)
+        self.pre_encoded_size, self.encoded_size = new_pre_encoded_columns, new_encoded_columns
+        self.rows_written, self.row_capacity = m.rows_written, m.row_capacity
+        self.merkle_tree = tree
+        self._write_metadata()  # keeps the ulid, which convert_unencoded_file's metadata lacks
+        m.ulid = self.file_ulid
+        return m, tree
+
+    # -- tree and metadata
+    def recalculate_merkle_tree(self) -> MerkleTree:
+        """:474-481 (process_file_to_merkle_tree on the GPU)."""
+        with open(self.encoded_file_handle, "rb") as f:
+            tree = self._reader(f).process_file_to_merkle_tree()
+        self.merkle_tree = tree
+        self.write_tree(tree)
+        return tree
+
+    def write_tree(self, tree: MerkleTree) -> None:
+        if len(tree) != self.encoded_size * 2 - 1:
+            raise ValueError("this Merkle tree is the incorrect size")
+        with open(self.merkle_tree_file_handle, "wb") as f:
+            write_tree_to_file(f, tree)
+
+    def _write_metadata(self) -> None:
+        with open(self.metadata_file_handle, "wb") as f:
+            self.get_encoded_metadata().write_to_file(f)
+
+    def verify_all_files_agree(self) -> None:
+        """:505-541: the tree from the .porenc, and the tree of a fresh encode of the raw file,
+        must both equal the stored tree (and the raw file must hold total_data_bytes)."""
+        if self.recalculate_tree_only() != self.merkle_tree:
+            raise AssertionError("the encoded file's tree differs from the stored tree")
+        n = os.path.getsize(self.unencoded_file_handle)
+        if n != self.total_data_bytes:
+            raise AssertionError("raw file length differs from the metadata")
+        rows = -(-(-(-n // DATA_BYTE_CAPACITY)) // self.pre_encoded_size)
+        img = np.zeros(max(rows, 1) * self.encoded_size * WRITTEN_BYTES_WIDTH, np.uint8)
+        data = np.fromfile(self.unencoded_file_handle, np.uint8)
+        tree = np.zeros((2 * self.encoded_size - 1, DIGEST_BYTES), np.uint8)
+        out_rows = C.c_size_t()
+        _raise(N.load().lcpc_pos_encode_file(_u8(data), n, self.pre_encoded_size, self.encoded_size, max(rows, 1),
+                                             _u8(img), _u8(tree), C.byref(out_rows)))
+        if MerkleTree(tree) != self.merkle_tree:
+            raise AssertionError("the raw file's re-encoded tree differs from the stored tree")
+
+    def recalculate_tree_only(self) -> MerkleTree:
+        with open(self.encoded_file_handle, "rb") as f:
+            return self._reader(f).process_file_to_merkle_tree()
+
+    def delete_all_files(self) -> None:
+        """:678-694"""
+        for p in (self.unencoded_file_handle, self.encoded_file_handle, self.merkle_tree_file_handle,
+                  self.metadata_file_handle):
+            os.remove(p)
+        d = os.path.dirname(self.unencoded_file_handle)
+        if not os.listdir(d):
+            os.rmdir(d)
