@@ -154,3 +154,25 @@ def test_reshape_and_columns_verify(PF, oracle, tmp_path):
     with pytest.raises(ValueError):
         fh.edit_bytes(len(data) - 10, b"x" * 11)
     fh.delete_all_files()
+
+
+@pytest.mark.parametrize("chunks", [[0, 5, 7 * 4, 1], [7 * 4 * 3], [1] * 9])
+def test_append_from_empty_and_on_row_boundaries(PF, oracle, tmp_path, chunks):
+    """appends into an empty file, exactly up to row boundaries and byte by byte (the capacity
+    starts at zero and doubles: EncodedFileReader::set_new_capacity layout)"""
+    pre, enc = 4, 8
+    src = tmp_path / "empty.bin"
+    src.write_bytes(b"")
+    fh = PF.FileHandler.create_from_unencoded_file("01EMPTYTEST000000000000000", str(src), pre, enc,
+                                                   directory=str(tmp_path / "files"))
+    contents = bytearray()
+    rng = np.random.default_rng(len(chunks))
+    for n in chunks:
+        new = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        fh.append_bytes(new)
+        contents += new
+        assert _read(fh.get_raw_file_handle()) == bytes(contents)
+        if contents:
+            fh.verify_all_files_agree()
+            _check_against_oracle(fh, oracle, bytes(contents))
+    fh.delete_all_files()
