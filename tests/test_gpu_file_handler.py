@@ -6,7 +6,7 @@ decode, verify_all_files_agree), every edited `.porenc` column and the tree are 
 the oracle's fresh encode of the edited raw data (oracle_ffi.pos_encode_file), bit for bit.
 
 The reference's 10000-byte fixture (test_files/10000_byte_file.bytes) is not in the
-repository; a 10000-byte ChaCha-like stream of the same size stands in.  test.txt is the
+repository; 10000 bytes from numpy.random.default_rng stand in.  test.txt is the
 reference's own (tests/golden/pos_test.txt).
 """
 import os
