@@ -42,12 +42,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1024)
     ap.add_argument("--warmup", type=int, default=64)
-    ap.add_argument("--log-len", type=int, default=24)
+    ap.add_argument("--log-len", type=int, default=None, help="log2 coefficients (24; 20 for --code encode)")
     ap.add_argument("--field", default="Ft127")
-    ap.add_argument("--code", choices=["ligero", "sdig", "pos"], default="ligero",
+    ap.add_argument("--code", choices=["ligero", "sdig", "pos", "encode"], default="ligero",
                     help="ligero: R-S / NTT rows (the BASELINE metric, cfg3); sdig: Brakedown "
                          "SdigCode3 expander code, seed 0 (cfg4); pos: proof-of-storage request "
-                         "on a resident file (cfg5)")
+                         "on a resident file (cfg5); encode: the Ligero R-S encode alone (cfg2)")
     ap.add_argument("--pos-bytes", type=int, default=1 << 30, help="file size for --code pos")
     ap.add_argument("--shard", choices=["none", "rows"], default="none",
                     help="rows: one Ligero commitment per step with its rows split across the "
@@ -72,6 +72,8 @@ def parse():
                          "4 for --code pos (a 1 GiB request's 2.3 GiB codeword per slot: deeper "
                          "pipelines only contend for HBM)")
     args = ap.parse_args()
+    if args.log_len is None:
+        args.log_len = 20 if args.code == "encode" else 24
     if args.pipeline <= 0:
         args.pipeline = 4 if args.code == "pos" else 16
     return args
@@ -195,6 +197,58 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
         mul_count=(n_rows * enc.matrix_nnz if sdig else n_rows * ntt_muls(n_cols)),
         mul_model=("one product per nonzero per row" if sdig else
                    "four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row"))
+
+
+def encode_workload(args, L, torch, rank, local_rank):
+    """cfg2: the Ligero R-S encode alone (LcEncoding::encode on every row of a 2^20-coefficient
+    commitment, lcpc-ligero-pc/src/lib.rs:162-164 -> fft_io), device rows in, device rows out."""
+    fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
+    nl = L.limbs(fid)
+    n = 1 << args.log_len
+    enc = L.LigeroEncoding.new(fid, n)
+    n_rows, n_per_row, n_cols = enc.get_dims(n)
+    coeffs = L.field_random(fid, n_rows * n_per_row, replica_seed(rank))
+    dev = f"cuda:{local_rank}"
+    d_src = torch.from_numpy(coeffs.view(np.int64)).to(dev)
+    dst = [torch.empty(n_rows * n_cols * nl, dtype=torch.int64, device=dev) for _ in range(max(1, args.pipeline))]
+    torch.cuda.synchronize()
+
+    def step(slot):
+        enc.encode_rows_device(d_src.data_ptr(), n_per_row, n_per_row, dst[slot].data_ptr(), n_cols, n_rows)
+        return None
+
+    def cpu_baseline(O):
+        # the same rows through the oracle's fft_io, then every GPU row against it
+        rows = coeffs.reshape(n_rows, n_per_row * nl)
+        t1 = time.perf_counter()
+        outs = []
+        for r in range(n_rows):
+            x = np.zeros(n_cols * nl, np.uint64)
+            x[:n_per_row * nl] = rows[r]
+            outs.append(O.fft_io(fid, x))
+        dt = time.perf_counter() - t1
+        step(0)
+        torch.cuda.synchronize()
+        got = dst[0].cpu().numpy().view(np.uint64).reshape(n_rows, n_cols * nl)
+        ok = all(np.array_equal(got[r], outs[r]) for r in range(n_rows))
+        return dt, ok, f"fft_io of all {n_rows} rows of the same 2^{args.log_len} {args.field} workload"
+
+    B = 8 * nl
+    return Workload(
+        units=n_rows * n_per_row, unit="field-elements/s", bytes_per_unit=B,
+        metric=f"encoded field-elements/s (Ligero R-S encode), 2^{args.log_len}-coeff {args.field} (cfg2)",
+        dtype=f"u64x{nl} ({args.field} Montgomery limbs)",
+        data=f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), resident in HBM",
+        config={"workload": f"Ligero R-S encode, {args.field}, 2^{args.log_len} coeffs, "
+                            f"{n_rows}x{n_per_row}->{n_cols}",
+                "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols},
+        step=step, cpu_baseline=cpu_baseline, cpu_cores=1, root_is_parity=True,
+        enc_kernels=("ntt_pass_a", "ntt_pass_b"),
+        enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per step, all {n_rows} rows)",
+        algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B,
+        traffic_key=(n, args.field, "encode"),
+        mul_count=n_rows * ntt_muls(n_cols),
+        mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row")
 
 
 def shard_workload(args, L, torch, rank, local_rank, dist):
@@ -333,7 +387,8 @@ def main():
     if args.shard == "rows":
         wl = shard_workload(args, L, torch, rank, local_rank, dist)
     else:
-        wl = (pos_workload if args.code == "pos" else ligero_or_sdig)(args, L, torch, rank, local_rank)
+        wl = {"pos": pos_workload, "encode": encode_workload}.get(args.code, ligero_or_sdig)(
+            args, L, torch, rank, local_rank)
     torch.cuda.synchronize()
 
     prof = not args.no_prof
@@ -487,7 +542,7 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ffi as O  # checker / CPU baseline only
 
-        cores = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        cores = getattr(wl, "cpu_cores", None) or args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         O.lib().of_set_threads(cores)
         cpu_s, oroot, sample = wl.cpu_baseline(O)
         out["cpu_baseline"] = {
@@ -497,7 +552,9 @@ def main():
             "kind": "port",
             "sample": f"{sample} ({cpu_s:.2f} s on {cores} threads)",
         }
-        if oroot is not None:
+        if getattr(wl, "root_is_parity", False):
+            out["parity_vs_oracle"] = bool(oroot)  # every encoded row equal to the oracle's
+        elif oroot is not None:
             out["parity_root_vs_oracle"] = oroot == root if root is not None else None
         # the CPU path on all host cores (above) and on one core
         if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and args.code == "ligero"
