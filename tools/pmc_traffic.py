@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """HBM traffic of the encode kernels from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-    python tools/pmc_traffic.py gpurun_out/<tag> profiles/pmc_traffic.json [--len N --field F]
+    python tools/pmc_traffic.py gpurun_out/<tag> profiles/pmc_traffic[_<code>].json [--len N --field F --code C]
+
+bench.py reads every profiles/pmc_traffic*.json and uses the one whose (len, field, code)
+matches its workload.
 
 Counter units are KiB.  Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): on gfx950
 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced streaming read, so it is
@@ -34,6 +37,7 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--len", type=int, default=1 << 24)
     ap.add_argument("--field", default="Ft127")
+    ap.add_argument("--code", default="ligero", help="bench.py --code of the profiled run")
     a = ap.parse_args()
     fpath = glob.glob(os.path.join(a.run_dir, "pmc_fetch", "*counter_collection.csv"))[0]
     wpath = glob.glob(os.path.join(a.run_dir, "pmc_write", "*counter_collection.csv"))[0]
@@ -47,7 +51,7 @@ def main():
                    "hbm_bytes": rd + wr, "launches": nf[k]}
     enc = kern["ntt_pass_a"]["hbm_bytes"] + kern["ntt_pass_b"]["hbm_bytes"]
     out = {
-        "config_len": a.len, "field": a.field,
+        "config_len": a.len, "field": a.field, "code": a.code,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
                   "(bench.py --pipeline 1); FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> B",
         "ntt_encode_bytes_per_launch": enc,
