@@ -208,3 +208,21 @@ def test_partial_and_full_polynomial_evaluation(gpu, pos, oracle):
     bad[3, 0] = (int(bad[3, 0]) + 1) % p
     with pytest.raises(pos.VerifierError):
         pos.verifiable_full_polynomial_evaluation(left, right_np, bad, cols, opened, np_, nc)
+    # server_retreive_columns (lcpc_online.rs:242-249) opens the same columns as the request path
+    again = pos.server_retreive_columns(comm, cols)
+    assert all(np.array_equal(a.col, b.col) and list(a.path) == list(b.path) for a, b in zip(again, opened))
+    # the single-point wrapper (lcpc_online.rs:545-566) forms its side vectors over n_cols, as the
+    # reference passes them, then runs the same check
+    left_nc, right_nc = pos.form_side_vectors_for_polynomial_evaluation_from_point(x, n_rows, nc)
+    dec_nc = pos.left_multiply_unencoded_matrix_by_vector(data, np_, left_nc)
+    res_nc = pos.verifiable_polynomial_evaluation(comm, left_nc)
+    pos.verify_proper_partial_polynomial_evaluation(left_nc, res_nc, cols, opened)
+    got_w = pos.verify_full_polynomial_evaluation_wrapper_with_single_eval_point(x, dec_nc, n_rows, nc, cols,
+                                                                                opened, np_)
+    got_d = pos.verifiable_full_polynomial_evaluation(left_nc, right_nc, dec_nc, cols, opened, np_, nc)
+    assert np.array_equal(got_w, got_d)
+    bad_nc = dec_nc.copy()
+    bad_nc[0, 0] = (int(bad_nc[0, 0]) + 1) % p
+    with pytest.raises(pos.VerifierError):
+        pos.verify_full_polynomial_evaluation_wrapper_with_single_eval_point(x, bad_nc, n_rows, nc, cols,
+                                                                            opened, np_)
