@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--stream-mode", choices=["pool", "serial"], default="pool",
                     help="pool: each call leases its own HIP stream (kernels of different "
                          "commitments overlap); serial: one in-order stream per GPU")
+    ap.add_argument("--verify-reps", type=int, default=8,
+                    help="verifies of one proof timed after the timed region (ligero/sdig; 0: skip)")
     ap.add_argument("--roofline-steps", type=int, default=3,
                     help="serial steps after the timed region whose encode launches give the roofline")
     ap.add_argument("--pipeline", type=int, default=0,
@@ -166,13 +168,41 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
         c.prove(outer, enc, tr)
         return root
 
+    inner = L.field_random(fid, n_per_row, 8)  # verify returns sum_c inner[c] p_eval[c]
+    cpu_verify = []  # (ms, accepted, evaluation) per cpu_baseline call
+
     def cpu_baseline(O):
         o_enc = (O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3) if sdig
                  else O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt))
         t1 = time.perf_counter()
         oc = O.Commit(o_enc, coeffs.reshape(-1))
-        oc.prove(o_enc, outer.reshape(-1), O.standard_transcript(nco, oc.root()))
-        return time.perf_counter() - t1, oc.root(), f"one full commit+open of the same 2^{args.log_len} {args.field} workload"
+        op = oc.prove(o_enc, outer.reshape(-1), O.standard_transcript(nco, oc.root()))
+        dt = time.perf_counter() - t1
+        # the oracle's verify of its own proof (outside the commit+open figure)
+        t2 = time.perf_counter()
+        rc, ev = op.verify(oc.root(), outer.reshape(-1), inner.reshape(-1), o_enc,
+                           O.standard_transcript(nco, oc.root()))
+        cpu_verify.append((1e3 * (time.perf_counter() - t2), rc == 0, ev))
+        return dt, oc.root(), f"one full commit+open of the same 2^{args.log_len} {args.field} workload"
+
+    def verify_bench(reps):
+        """LcEvalProof::verify (lcpc-2d/src/lib.rs:862-982) of one proof of this workload: the
+        verifier's encodes of p_random / p_eval and the column checks, timed over `reps` calls."""
+        c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+        root = c.get_root()
+
+        def tr():
+            t = L.Transcript(b"test transcript")
+            t.append_message(b"polycommit", root)
+            t.append_message(b"ncols", nco.to_bytes(8, "big"))
+            return t
+
+        pf = c.prove(outer, enc, tr())
+        ev = pf.verify(root, outer, inner, enc, tr())
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            pf.verify(root, outer, inner, enc, tr())
+        return 1e3 * (time.perf_counter() - t1) / reps, ev
 
     B = 8 * nl
     name = (f"Brakedown (SdigCode3, seed 0) commit+open, {args.field}, 2^{args.log_len} coeffs, " if sdig
@@ -187,7 +217,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
                                    f"BLAKE3 Merkle",
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                 "n_col_opens": nco, "n_degree_tests": ndt},
-        step=step, cpu_baseline=cpu_baseline,
+        step=step, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify,
         enc_kernels=("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b"),
         enc_kernel_desc=("sdig_encode = transpose + 13 SpMM / Reed-Solomon levels (per commit, all rows)" if sdig
                          else f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
@@ -543,6 +573,13 @@ def main():
                 "model": wl.mul_model,
             }
 
+    # ---- the verifier (outside the timed region): one proof of this workload, verified again
+    gev = None
+    if getattr(wl, "verify_bench", None) and args.verify_reps > 0:
+        vms, gev = wl.verify_bench(args.verify_reps)
+        out["verify"] = {"ms": vms, "reps": args.verify_reps,
+                         "what": "LcEvalProof::verify of one proof of this workload (host + GPU, serial)"}
+
     # ---- CPU baseline: the oracle (C restatement) on the same workload, rank 0 at N = 1
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
     if rank == 0 and want_cpu:
@@ -578,6 +615,14 @@ def main():
             if oroot1 is not None and root is not None:
                 out["parity_root_vs_oracle"] = out.get("parity_root_vs_oracle", True) and oroot1 == root
 
+    cv = getattr(wl, "cpu_verify", None)
+    if cv and "verify" in out:
+        out["verify"]["cpu_ms"] = cv[0][0]
+        if len(cv) > 1:
+            out["verify"]["cpu_1core_ms"] = cv[1][0]
+        out["verify"]["parity_vs_oracle"] = bool(all(a for _, a, _ in cv) and gev is not None and
+                                                 np.array_equal(np.asarray(cv[0][2]).reshape(-1),
+                                                                np.asarray(gev).reshape(-1)))
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:
