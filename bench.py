@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+LEAF_PEAK_GCPS = 54.2    # BLAKE3 compressions/s with no loads (tools/microbench/leafbench.hip, MI355X)
 SEED = 0x1CDC2024       # coefficients = F::random(ChaCha20Rng::seed_from_u64(SEED))
 
 
@@ -137,6 +138,16 @@ def ntt_muls(n):
     return (n // 2) * max(lg - 2, 0) + n
 
 
+def leaf_compressions(n_rows, n_cols, elem_bytes):
+    """BLAKE3 compressions of the column leaves (lcpc-2d/src/lib.rs:736-775): each leaf message
+    is 32 zero bytes + n_rows elements, one compression per 64-byte block (the last one of a
+    chunk included), plus the chunk-merge parents (chunks - 1 per column)."""
+    msg = 32 + n_rows * elem_bytes
+    blocks = -(-msg // 64)
+    chunks = -(-msg // 1024)
+    return n_cols * (blocks + chunks - 1)
+
+
 class Workload:
     """One bench configuration: `step(slot)` runs one pass of the hot path on resident inputs."""
 
@@ -224,6 +235,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
         # encode bytes per commit (read the coefficients, write the codeword; SDIG
         # also streams its code matrices once: 16-B values + 4-B indices)
         algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B + (enc.matrix_nnz * (B + 4) if sdig else 0),
+        leaf_compressions=leaf_compressions(n_rows, n_cols, B),
         traffic_key=(n, args.field, args.code),
         mul_count=(n_rows * enc.matrix_nnz if sdig else n_rows * ntt_muls(n_cols)),
         mul_model=("one product per nonzero per row" if sdig else
@@ -404,6 +416,7 @@ def pos_workload(args, L, torch, rank, local_rank):
         enc_kernels=("ntt_pass_a", "ntt_pass_b"),
         enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)",
         algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
+        leaf_compressions=leaf_compressions(n_rows, nc, 8),
         traffic_key=(n_el, "Ft63", "pos"),
         mul_count=n_rows * ntt_muls(nc),
         mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row")
@@ -572,6 +585,17 @@ def main():
                 "frac": ach / peak if ach and peak else None, "muls_per_launch": wl.mul_count,
                 "model": wl.mul_model,
             }
+
+    # ---- the column-leaf kernels against the BLAKE3 compression rate (VALU-issue bound)
+    lc = getattr(wl, "leaf_compressions", 0)
+    if iso and lc and "leaf_chunks" in iso:
+        leaf_ms = sum(iso[k][0] / max(iso[k][1], 1) for k in ("leaf_chunks", "leaf_merge") if k in iso)
+        ach = lc / (leaf_ms * 1e-3) / 1e9
+        out["roofline_leaf"] = {
+            "kernel": "leaf_chunks + leaf_merge (BLAKE3 column leaves)", "bound": "valu (BLAKE3 compressions)",
+            "achieved": ach, "peak": LEAF_PEAK_GCPS, "unit": "G compressions/s", "frac": ach / LEAF_PEAK_GCPS,
+            "compressions_per_launch": lc, "avg_ms": leaf_ms,
+            "peak_source": "tools/microbench/leafbench.hip compress-only twin of the leaf kernel, MI355X"}
 
     # ---- the verifier (outside the timed region): one proof of this workload, verified again
     gev = None

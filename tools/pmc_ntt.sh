@@ -1,8 +1,8 @@
 #!/bin/bash
 # Issue-level PMC counters of the encode kernels (one counter group per rocprofv3 pass).
-# Usage (repo root, on the box): bash tools/pmc_ntt.sh <tag>
+# Usage (repo root, on the box): bash tools/pmc_ntt.sh <tag> [bench args...]
 set -o pipefail
-TAG=${1:-ntt}
+TAG=${1:-ntt}; shift
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -13,7 +13,7 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
            "SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp -d "$OUT/p$i" -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --pipeline 1 --cpu-baseline off --no-prof > /dev/null 2> "$OUT/p$i.err" \
+    python3 bench.py --steps 2 --warmup 1 --pipeline 1 --cpu-baseline off --no-prof --verify-reps 0 "$@" > /dev/null 2> "$OUT/p$i.err" \
     || { tail -20 "$OUT/p$i.err"; exit 1; }
 done
 echo done
