@@ -229,7 +229,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                 "n_col_opens": nco, "n_degree_tests": ndt},
         step=step, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify,
-        enc_kernels=("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b"),
+        enc_kernels=("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=("sdig_encode = transpose + 13 SpMM / Reed-Solomon levels (per commit, all rows)" if sdig
                          else f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
         # encode bytes per commit (read the coefficients, write the codeword; SDIG
@@ -292,7 +292,7 @@ def encode_workload(args, L, torch, rank, local_rank):
                             f"{n_rows}x{n_per_row}->{n_cols}",
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols},
         step=step, cpu_baseline=cpu_baseline, cpu_cores=1, root_is_parity=True,
-        enc_kernels=("ntt_pass_a", "ntt_pass_b"),
+        enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per step, all {n_rows} rows)",
         algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B,
         traffic_key=(n, args.field, "encode"),
@@ -355,7 +355,7 @@ def shard_workload(args, L, torch, rank, local_rank, dist):
                             f"{n_cols}, rows sharded at BLAKE3 chunk boundaries",
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                 "n_col_opens": nco, "n_degree_tests": ndt},
-        step=step, cpu_baseline=cpu_baseline, enc_kernels=("ntt_pass_a", "ntt_pass_b"),
+        step=step, cpu_baseline=cpu_baseline, enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc="ntt_encode = ntt_pass_a + ntt_pass_b (this rank's rows)",
         algo_bytes=0, traffic_key=None, mul_count=0, mul_model="")
 
@@ -413,7 +413,7 @@ def pos_workload(args, L, torch, rank, local_rank):
                             f"dims {n_rows}x{np_}->{nc}, u^T Enc(M) at a point, 256 opened columns",
                 "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd},
         step=step, cpu_baseline=cpu_baseline,
-        enc_kernels=("ntt_pass_a", "ntt_pass_b"),
+        enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)",
         algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
         leaf_compressions=leaf_compressions(n_rows, nc, 8),
@@ -568,7 +568,7 @@ def main():
             "traffic": traffic,
             "algorithmic_bytes": wl.algo_bytes,
             "avg_ms": enc_ms,
-            "launches": min(ki.get(k, {}).get("launches", 0) for k in wl.enc_kernels),
+            "launches": min((ki[k]["launches"] for k in wl.enc_kernels if k in ki), default=0),
             "measured": f"HIP events on the launching stream, {args.roofline_steps} serial steps after the "
                         f"timed region (same process, inputs and kernels)",
             "timed_region_avg_ms": tr_ms,

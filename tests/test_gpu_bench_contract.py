@@ -1,0 +1,74 @@
+"""GPU: bench.py's output contract on small shapes, one child process per workload.
+
+The driver parses one JSON line per run; these runs check its keys (metric, value, unit,
+roofline with bound / achieved / peak / unit / frac / traffic, cpu_baseline with value / unit /
+cores / kind / sample) and the parity flags the bench computes against the oracle.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, timeout=100):
+    env = dict(os.environ)
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _check_common(d, steps):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == steps and d["value"] > 0 and d["higher_is_better"] is True
+    assert d["scaling"] in ("weak", "strong") and "workload" in d["config"]
+    rf = d["roofline"]
+    assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s")
+    assert rf["achieved"] > 0 and rf["peak"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    assert "traffic" in rf
+
+
+def _check_cpu(d):
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference") and cb["sample"]
+    assert cb["unit"] == d["unit"]
+
+
+def test_bench_ligero_small(gpu):
+    d = _bench("--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1")
+    _check_common(d, 4)
+    _check_cpu(d)
+    assert d["parity_root_vs_oracle"] is True
+    assert d["verify"]["parity_vs_oracle"] is True and d["verify"]["ms"] > 0
+    assert d["config"]["n_rows"] * d["config"]["n_per_row"] == 1 << 16
+
+
+def test_bench_encode_small(gpu):
+    d = _bench("--code", "encode", "--steps", "4", "--warmup", "2", "--log-len", "14")
+    _check_common(d, 4)
+    _check_cpu(d)
+    assert d["parity_vs_oracle"] is True
+
+
+def test_bench_sdig_small(gpu):
+    d = _bench("--code", "sdig", "--steps", "2", "--warmup", "2", "--log-len", "14", "--cpu-baseline", "off",
+               "--verify-reps", "1")
+    _check_common(d, 2)
+    assert "cpu_baseline" not in d
+
+
+def test_bench_pos_small(gpu):
+    d = _bench("--code", "pos", "--steps", "2", "--warmup", "2", "--pos-bytes", str(1 << 20))
+    _check_common(d, 2)
+    _check_cpu(d)
