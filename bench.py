@@ -508,6 +508,8 @@ def main():
         # The roofline launches: the same step run serially after the timed region, so each
         # encode launch has the GPU to itself (inside the pipelined region, kernels of
         # different commitments share the CUs and a launch's duration measures the sharing).
+        # One untimed step first: this (main) thread's pinned staging is allocated on first use.
+        wl.step(0)
         L.prof_reset()
         L.prof_enable(True)
         for _ in range(args.roofline_steps):
