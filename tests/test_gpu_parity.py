@@ -84,6 +84,25 @@ def test_commit_matches_oracle(gpu, oracle, fid, n_per_row, n_cols, length):
     assert g.get_root() == o.root()
 
 
+def test_commit_empty_and_oversized_inputs(gpu, oracle):
+    """commit's shape asserts (lcpc-2d/src/lib.rs:659-661) are LcpcError here, not a panic: an
+    empty polynomial has no rows ((n_rows - 1) underflows in the reference); a device commit of
+    zero elements likewise.  Encoding dims that break dims_ok are refused at construction."""
+    enc = gpu.RsEncoding.new(1, 8, 16, 4, 1)
+    with pytest.raises(gpu.LcpcError):
+        gpu.LcCommit.commit(np.zeros(0, np.uint64), enc)
+    with pytest.raises(gpu.LcpcError):
+        gpu.LcCommit.commit_device(0, 0, enc)
+    with pytest.raises(gpu.LcpcError):
+        gpu.RsEncoding.new(1, 8, 12, 4, 1)      # n_cols not a power of two
+    with pytest.raises(gpu.LcpcError):
+        gpu.RsEncoding.new(1, 16, 16, 4, 1)     # no redundancy (n_per_row == n_cols)
+    # one element: a single row whose tail is zero-padded, as the reference pads
+    c = gpu.LcCommit.commit(rand_elems(oracle, 1, 1, 3), enc)
+    o = oracle.Commit(oracle.Encoding.ligero(1, 8, 16, 4, 1), rand_elems(oracle, 1, 1, 3))
+    assert c.get_n_rows() == 1 and c.get_root() == o.root()
+
+
 @pytest.mark.parametrize("fid,n_per_row,n_cols,length", [
     (1, 2048, 4096, 1 << 16),          # small-row kernel
     (0, 100, 256, 3000),               # ragged, small-row kernel
