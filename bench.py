@@ -428,7 +428,12 @@ def main():
     os.environ["LCPC_STREAM_MODE"] = args.stream_mode  # read when the library creates streams
     import torch
 
-    dist = init_dist(world, local_rank)
+    # LCPC_BENCH_BACKEND=gloo with LCPC_BENCH_SHARE_GPU=1 rehearses N ranks on one GPU (a
+    # one-GPU box); the default is one rank per GPU over RCCL
+    backend = os.environ.get("LCPC_BENCH_BACKEND", "nccl")
+    if os.environ.get("LCPC_BENCH_SHARE_GPU") == "1":
+        local_rank = 0
+    dist = init_dist(world, local_rank, backend=backend)
     torch.cuda.set_device(local_rank)
 
     import lcpc_proof_of_storage_amd as L
@@ -516,7 +521,7 @@ def main():
             wl.step(0)
         L.prof_enable(False)
         iso = L.prof_stats()
-    elapsed = max_over_ranks(dist, elapsed, f"cuda:{local_rank}")
+    elapsed = max_over_ranks(dist, elapsed, "cpu" if backend == "gloo" else f"cuda:{local_rank}")
     scaling = getattr(wl, "scaling", "weak")
     value = job_throughput(wl.units, args.steps, world if scaling == "weak" else 1, elapsed)
     out = {
