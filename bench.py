@@ -583,9 +583,9 @@ def main():
         if wl.mul_count:  # noqa: E501
             # the encode is bound by the 32-bit multiply-add pipe, not HBM: its VALU roofline is
             # the Montgomery-multiply rate of the field measured in isolation
-            # (the best of tools/microbench/femul_variants.hip and mulbench.hip on MI355X:
-            # Ft63 1595, Ft127 473, Ft255 133 G/s; profiles/r01_mulbench.txt)
-            peak = {"Ft63": 1595.0, "Ft127": 473.0, "Ft255": 133.0}.get(args.field if args.code != "pos" else "Ft63")
+            # (the library multiply in isolation, tools/microbench/femul2.hip on MI355X:
+            # Ft63 1701, Ft127 503, Ft255 137 G/s; profiles/r01_femul2.txt)
+            peak = {"Ft63": 1701.0, "Ft127": 503.0, "Ft255": 137.0}.get(args.field if args.code != "pos" else "Ft63")
             ach = wl.mul_count / (enc_ms * 1e-3) / 1e9 if enc_ms else None
             out["roofline_valu"] = {
                 "kernel": wl.enc_kernel_desc, "bound": "valu (v_mad_u64_u32 Montgomery products)",
