@@ -179,7 +179,7 @@ hipError_t ntt_rows_v1(const NttPlan &p, const uint32_t *src, size_t ss, size_t 
   if (p.log_n <= 12) {
     prof::Scope ps("ntt_small", s);
     hipLaunchKernelGGL((k_ntt_small<F>), dim3(n_rows), dim3(NTHREADS), 0, s, src, ss, nv, dst, ds,
-                       p.d_tw, p.log_n, (uint32_t *)nullptr, (size_t)0);
+                       p.d_tw, p.log_n, (uint32_t *)nullptr, (size_t)0, 0);
     return hipGetLastError();
   }
   constexpr int LE = log_elems<F>();

@@ -103,6 +103,13 @@ void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
       V2(7, 5, 9, 8, 3, 9)
       V2(7, 5, 9, 8, 2, 8)
       V2(7, 5, 9, 8, 1, 7)
+      // the other split, l1 = 8 (pass A over 256-point columns, pass B over 128-point blocks)
+      V2(8, 4, 9, 7, 5, 9)
+      V2(8, 4, 8, 7, 5, 9)
+      V2(8, 3, 8, 7, 5, 9)
+      V2(8, 5, 10, 7, 5, 9)
+      V2(8, 4, 9, 7, 4, 9)
+      V2(8, 4, 9, 7, 6, 10)
     } else {
       V2(8, 4, 8, 8, 4, 8)
       V2(8, 3, 8, 8, 3, 8)
