@@ -27,7 +27,9 @@ hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream
     return hipErrorInvalidValue;
   p.fid = fid;
   p.log_n = log_n;
-  p.l1 = log_n / 2;
+  // Ft63 at 2^15 (the PoS default n_cols): the l1 = 8 split measured 5 % faster than l1 = 7
+  // (tools/microbench/nttbench.hip mode 5, 9363 rows); every other shape splits evenly.
+  p.l1 = fid == 0 && log_n == 15 ? 8 : log_n / 2;
   p.l2 = log_n - p.l1;
   const size_t n = (size_t)1 << log_n;
   hipError_t e = hipMalloc(&p.d_tw, n * field_bytes(fid));

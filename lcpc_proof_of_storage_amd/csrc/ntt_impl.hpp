@@ -160,8 +160,7 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
   constexpr int R = Shape<F>::R, E = Shape<F>::E;
   const bool halfz = 2 * nv <= ((size_t)1 << p.log_n);
   constexpr int HI = F::N >= 8 ? 11 : 12;  // LDS budget of 32-byte fields
-  hipError_t e = dispatch_logs<F, 6, HI>(p.l1, [&]<int L>() {
-    constexpr int CW = log_cw<L, E>();
+  auto pass_a = [&]<int L, int CW>() {
     constexpr int T = L + CW - R;
     const uint32_t *tc = p.d_tw_canon;
     if (halfz && canon)
@@ -171,7 +170,18 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
     if (canon)
       return ntt_v2::launch_a<F, L, CW, T, false, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, tc);
     return ntt_v2::launch_a<F, L, CW, T, false>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs);
-  });
+  };
+  hipError_t e;
+  if constexpr (F::ID == 0) {
+    // PoS default dims (n_cols = 2^15, ntt_plan_init's l1 = 8): pass A over 32 columns of
+    // 256-point DIFs in 1024 threads (tools/microbench/nttbench.hip mode 5, fastest split).
+    if (p.log_n == 15 && p.l1 == 8)
+      e = pass_a.template operator()<8, 5>();
+    else
+      e = dispatch_logs<F, 6, HI>(p.l1, [&]<int L>() { return pass_a.template operator()<L, log_cw<L, E>()>(); });
+  } else {
+    e = dispatch_logs<F, 6, HI>(p.l1, [&]<int L>() { return pass_a.template operator()<L, log_cw<L, E>()>(); });
+  }
   if (e != hipSuccess) return e;
   return dispatch_logs<F, 7, HI>(p.l2, [&]<int L>() {
     constexpr int CW = log_cw<L, E>();

@@ -34,7 +34,7 @@ def test_encode_matches_fffft(gpu, oracle, fid, log_n):
 
 
 @pytest.mark.parametrize("fid", [0, 1])
-@pytest.mark.parametrize("log_n", [13, 14, 16])
+@pytest.mark.parametrize("log_n", [13, 14, 15, 16])
 def test_encode_full_rows(gpu, oracle, fid, log_n):
     """Full-length (no zero padding) batched rows."""
     n = 1 << log_n
