@@ -110,6 +110,15 @@ void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
       V2(8, 5, 10, 7, 5, 9)
       V2(8, 4, 9, 7, 4, 9)
       V2(8, 4, 9, 7, 6, 10)
+    } else if (log_n == 17) {  // PoS bench dims 65536 -> 131072: product l1 = 8 first, then l1 = 9
+      V2(8, 4, 9, 9, 3, 9)
+      V2(8, 5, 10, 9, 3, 9)
+      V2(8, 4, 9, 9, 2, 8)
+      V2(9, 3, 9, 8, 4, 9)
+      V2(9, 3, 9, 8, 5, 10)
+      V2(9, 2, 8, 8, 4, 9)
+      V2(9, 4, 10, 8, 4, 9)
+      V2(9, 3, 9, 8, 3, 8)
     } else {
       V2(8, 4, 8, 8, 4, 8)
       V2(8, 3, 8, 8, 3, 8)
@@ -163,6 +172,7 @@ int main(int argc, char **argv) {
   if (which == 1) { bench<Ft127>("Ft127", 16, 512); bench<Ft127>("Ft127", 14, 128); }
   if (which == 0) bench<Ft63>("Ft63", 16, 512);
   if (which == 5) bench<Ft63>("Ft63 PoS 1 GiB (copy)", 15, 9363, true);
+  if (which == 7) bench<Ft63>("Ft63 PoS bench dims (copy)", 17, 2341, true);
   if (which == 3) bench<Ft255>("Ft255", 17, 256);
   return 0;
 }
