@@ -489,13 +489,39 @@ class LcEvalProof:
             res.append(LcColumn(col, [pb[32 * i:32 * i + 32] for i in range(self.path_len)]))
         return res
 
+    @staticmethod
+    def _check_shapes(field: int, p_eval, p_random_vec, col_lens, path_lens, digest_lens):
+        """A proof from untrusted bytes must be rectangular before its flat buffers reach
+        lcpc_proof_from_parts (which copies n_col_opens x n_rows elements, etc.).  The reference
+        cannot even represent a digest that is not 32 bytes (Output<Blake3> is a fixed array:
+        bincode rejects it); a ragged proof it does represent fails verify (lib.rs:862-982) --
+        a short column changes the tensor dot product (ColumnDegree), a long column or a wrong
+        path length changes the recomputed root (ColumnPath), a p_random of another length
+        changes the absorbed transcript (ColumnDegree).  (A wrong NUMBER of p_random vectors,
+        which panics at lib.rs:914 when too few, is rejected by lcpc_verify as EncodingDims.)"""
+        n_per_row = _elems(p_eval, field).shape[0]
+        if any(int(d) != 32 for d in digest_lens):
+            raise LcpcError(30, "malformed proof: a Merkle digest is not 32 bytes")
+        if any(_elems(x, field).shape[0] != n_per_row for x in p_random_vec):
+            raise VerifierError(13, "malformed proof: p_random length differs from p_eval")
+        if col_lens:
+            n_rows = col_lens[0]
+            if any(n < n_rows for n in col_lens):
+                raise VerifierError(13, "malformed proof: ragged columns")
+            if any(n > n_rows for n in col_lens):
+                raise VerifierError(11, "malformed proof: ragged columns")
+            if any(pl != path_lens[0] for pl in path_lens):
+                raise VerifierError(11, "malformed proof: Merkle paths of different lengths")
+
     @classmethod
     def from_parts(cls, field: int, n_cols: int, p_eval, p_random_vec, columns: List[LcColumn]):
         nl = limbs(field)
+        cls._check_shapes(field, p_eval, p_random_vec, [_elems(c.col, field).shape[0] for c in columns],
+                          [len(c.path) for c in columns], [len(d) for c in columns for d in c.path])
         pe = _elems(p_eval, field)
         pr = np.ascontiguousarray(np.concatenate([_elems(x, field) for x in p_random_vec]) if p_random_vec
                                   else np.zeros((1, nl), np.uint64))
-        n_rows = columns[0].col.shape[0] if columns else 0
+        n_rows = _elems(columns[0].col, field).shape[0] if columns else 0
         path_len = len(columns[0].path) if columns else 0
         cols = np.ascontiguousarray(np.concatenate([_elems(c.col, field) for c in columns]) if columns
                                     else np.zeros((1, nl), np.uint64))
@@ -577,6 +603,7 @@ class LcEvalProof:
         """from_parts with the columns as one (n_col_opens, n_rows, limbs) array and the paths
         as one (n_col_opens, path_len, 32) byte array."""
         nl = limbs(field)
+        cls._check_shapes(field, p_eval, p_random_vec, [], [], [])
         pe = _elems(p_eval, field)
         pr = np.ascontiguousarray(np.concatenate([_elems(x, field) for x in p_random_vec]) if p_random_vec
                                   else np.zeros((1, nl), np.uint64))
@@ -584,6 +611,10 @@ class LcEvalProof:
         paths = np.ascontiguousarray(paths, dtype=np.uint8)
         nco, n_rows = cols.shape[0], (cols.shape[1] if cols.ndim > 1 else 0)
         path_len = paths.shape[1] if paths.ndim > 1 else 0
+        if nco and (cols.ndim != 3 or cols.shape[2] != nl):
+            raise LcpcError(30, f"columns must be (n_col_opens, n_rows, {nl}) limbs")
+        if nco and (paths.shape[0] != nco or (path_len and (paths.ndim != 3 or paths.shape[2] != 32))):
+            raise LcpcError(30, "paths must be (n_col_opens, path_len, 32) bytes")
         if nco == 0:
             cols = np.zeros((1, nl), np.uint64)
             paths = np.zeros(1, np.uint8)

@@ -231,6 +231,11 @@ def client_online_verify_column_paths_without_full_columns(
     plen = len(received_column_paths[0])
     if any(len(p) != plen for p in received_column_paths):
         raise _verifier_error("ColumnEval", "path lengths differ")
+    # untrusted server data: every digest is exactly one BLAKE3 output (the reference's
+    # Output<Blake3> is a fixed 32-byte array, so anything else never deserializes)
+    if any(len(d) != 32 for d in received_columns_digests[:n]) or \
+            any(len(d) != 32 for p in received_column_paths for d in p):
+        raise _verifier_error("ColumnEval", "digest is not 32 bytes")
     leaves = np.frombuffer(b"".join(received_columns_digests[:n]), np.uint8).copy()
     paths = np.frombuffer(b"".join(b"".join(p) for p in received_column_paths) or b"\0", np.uint8).copy()
     idx = np.ascontiguousarray(np.array(requested_columns, dtype=np.uint64))

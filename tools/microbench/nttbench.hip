@@ -1,6 +1,6 @@
 // nttbench.hip -- A/B harness for NTT pass variants on gfx950 (one process, interleaved
-// rounds; outputs checked bit-for-bit against the v1 kernels, which the GPU parity tests pin
-// to the CPU oracle).  Usage: ./nttbench [log_n] [rows]
+// rounds; outputs checked bit-for-bit against the product kernels, which the GPU parity tests
+// pin to the CPU oracle).  Usage: ./nttbench [log_n] [rows]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -10,7 +10,7 @@
 #include <string>
 #include <vector>
 
-#include "ntt_v1.hpp"
+#include "../../lcpc_proof_of_storage_amd/csrc/ntt_impl.hpp"
 
 using namespace lcpc;
 
@@ -55,15 +55,12 @@ void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
   plan.fid = F::ID; plan.log_n = log_n; plan.l1 = log_n / 2; plan.l2 = log_n - plan.l1; plan.d_tw = tw;
   hipStream_t s;
   CK(hipStreamCreate(&s));
-  CK(ntt_v1::ntt_rows_v1<F>(plan, coeffs, np, np, ref, n, rows, s));
+  CK(ntt_detail::ntt_rows_t<F>(plan, coeffs, np, np, ref, n, rows, s, nullptr, 0, false));
   CK(hipStreamSynchronize(s));
 
   std::vector<Variant> vs;
   vs.push_back({"product (ntt_rows_t)", [&](const uint32_t *c, uint32_t *o, hipStream_t st) {
                   CK(ntt_detail::ntt_rows_t<F>(plan, c, np, np, o, n, rows, st, nullptr, 0, false));
-                }});
-  vs.push_back({"v1 (256thr, 3 LDS trips)", [&](const uint32_t *c, uint32_t *o, hipStream_t st) {
-                  CK(ntt_v1::ntt_rows_v1<F>(plan, c, np, np, o, n, rows, st));
                 }});
 #define V2(LA, CWA, TA, LB, CWB, TB)                                                           \
   vs.push_back({"v2 A(S=2^" #LA ",CW=2^" #CWA ",T=2^" #TA ") B(S=2^" #LB ",CW=2^" #CWB ",T=2^" #TB ")", \
