@@ -6,388 +6,13 @@
 // across PCIe, and runs the inherently serial Fiat-Shamir steps (transcript.cpp).
 // There is no CPU fallback: with no usable HIP device every compute entry point fails with
 // LCPC_ERR_NO_DEVICE.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <atomic>
-#include <cstdlib>
-#include <cmath>
-#include <cstring>
-#include <map>
-#include <memory>
-#include <mutex>
-#include <string>
-#include <thread>
-#include <vector>
-
-#include "../../include/lcpc_mi.h"
-#include "field.hpp"
-#include "kernels.hpp"
-#include "pos.hpp"
-#include "prof.hpp"
-#include "sdig.hpp"
-#include "transcript.hpp"
+#include "host_internal.hpp"
 
 using namespace lcpc;
-
-namespace {
-
-thread_local std::string g_err;
-thread_local int g_device = 0;
-
-lcpc_status fail(lcpc_status st, const std::string &msg) {
-  g_err = msg;
-  return st;
-}
-
-#define HIP_TRY(expr)                                                                  \
-  do {                                                                                 \
-    hipError_t e__ = (expr);                                                           \
-    if (e__ != hipSuccess)                                                             \
-      return fail(e__ == hipErrorOutOfMemory ? LCPC_ERR_OUT_OF_MEMORY : LCPC_ERR_DEVICE, \
-                  std::string(#expr) + ": " + hipGetErrorString(e__));               \
-  } while (0)
-
-const uint8_t LABEL_DT[] = {'$', 'l', '/', '/', 'D', 'T'};  // lcpc-2d/src/macros.rs:29-36:
-const uint8_t LABEL_PR[] = {'$', 'l', '/', '/', 'P', 'R'};  // b"$l//DT" is a byte-string
-const uint8_t LABEL_PE[] = {'$', 'l', '/', '/', 'P', 'E'};  // literal, which macro_rules!
-const uint8_t LABEL_CO[] = {'$', 'l', '/', '/', 'C', 'O'};  // never substitutes into.
-
-struct FieldInfo {
-  int limbs, num_bits, s;
-  uint64_t p[4];
-};
-
-FieldInfo field_info(int fid) {
-  return dispatch_field(fid, []<class F>() {
-    FieldInfo fi{};
-    fi.limbs = F::N / 2;
-    fi.num_bits = F::NUM_BITS;
-    fi.s = F::S;
-    for (int i = 0; i < F::N / 2; i++)
-      fi.p[i] = (uint64_t)F::P[2 * i] | ((uint64_t)F::P[2 * i + 1] << 32);
-    return fi;
-  });
-}
-
-bool valid_field(int f) { return f >= 0 && f <= 4; }
-
-// ---------------------------------------------------------------- per-device context
-// A pool of HIP streams and a caching allocator per device.  Every API call leases its own
-// stream, so independent commitments run concurrently (their CPU-side Fiat-Shamir work
-// overlaps another commitment's kernels); only pool bookkeeping is locked.
-struct Device {
-  int id = 0;
-  bool ok = false;
-  std::string init_err;
-  std::mutex mu;  // guards the pools below
-  std::vector<hipStream_t> idle_streams[2];  // [0] bulk (commit / encode), [1] high priority
-  std::multimap<size_t, void *> free_blocks;  // size -> block
-  std::map<void *, size_t> sizes;
-
-  // high-priority streams carry the prover's short latency-critical kernels (row
-  // combinations, conversions, gathers) ahead of other commitments' bulk encode work
-  hipStream_t shared_stream = nullptr;  // LCPC_STREAM_MODE=serial: every call on one stream
-
-  static bool serial_mode() {
-    static const bool v = [] {
-      const char *m = getenv("LCPC_STREAM_MODE");
-      return m && std::string(m) == "serial";
-    }();
-    return v;
-  }
-
-  hipStream_t acquire_stream(bool high) {
-    if (serial_mode()) {
-      std::lock_guard<std::mutex> lk(mu);
-      if (!shared_stream) {
-        (void)hipSetDevice(id);
-        if (hipStreamCreateWithFlags(&shared_stream, hipStreamNonBlocking) != hipSuccess)
-          shared_stream = nullptr;
-      }
-      return shared_stream;
-    }
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      auto &pool = idle_streams[high ? 1 : 0];
-      if (!pool.empty()) {
-        hipStream_t s = pool.back();
-        pool.pop_back();
-        return s;
-      }
-    }
-    hipStream_t s = nullptr;
-    (void)hipSetDevice(id);
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = lo = 0;
-    static const bool prio = [] {
-      const char *v = getenv("LCPC_PRIORITY_STREAMS");
-      return !(v && v[0] == '0');
-    }();
-    if (!prio) hi = lo;
-    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? hi : lo) != hipSuccess) return nullptr;
-    return s;
-  }
-  void release_stream(hipStream_t s, bool high) {
-    if (serial_mode()) return;
-    std::lock_guard<std::mutex> lk(mu);
-    idle_streams[high ? 1 : 0].push_back(s);
-  }
-  hipError_t alloc(void **p, size_t bytes) {
-    if (bytes == 0) bytes = 16;
-    bytes = (bytes + 255) & ~(size_t)255;
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      auto it = free_blocks.find(bytes);
-      if (it != free_blocks.end()) {
-        *p = it->second;
-        free_blocks.erase(it);
-        return hipSuccess;
-      }
-    }
-    hipError_t e = hipMalloc(p, bytes);
-    if (e == hipErrorOutOfMemory) {
-      (void)hipGetLastError();
-      trim();
-      e = hipMalloc(p, bytes);
-    }
-    if (e == hipSuccess) {
-      std::lock_guard<std::mutex> lk(mu);
-      sizes[*p] = bytes;
-    }
-    return e;
-  }
-  // the caller guarantees no queued work still uses p
-  void release(void *p) {
-    if (!p) return;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = sizes.find(p);
-    if (it == sizes.end()) return;
-    free_blocks.emplace(it->second, p);
-  }
-  // page-locked host blocks for the file paths' staging (pinning is slow: blocks are reused)
-  std::multimap<size_t, void *> pinned_free;
-  std::map<void *, size_t> pinned_sizes;
-  void *pinned_get(size_t bytes) {
-    bytes = std::max<size_t>(bytes, 4096);
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      auto it = pinned_free.lower_bound(bytes);
-      if (it != pinned_free.end() && it->first <= 2 * bytes) {
-        void *p = it->second;
-        pinned_free.erase(it);
-        return p;
-      }
-    }
-    const size_t want = (bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
-    void *p = nullptr;
-    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    pinned_sizes[p] = want;
-    return p;
-  }
-  void pinned_put(void *p) {
-    if (!p) return;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = pinned_sizes.find(p);
-    if (it != pinned_sizes.end()) pinned_free.emplace(it->second, p);
-  }
-  void trim() {
-    (void)hipDeviceSynchronize();
-    std::lock_guard<std::mutex> lk(mu);
-    for (auto &kv : free_blocks) {
-      sizes.erase(kv.second);
-      (void)hipFree(kv.second);
-    }
-    free_blocks.clear();
-  }
-};
-
-std::mutex g_devices_mu;
-std::map<int, std::unique_ptr<Device>> g_devices;
-
-Device *get_device(int id, lcpc_status *st) {
-  std::lock_guard<std::mutex> lk(g_devices_mu);
-  auto &slot = g_devices[id];
-  if (!slot) {
-    slot = std::make_unique<Device>();
-    slot->id = id;
-    int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
-    if (e != hipSuccess || n <= id) {
-      slot->init_err = "no HIP device available (liblcpc_mi has no CPU fallback)";
-    } else if ((e = hipSetDevice(id)) != hipSuccess) {
-      slot->init_err = std::string("HIP init failed: ") + hipGetErrorString(e);
-    } else {
-      slot->ok = true;
-    }
-  }
-  if (!slot->ok) {
-    *st = fail(LCPC_ERR_NO_DEVICE, slot->init_err);
-    return nullptr;
-  }
-  *st = LCPC_OK;
-  return slot.get();
-}
-
-thread_local hipStream_t t_stream = nullptr;  // stream of the innermost live Lease
-
-// A stream leased for the duration of one API call (also makes the device current).
-struct Lease {
-  Device *d;
-  hipStream_t s;
-  hipStream_t prev;
-  bool high;
-  explicit Lease(Device *dev, bool high_priority = false)
-      : d(dev), s(nullptr), prev(t_stream), high(high_priority) {
-    (void)hipSetDevice(dev->id);
-    s = dev->acquire_stream(high);
-    t_stream = s;
-  }
-  ~Lease() {
-    if (s) {
-      (void)hipStreamSynchronize(s);
-      d->release_stream(s, high);
-    }
-    t_stream = prev;
-  }
-  Lease(const Lease &) = delete;
-  Lease &operator=(const Lease &) = delete;
-};
-
-// RAII device buffer from the pool.  It remembers the stream it was allocated for and
-// drains that stream before returning the block (error paths leave work queued).
-struct DBuf {
-  Device *d = nullptr;
-  void *p = nullptr;
-  size_t n = 0;
-  hipStream_t s = nullptr;
-  DBuf() = default;
-  DBuf(const DBuf &) = delete;
-  DBuf &operator=(const DBuf &) = delete;
-  DBuf(DBuf &&o) noexcept : d(o.d), p(o.p), n(o.n), s(o.s) { o.p = nullptr; }
-  DBuf &operator=(DBuf &&o) noexcept {
-    reset();
-    d = o.d; p = o.p; n = o.n; s = o.s; o.p = nullptr;
-    return *this;
-  }
-  ~DBuf() { reset(); }
-  void reset() {
-    if (p && d) {
-      if (s) (void)hipStreamSynchronize(s);
-      d->release(p);
-    }
-    p = nullptr;
-  }
-  // the queued work using this buffer has completed (no drain needed at release)
-  void settle() { s = nullptr; }
-  hipError_t alloc(Device *dev, size_t bytes) {
-    reset();
-    d = dev;
-    n = bytes;
-    s = t_stream;
-    return dev->alloc(&p, bytes);
-  }
-  template <class T>
-  T *as() const { return reinterpret_cast<T *>(p); }
-};
-
-// Thread-local pinned (page-locked) host staging buffers: device<->host copies of proof-sized
-// vectors go through these so they are true async DMA (pageable copies are staged and
-// serialize concurrent commitments).  Slots are grown on demand and reused across calls.
-struct PinnedSlot {
-  void *p = nullptr;
-  size_t cap = 0;
-  ~PinnedSlot() {
-    if (p) (void)hipHostFree(p);
-  }
-  void *get(size_t n) {
-    if (n > cap) {
-      if (p) (void)hipHostFree(p);
-      p = nullptr;
-      cap = 0;
-      size_t want = n < 4096 ? 4096 : n + n / 4;
-      if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
-      cap = want;
-    }
-    return p;
-  }
-};
-enum { PIN_REPR = 0, PIN_PRANDOM, PIN_PEVAL, PIN_COLS, PIN_PATHS, PIN_TENSOR, PIN_OUTER, PIN_N };
-thread_local PinnedSlot t_pin[PIN_N];
-
-size_t next_pow2(size_t v) {
-  size_t p = 1;
-  while (p < v) p <<= 1;
-  return p;
-}
-size_t log2_np2(size_t v) {  // lcpc-2d log2 (:857-859)
-  size_t p = next_pow2(v), l = 0;
-  while (((size_t)1 << l) < p) l++;
-  return l;
-}
-
-}  // namespace
-
-// ---------------------------------------------------------------- handles
-enum { KIND_RS = 0, KIND_SDIG = 1 };
-
-struct lcpc_encoding {
-  int fid = 1;
-  int kind = KIND_RS;  // R-S / fft_io (Ligero) or SDIG expander code (Brakedown)
-  int code = 0;        // SdigCode id
-  uint64_t seed = 0;
-  size_t n_per_row = 0, n_cols = 0, n_col_opens = 0, n_degree_tests = 0;
-  Device *dev = nullptr;
-  NttPlan plan;
-  SdigPlan sdig;
-  ~lcpc_encoding() {
-    if (dev) {
-      Lease lease(dev);
-      (void)hipSetDevice(dev->id);
-      (void)hipStreamSynchronize(lease.s);
-      ntt_plan_free(plan);
-      sdig_plan_free(sdig);
-    }
-  }
-};
-
-struct lcpc_commit {
-  int fid = 1;
-  Device *dev = nullptr;
-  size_t n_rows = 0, n_cols = 0, n_per_row = 0, n_hashes = 0;
-  bool col_major = false;  // comm stored [n_cols][n_rows] (SDIG) instead of [n_rows][n_cols]
-  bool canon = false;      // comm holds canonical values (R-S: ntt_rows canon_out), not Montgomery
-  DBuf coeffs, comm, hashes;
-  uint8_t root[32];
-};
-
-struct lcpc_proof {
-  int fid = 1;
-  size_t n_cols = 0, n_per_row = 0, n_rows = 0, ndt = 0, nco = 0, path_len = 0;
-  std::vector<uint64_t> p_eval, p_random, cols, col_idx;
-  std::vector<uint8_t> paths;
-};
-
-struct lcpc_transcript {
-  Transcript t;
-  explicit lcpc_transcript(const uint8_t *l, size_t n) : t(l, n) {}
-};
+using namespace lcpc_host;
 
 // ---------------------------------------------------------------- internal helpers
 namespace {
-
-lcpc_status encoding_dims_ok(const lcpc_encoding *e, size_t n_per_row, size_t n_cols) {
-  if (e->kind == KIND_SDIG)  // SdigEncodingS::dims_ok (lcpc-brakedown-pc/src/lib.rs:157-164)
-    return (n_per_row < n_cols && n_per_row == e->n_per_row && n_cols == e->n_cols)
-               ? LCPC_OK
-               : LCPC_ERR_INVALID_ARG;
-  // LigeroEncodingRho::dims_ok (lcpc-ligero-pc/src/lib.rs:171-177)
-  const bool pow = n_cols && !(n_cols & (n_cols - 1));
-  return (n_per_row < n_cols && pow && n_per_row == e->n_per_row && n_cols == e->n_cols) ? LCPC_OK
-                                                                                       : LCPC_ERR_INVALID_ARG;
-}
-
 lcpc_status make_rs_encoding(int fid, size_t n_per_row, size_t n_cols, size_t nco, size_t ndt,
                              lcpc_encoding **out) {
   if (!out) return fail(LCPC_ERR_INVALID_ARG, "null out");
@@ -456,74 +81,6 @@ lcpc_status make_sdig_encoding(int fid, int code, size_t n_per_row, size_t want_
   e->dev = dev;
   *out = e.release();
   return LCPC_OK;
-}
-
-// Encode n_rows row-major rows: row r reads n_valid leading coefficients at src + r * ss (the
-// rest of its message zero) and writes n_cols elements at dst + r * ds.  Runs on stream s
-// (normally the caller's lease); scratch comes from the pool.
-lcpc_status encode_rows_any(const lcpc_encoding *e, const uint32_t *src, size_t ss, size_t nv,
-                            uint32_t *dst, size_t ds, size_t n_rows, hipStream_t s) {
-  if (n_rows == 0) return LCPC_OK;
-  if (e->kind == KIND_RS) {
-    HIP_TRY(ntt_rows(e->plan, src, ss, nv, dst, ds, n_rows, s));
-    return LCPC_OK;
-  }
-  // SDIG: element-major working codeword, then back to rows
-  const size_t nc = e->n_cols, np = e->n_per_row;
-  const int wb = field_bytes(e->fid);
-  DBuf cw, tmp;
-  HIP_TRY(cw.alloc(e->dev, nc * n_rows * wb));
-  HIP_TRY(tmp.alloc(e->dev, e->sdig.tmp_elems * n_rows * wb));
-  HIP_TRY(transpose_elems(e->fid, src, n_rows, np, ss, nv < np ? nv : np, cw.as<uint32_t>(), n_rows, s));
-  HIP_TRY(sdig_encode_cm(e->sdig, cw.as<uint32_t>(), n_rows, tmp.as<uint32_t>(), s));
-  HIP_TRY(transpose_elems(e->fid, cw.as<uint32_t>(), nc, n_rows, n_rows, n_rows, dst, ds, s));
-  HIP_TRY(hipStreamSynchronize(s));  // before the pool reuses cw / tmp
-  return LCPC_OK;
-}
-
-// upload host -> device (pool buffer)
-lcpc_status upload(Device *dev, DBuf &b, const void *h, size_t bytes) {
-  HIP_TRY(b.alloc(dev, bytes));
-  if (bytes) HIP_TRY(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, t_stream));
-  return LCPC_OK;
-}
-
-// field elements -> canonical repr bytes (device convert, D2H into a pinned slot, host byte
-// order); *out points into thread-local pinned memory valid until the next call.
-lcpc_status to_repr_host(Device *dev, int fid, const uint32_t *d_elems, size_t n,
-                         const uint8_t **out) {
-  const int wb = field_bytes(fid);
-  DBuf canon;
-  HIP_TRY(canon.alloc(dev, n * wb));
-  HIP_TRY(convert(fid, d_elems, canon.as<uint32_t>(), n, false, t_stream));
-  uint8_t *h = (uint8_t *)t_pin[PIN_REPR].get(n * wb);
-  if (!h) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
-  if (n) HIP_TRY(hipMemcpyAsync(h, canon.p, n * wb, hipMemcpyDeviceToHost, t_stream));
-  HIP_TRY(hipStreamSynchronize(t_stream));
-  if (fid == LCPC_FT253_192) {  // PrimeFieldReprEndianness = "big" (ft253_192.rs:9)
-    for (size_t i = 0; i < n; i++) std::reverse(h + i * wb, h + (i + 1) * wb);
-  }
-  *out = h;
-  return LCPC_OK;
-}
-
-void challenge_tensor(Transcript &tr, int fid, size_t n_rows, std::vector<uint64_t> &out) {
-  // lcpc-2d/src/lib.rs:1056-1062 (prove) / :899-907 (verify)
-  uint8_t key[32];
-  tr.challenge_bytes(LABEL_DT, 6, key, 32);
-  ChaCha20Rng rng(key);
-  const FieldInfo fi = field_info(fid);
-  out.resize(n_rows * fi.limbs);
-  field_random(rng, fi.limbs, fi.num_bits, fi.p, out.data(), n_rows);
-}
-
-void challenge_columns(Transcript &tr, size_t n_cols, size_t nco, std::vector<uint64_t> &idx) {
-  // lcpc-2d/src/lib.rs:1103-1110 (prove) / :932-941 (verify)
-  uint8_t key[32];
-  tr.challenge_bytes(LABEL_CO, 6, key, 32);
-  ChaCha20Rng rng(key);
-  idx.resize(nco);
-  for (size_t i = 0; i < nco; i++) idx[i] = uniform_usize(rng, 0, n_cols);
 }
 
 lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is_host, size_t len,
@@ -608,7 +165,6 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   *out = c.release();
   return LCPC_OK;
 }
-
 }  // namespace
 
 // ================================================================= C ABI
@@ -1205,7 +761,6 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
 }
 
 // ---------------------------------------------------------------- free functions
-static Device *current_device(lcpc_status *st) { return get_device(g_device, st); }
 
 lcpc_status lcpc_collapse_columns(lcpc_field f, const uint64_t *coeffs, const uint64_t *tensor,
                                   uint64_t *poly, size_t n_rows, size_t n_per_row) {
