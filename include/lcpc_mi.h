@@ -407,6 +407,83 @@ lcpc_status lcpc_transcript_append_field_elems(lcpc_transcript *tr, const uint8_
                                                const uint64_t *elems, size_t n);
 lcpc_status lcpc_challenge_columns(lcpc_transcript *tr, size_t n_cols, size_t n, uint64_t *out);
 
+/* ------------------------------------------------------------------ communicators (multi-GPU)
+ * One process per GPU.  A row-sharded commitment (below) moves its chaining values, subtree
+ * digests, challenge vectors, partial row combinations and opened-column pieces through an
+ * lcpc_comm: RCCL over xGMI (librccl.so.1, loaded at first use; every exchange is a device-side
+ * send / recv on device buffers), or collectives the caller supplies (a host transport: the
+ * tests, or several ranks sharing one GPU, which RCCL refuses).  All ranks must make the same
+ * sequence of sharded calls on a comm, one at a time per comm.  Replaces the exchanges that
+ * lcpc-2d's rayon row loop never needed (lcpc-2d/src/lib.rs:677-682 encodes rows in parallel on
+ * one host; here the rows live on several GPUs). */
+typedef struct lcpc_comm lcpc_comm;
+#define LCPC_COMM_UNIQUE_ID_BYTES 128
+/* ncclGetUniqueId: rank 0 makes the id and hands it to the other ranks out of band */
+lcpc_status lcpc_comm_rccl_unique_id(uint8_t id[LCPC_COMM_UNIQUE_ID_BYTES]);
+/* ncclCommInitRank on the calling thread's device (lcpc_set_device); collective */
+lcpc_status lcpc_comm_rccl_new(const uint8_t id[LCPC_COMM_UNIQUE_ID_BYTES], int nranks, int rank,
+                               lcpc_comm **out);
+/* Caller-supplied collectives on DEVICE buffers of the current device.  The library drains the
+ * work producing a buffer before the call and expects the data in place when it returns;
+ * 0 = success.  all_gather: d_recv = the nranks ranks' `bytes`-byte buffers in rank order.
+ * all_to_all_v: d_send holds send_bytes[k] bytes for rank k back to back, d_recv receives
+ * recv_bytes[k] bytes from rank k back to back.  broadcast: root's d_buf to every rank. */
+typedef struct lcpc_comm_ops {
+  void *user;
+  int (*all_gather)(void *user, const void *d_send, void *d_recv, size_t bytes);
+  int (*all_to_all_v)(void *user, const void *d_send, const size_t *send_bytes, void *d_recv,
+                      const size_t *recv_bytes);
+  int (*broadcast)(void *user, void *d_buf, size_t bytes, int root);
+} lcpc_comm_ops;
+lcpc_status lcpc_comm_from_ops(const lcpc_comm_ops *ops, int nranks, int rank, lcpc_comm **out);
+int lcpc_comm_nranks(const lcpc_comm *c);
+int lcpc_comm_rank(const lcpc_comm *c);
+int lcpc_comm_is_rccl(const lcpc_comm *c);
+void lcpc_comm_free(lcpc_comm *c);
+
+/* ------------------------------------------------------------------ row-sharded commitments
+ * One Ligero commitment whose n_rows coefficient rows are split over the comm's ranks
+ * (SURVEY.md §8e), reproducing commit (lcpc-2d/src/lib.rs:651-815) and prove (:1034-1123) bit
+ * for bit.  Rank g encodes rows [row0_g, row0_g + n_g) -- cut on BLAKE3 chunk boundaries of the
+ * leaf message -- and the chaining values of its chunks of every column; an all-to-all by column
+ * block gives rank k the leaves and subtree of block k; an all-gather of the subtrees gives
+ * every rank the whole Merkle tree (the bytes of lcpc_commit_copy_hashes).  prove runs the
+ * Merlin transcript on one `root` rank: it broadcasts each challenge vector, gathers the ranks'
+ * partial row combinations and folds them mod p (RCCL has no mod-p reduction), then gathers the
+ * opened columns' row pieces.  Needs a power-of-two rank count dividing n_cols. */
+/* the rows of rank `rank` */
+lcpc_status lcpc_sharded_rows(lcpc_field f, size_t n_rows, int nranks, int rank, size_t *row0,
+                              size_t *n_shard_rows);
+typedef struct lcpc_sharded_commit lcpc_sharded_commit;
+/* collective: d_rows = this rank's n_shard_rows zero-padded coefficient rows (n_per_row
+ * elements each) in device memory; n_rows = the whole matrix's row count */
+lcpc_status lcpc_sharded_commit_new_device(const lcpc_encoding *e, const void *d_rows, size_t n_rows,
+                                           lcpc_comm *comm, lcpc_sharded_commit **out);
+void lcpc_sharded_commit_free(lcpc_sharded_commit *c);
+lcpc_status lcpc_sharded_commit_get_root(const lcpc_sharded_commit *c, uint8_t root[32]);
+size_t lcpc_sharded_commit_n_hashes(const lcpc_sharded_commit *c);
+lcpc_status lcpc_sharded_commit_copy_hashes(const lcpc_sharded_commit *c, uint8_t *out);
+/* collective prove (:1034-1123): outer = the n_rows-element outer tensor (host, every rank);
+ * on rank `root`, tr is the transcript and *out receives the proof; elsewhere tr is ignored
+ * (may be NULL) and *out is set to NULL */
+lcpc_status lcpc_sharded_prove(lcpc_sharded_commit *c, const uint64_t *outer, size_t outer_len,
+                               const lcpc_encoding *e, lcpc_transcript *tr, int root,
+                               lcpc_proof **out);
+/* Pipelined commit + prove of n_polys row-sharded polynomials (a proof-of-storage server's
+ * objects, the bench's steps): polynomial i reads this rank's rows at d_rows[i] and is proved on
+ * rank i % nranks, whose transcript is make_transcript(user, i, root_i) (the library frees it);
+ * proofs[i] is set there and NULL elsewhere (proofs may be NULL: proofs are dropped), roots
+ * (optional) gets every root on every rank.  Up to `depth` polynomials are in flight; the
+ * exchanges of different polynomials go out in one fixed order on every rank (one RCCL group per
+ * pipeline tick), `lag` ticks apart wherever the root rank absorbs a row combination into its
+ * transcript (0: automatic). */
+typedef lcpc_transcript *(*lcpc_make_transcript_fn)(void *user, size_t i, const uint8_t root[32]);
+lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *const *d_rows,
+                                           size_t n_polys, size_t n_rows, const uint64_t *outer,
+                                           lcpc_comm *comm, lcpc_make_transcript_fn make_transcript,
+                                           void *user, size_t lag, lcpc_proof **proofs,
+                                           uint8_t *roots);
+
 /* ------------------------------------------------------------------ kernel timing
  * HIP-event timing of every kernel launch on the handle streams (off by default). */
 void lcpc_prof_enable(int enable);

@@ -25,6 +25,19 @@ vp = C.c_void_p
 sz = C.c_size_t
 i32 = C.c_int
 
+# caller-supplied collectives of lcpc_comm_from_ops and the transcript factory of
+# lcpc_sharded_commit_prove_many (include/lcpc_mi.h)
+ALL_GATHER_FN = C.CFUNCTYPE(C.c_int, vp, vp, vp, sz)
+ALL_TO_ALL_V_FN = C.CFUNCTYPE(C.c_int, vp, vp, szp, vp, szp)
+BROADCAST_FN = C.CFUNCTYPE(C.c_int, vp, vp, sz, C.c_int)
+MAKE_TRANSCRIPT_FN = C.CFUNCTYPE(vp, vp, sz, u8p)
+
+
+class CommOps(C.Structure):
+    _fields_ = [("user", vp), ("all_gather", ALL_GATHER_FN), ("all_to_all_v", ALL_TO_ALL_V_FN),
+                ("broadcast", BROADCAST_FN)]
+
+
 # name: (restype, argtypes)
 SIGNATURES = {
     "lcpc_abi_version": (i32, []),
@@ -143,6 +156,22 @@ SIGNATURES = {
     "lcpc_challenge_tensor": (i32, [vp, i32, sz, u64p]),
     "lcpc_transcript_append_field_elems": (i32, [vp, u8p, sz, i32, u64p, sz]),
     "lcpc_challenge_columns": (i32, [vp, sz, sz, u64p]),
+    "lcpc_comm_rccl_unique_id": (i32, [u8p]),
+    "lcpc_comm_rccl_new": (i32, [u8p, i32, i32, C.POINTER(vp)]),
+    "lcpc_comm_from_ops": (i32, [C.POINTER(CommOps), i32, i32, C.POINTER(vp)]),
+    "lcpc_comm_nranks": (i32, [vp]),
+    "lcpc_comm_rank": (i32, [vp]),
+    "lcpc_comm_is_rccl": (i32, [vp]),
+    "lcpc_comm_free": (None, [vp]),
+    "lcpc_sharded_rows": (i32, [i32, sz, i32, i32, szp, szp]),
+    "lcpc_sharded_commit_new_device": (i32, [vp, vp, sz, vp, C.POINTER(vp)]),
+    "lcpc_sharded_commit_free": (None, [vp]),
+    "lcpc_sharded_commit_get_root": (i32, [vp, u8p]),
+    "lcpc_sharded_commit_n_hashes": (sz, [vp]),
+    "lcpc_sharded_commit_copy_hashes": (i32, [vp, u8p]),
+    "lcpc_sharded_prove": (i32, [vp, u64p, sz, vp, vp, i32, C.POINTER(vp)]),
+    "lcpc_sharded_commit_prove_many": (i32, [vp, C.POINTER(vp), sz, sz, u64p, vp, MAKE_TRANSCRIPT_FN, vp, sz,
+                                             C.POINTER(vp), u8p]),
     "lcpc_prof_enable": (None, [i32]),
     "lcpc_prof_reset": (None, []),
     "lcpc_prof_get": (i32, [C.c_char_p, C.POINTER(C.c_double), u64p]),

@@ -1,0 +1,1041 @@
+// shard_native.cpp -- row-sharded Ligero commit / prove across GPUs behind the C ABI
+// (include/lcpc_mi.h, "communicators" and "row-sharded commitments").
+//
+// One process per GPU.  A commitment's n_rows rows are cut at BLAKE3 chunk boundaries of the
+// leaf message (32 zero bytes || column, lcpc-2d/src/lib.rs:736-775), so rank g can encode its
+// rows and compute the chaining values of its chunks of every column by itself.  The exchanges
+// (all on device buffers; with RCCL they are device-side sends / receives over xGMI):
+//   commit (lib.rs:651-815)
+//     A  all-to-all by column block: rank k receives every rank's chaining values of block k
+//        (at cfg3 x 8 GPUs 2.4 MB per rank, instead of the 64 MiB codeword shard), merges them
+//        into the block's leaves and builds the block's subtree;
+//     B  all-gather of the subtrees: every rank assembles the whole tree (the bytes the
+//        single-GPU commit holds) and the root;
+//   prove (lib.rs:1034-1123), the Merlin transcript on one root rank
+//     BC_r  broadcast of degree-test tensor r (then the column indices) from the root,
+//     G_r   gather of the partial row combinations to the root, which folds them mod p and
+//           absorbs the sum (RCCL has no mod-p reduction),
+//     G_c   gather of the opened columns' row pieces; the root reads the paths off its tree.
+// Every step's exchanges are one op kind of a generic "exchange group"; the pipelined driver
+// (lcpc_sharded_commit_prove_many) puts the ops of several polynomials in flight into one group
+// per tick, in a schedule fixed at launch so that every rank issues identical groups in identical
+// order on one comm stream (RCCL ops that wait on peers therefore never deadlock against each
+// other), while each polynomial's compute runs on its own stream and the root ranks' transcript
+// absorption runs on host threads.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <future>
+
+#include "host_internal.hpp"
+
+using namespace lcpc;
+using namespace lcpc_host;
+
+namespace {
+
+// ---------------------------------------------------------------- RCCL, loaded at first use
+// (no link-time dependency: a process that never shards never loads it; a process where torch
+// already loaded its librccl.so.1 shares that copy, same SONAME)
+struct Rccl {
+  bool ok = false;
+  std::string err;
+  decltype(&::ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&::ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&::ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&::ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&::ncclSend) Send = nullptr;
+  decltype(&::ncclRecv) Recv = nullptr;
+  decltype(&::ncclGroupStart) GroupStart = nullptr;
+  decltype(&::ncclGroupEnd) GroupEnd = nullptr;
+};
+
+Rccl &rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    const char *name = getenv("LCPC_RCCL_LIB");
+    void *h = dlopen(name && *name ? name : "librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      x.err = std::string("cannot load librccl.so.1: ") + dlerror();
+      return x;
+    }
+#define SYM(f)                                                   \
+  x.f = reinterpret_cast<decltype(x.f)>(dlsym(h, "nccl" #f));    \
+  if (!x.f) {                                                    \
+    x.err = "librccl.so.1 lacks nccl" #f;                        \
+    return x;                                                    \
+  }
+    SYM(GetUniqueId) SYM(CommInitRank) SYM(CommDestroy) SYM(GetErrorString) SYM(Send) SYM(Recv)
+    SYM(GroupStart) SYM(GroupEnd)
+#undef SYM
+    x.ok = true;
+    return x;
+  }();
+  return r;
+}
+
+#define NCCL_TRY(expr)                                                                   \
+  do {                                                                                   \
+    ncclResult_t r__ = (expr);                                                           \
+    if (r__ != ncclSuccess)                                                              \
+      return fail(LCPC_ERR_DEVICE, std::string(#expr) + ": " + rccl().GetErrorString(r__)); \
+  } while (0)
+
+// ---------------------------------------------------------------- a small host task pool
+// (the root rank's transcript work for several polynomials in flight)
+class TaskPool {
+ public:
+  explicit TaskPool(size_t n) {
+    for (size_t i = 0; i < n; i++) th_.emplace_back([this] { run(); });
+  }
+  ~TaskPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  std::future<lcpc_status> submit(std::function<lcpc_status()> fn) {
+    auto task = std::make_shared<std::packaged_task<lcpc_status()>>(std::move(fn));
+    auto fut = task->get_future();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.emplace_back([task] { (*task)(); });
+    }
+    cv_.notify_one();
+    return fut;
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        job = std::move(q_.front());
+        q_.pop_front();
+      }
+      job();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::deque<std::function<void()>> q_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------- the communicator
+struct lcpc_comm {
+  int nranks = 1, rank = 0;
+  bool is_rccl = false;
+  ncclComm_t nc = nullptr;
+  lcpc_comm_ops ops{};
+  Device *dev = nullptr;
+  hipStream_t cs = nullptr;  // the comm stream: every exchange, in issue order
+  std::mutex mu;             // one sharded call at a time
+  ~lcpc_comm() {
+    if (cs) {
+      (void)hipStreamSynchronize(cs);
+      (void)hipStreamDestroy(cs);
+    }
+    if (nc) rccl().CommDestroy(nc);
+  }
+};
+
+namespace {
+
+// One exchange of a group.  Device buffers; `ready` (optional) marks the device work that
+// produces the send data.
+struct Xop {
+  enum Kind { ALL_GATHER, ALL_TO_ALL, BROADCAST } kind;
+  const uint8_t *send = nullptr;
+  uint8_t *recv = nullptr;  // BROADCAST: the buffer (send data on the root)
+  size_t bytes = 0;         // ALL_GATHER: per rank; BROADCAST: total
+  std::vector<size_t> sb, rb;  // ALL_TO_ALL: bytes to / from each rank
+  int root = 0;
+  hipEvent_t ready = nullptr;
+};
+
+// Issues one group of exchanges on the comm stream; `done` events are recorded after it.
+lcpc_status run_group(lcpc_comm *c, std::vector<Xop> &ops, const std::vector<hipEvent_t> &done) {
+  const int G = c->nranks, me = c->rank;
+  hipStream_t cs = c->cs;
+  if (c->is_rccl || G == 1) {
+    for (auto &op : ops)
+      if (op.ready) HIP_TRY(hipStreamWaitEvent(cs, op.ready, 0));
+    // own pieces: device copies on the comm stream
+    for (auto &op : ops) {
+      if (op.kind == Xop::ALL_GATHER && op.bytes)
+        HIP_TRY(hipMemcpyAsync(op.recv + (size_t)me * op.bytes, op.send, op.bytes, hipMemcpyDeviceToDevice, cs));
+      if (op.kind == Xop::ALL_TO_ALL && op.rb[me]) {
+        size_t so = 0, ro = 0;
+        for (int k = 0; k < me; k++) so += op.sb[k], ro += op.rb[k];
+        HIP_TRY(hipMemcpyAsync(op.recv + ro, op.send + so, op.rb[me], hipMemcpyDeviceToDevice, cs));
+      }
+    }
+    if (G > 1) {
+      Rccl &R = rccl();
+      NCCL_TRY(R.GroupStart());
+      for (auto &op : ops) {
+        switch (op.kind) {
+          case Xop::ALL_GATHER:
+            if (!op.bytes) break;
+            for (int p = 0; p < G; p++) {
+              if (p == me) continue;
+              NCCL_TRY(R.Send(op.send, op.bytes, ncclUint8, p, c->nc, cs));
+              NCCL_TRY(R.Recv(op.recv + (size_t)p * op.bytes, op.bytes, ncclUint8, p, c->nc, cs));
+            }
+            break;
+          case Xop::ALL_TO_ALL: {
+            size_t so = 0, ro = 0;
+            for (int p = 0; p < G; p++) {
+              if (p != me) {
+                if (op.sb[p]) NCCL_TRY(R.Send(op.send + so, op.sb[p], ncclUint8, p, c->nc, cs));
+                if (op.rb[p]) NCCL_TRY(R.Recv(op.recv + ro, op.rb[p], ncclUint8, p, c->nc, cs));
+              }
+              so += op.sb[p];
+              ro += op.rb[p];
+            }
+            break;
+          }
+          case Xop::BROADCAST:
+            if (!op.bytes) break;
+            if (me == op.root) {
+              for (int p = 0; p < G; p++)
+                if (p != me) NCCL_TRY(R.Send(op.recv, op.bytes, ncclUint8, p, c->nc, cs));
+            } else {
+              NCCL_TRY(R.Recv(op.recv, op.bytes, ncclUint8, op.root, c->nc, cs));
+            }
+            break;
+        }
+      }
+      NCCL_TRY(R.GroupEnd());
+    }
+  } else {
+    // caller-supplied collectives: synchronous on drained buffers
+    for (auto &op : ops)
+      if (op.ready) HIP_TRY(hipEventSynchronize(op.ready));
+    HIP_TRY(hipStreamSynchronize(cs));
+    for (auto &op : ops) {
+      int rc = 0;
+      switch (op.kind) {
+        case Xop::ALL_GATHER:
+          rc = c->ops.all_gather(c->ops.user, op.send, op.recv, op.bytes);
+          break;
+        case Xop::ALL_TO_ALL:
+          rc = c->ops.all_to_all_v(c->ops.user, op.send, op.sb.data(), op.recv, op.rb.data());
+          break;
+        case Xop::BROADCAST:
+          rc = c->ops.broadcast(c->ops.user, op.recv, op.bytes, op.root);
+          break;
+      }
+      if (rc) return fail(LCPC_ERR_DEVICE, "caller-supplied collective failed (" + std::to_string(rc) + ")");
+    }
+  }
+  for (hipEvent_t e : done) HIP_TRY(hipEventRecord(e, cs));
+  return LCPC_OK;
+}
+
+// ---------------------------------------------------------------- partition
+struct Part {
+  size_t c_lo, c_hi, r_lo, r_hi;
+};
+
+size_t chunk_first_row(int fid, size_t chunk, size_t n_chunks, size_t n_rows) {
+  if (chunk == 0) return 0;
+  if (chunk >= n_chunks) return n_rows;
+  const size_t wb = (size_t)field_bytes(fid);
+  return std::min(n_rows, (1024 * chunk - 32 + wb - 1) / wb);
+}
+
+std::vector<Part> partition(int fid, size_t n_rows, int G) {
+  const size_t nch = leaf_n_chunks(fid, n_rows);
+  std::vector<Part> p(G);
+  for (int g = 0; g < G; g++) {
+    p[g].c_lo = (size_t)g * nch / G;
+    p[g].c_hi = (size_t)(g + 1) * nch / G;
+    p[g].r_lo = chunk_first_row(fid, p[g].c_lo, nch, n_rows);
+    p[g].r_hi = chunk_first_row(fid, p[g].c_hi, nch, n_rows);
+  }
+  return p;
+}
+
+// pinned host block from the device pool
+struct HostBuf {
+  Device *d = nullptr;
+  uint8_t *p = nullptr;
+  HostBuf() = default;
+  HostBuf(const HostBuf &) = delete;
+  HostBuf &operator=(const HostBuf &) = delete;
+  ~HostBuf() {
+    if (p) d->pinned_put(p);
+  }
+  lcpc_status get(Device *dev, size_t n) {
+    d = dev;
+    p = (uint8_t *)dev->pinned_get(n);
+    return p ? LCPC_OK : fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------- one polynomial's shard state
+struct lcpc_sharded_commit {
+  const lcpc_encoding *e = nullptr;
+  lcpc_comm *comm = nullptr;
+  Device *dev = nullptr;
+  int fid = 1, wb = 16, G = 1, me = 0;
+  size_t n_rows = 0, np = 0, nc = 0, B = 0, n_chunks = 0, nr = 0;
+  std::vector<Part> part;
+  hipStream_t s = nullptr;        // this polynomial's compute stream
+  hipEvent_t ev_ready = nullptr;  // send data of the next exchange written
+  hipEvent_t ev_done = nullptr;   // the last exchange completed (comm stream)
+  hipEvent_t ev_host = nullptr;   // device -> host copies of the last stage landed
+  DBuf coeffs, comm_rows, hashes;  // kept for prove
+  DBuf cv_send, cv_recv, sub, subs;  // commit scratch
+  uint8_t root[32] = {0};
+  // prove state
+  int root_rank = 0;
+  size_t ndt = 0, nco = 0, rounds = 0;
+  lcpc_transcript *tr = nullptr;
+  bool own_tr = false;
+  DBuf bt, tens, part_d, allpart, sum, canon, didx, mycols, allcols, dpaths, scratch;
+  HostBuf h_root, h_t, h_sum, h_repr, h_repr_eval, h_idx, h_cols, h_paths;
+  std::vector<uint64_t> p_random, p_eval, col_idx;
+  std::future<lcpc_status> next;  // root rank: the next challenge vector is in h_t / h_idx
+  ~lcpc_sharded_commit() {
+    if (s) (void)hipStreamSynchronize(s);
+    if (own_tr) delete tr;
+    if (ev_ready) (void)hipEventDestroy(ev_ready);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+    if (ev_host) (void)hipEventDestroy(ev_host);
+    // DBufs drain s in their destructors (declared after s, destroyed before it is released)
+  }
+};
+
+namespace {
+
+void release_stream(lcpc_sharded_commit *c) {
+  if (c->s) {
+    (void)hipStreamSynchronize(c->s);
+    c->dev->release_stream(c->s, false);
+    c->s = nullptr;
+  }
+}
+
+struct ShardDeleter {
+  void operator()(lcpc_sharded_commit *c) const {
+    if (!c) return;
+    hipStream_t s = c->s;
+    Device *d = c->dev;
+    c->s = nullptr;
+    if (s) (void)hipStreamSynchronize(s);
+    delete c;
+    if (s) d->release_stream(s, false);
+  }
+};
+using ShardPtr = std::unique_ptr<lcpc_sharded_commit, ShardDeleter>;
+
+lcpc_status check_shardable(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows) {
+  if (!e || !comm) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (e->kind != KIND_RS) return fail(LCPC_ERR_UNSUPPORTED, "row shards: Ligero / R-S encodings only");
+  const int G = comm->nranks;
+  if (G < 1 || (G & (G - 1)) || e->n_cols % (size_t)G)
+    return fail(LCPC_ERR_UNSUPPORTED, "row shards need a power-of-two rank count dividing n_cols");
+  if (n_rows == 0) return fail(LCPC_ERR_INVALID_ARG, "n_rows");
+  if (comm->dev != e->dev) return fail(LCPC_ERR_INVALID_ARG, "comm and encoding on different devices");
+  return LCPC_OK;
+}
+
+lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, ShardPtr &out) {
+  ShardPtr c(new lcpc_sharded_commit());
+  c->e = e;
+  c->comm = comm;
+  c->dev = e->dev;
+  c->fid = e->fid;
+  c->wb = field_bytes(e->fid);
+  c->G = comm->nranks;
+  c->me = comm->rank;
+  c->n_rows = n_rows;
+  c->np = e->n_per_row;
+  c->nc = e->n_cols;
+  c->B = c->nc / c->G;
+  c->n_chunks = leaf_n_chunks(c->fid, n_rows);
+  c->part = partition(c->fid, n_rows, c->G);
+  c->nr = c->part[c->me].r_hi - c->part[c->me].r_lo;
+  HIP_TRY(hipSetDevice(c->dev->id));
+  c->s = c->dev->acquire_stream(false);
+  if (!c->s) return fail(LCPC_ERR_DEVICE, "no HIP stream");
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_host, hipEventDisableTiming));
+  out = std::move(c);
+  return LCPC_OK;
+}
+
+// DBuf allocations drain the polynomial's stream (not the caller's lease) when released
+hipError_t salloc(lcpc_sharded_commit *c, DBuf &b, size_t bytes) {
+  hipStream_t prev = t_stream;
+  t_stream = c->s;
+  hipError_t e = b.alloc(c->dev, bytes);
+  t_stream = prev;
+  return e;
+}
+
+// ---- commit
+// encode this rank's rows (the first NTT pass writes the commitment's own coefficient copy),
+// chaining values of its chunks of every column, laid out [dest rank][chunk][block col]
+lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
+  const Part &pm = c->part[c->me];
+  const size_t nch = pm.c_hi - pm.c_lo, wb = c->wb;
+  HIP_TRY(salloc(c, c->coeffs, c->nr * c->np * wb + 16));
+  HIP_TRY(salloc(c, c->comm_rows, c->nr * c->nc * wb + 16));
+  HIP_TRY(salloc(c, c->cv_send, nch * c->nc * 32 + 16));
+  HIP_TRY(salloc(c, c->cv_recv, c->n_chunks * c->B * 32 + 16));
+  if (c->nr) {
+    if (!d_rows) return fail(LCPC_ERR_INVALID_ARG, "null rows");
+    HIP_TRY(ntt_rows(c->e->plan, (const uint32_t *)d_rows, c->np, c->np, c->comm_rows.as<uint32_t>(), c->nc, c->nr,
+                     c->s, c->coeffs.as<uint32_t>(), c->np, true));
+  }
+  if (nch) {
+    DBuf cv;
+    HIP_TRY(salloc(c, cv, nch * c->nc * 32));
+    HIP_TRY(leaf_chunk_cvs(c->fid, c->comm_rows.as<uint32_t>(), pm.r_lo, c->n_rows, c->nc, c->nc, pm.c_lo, pm.c_hi,
+                           cv.as<uint32_t>(), c->s, true));
+    // [chunk][G][B] -> [G][chunk][B]
+    const size_t row = c->B * 32;
+    for (int k = 0; k < c->G; k++)
+      HIP_TRY(hipMemcpy2DAsync(c->cv_send.as<uint8_t>() + (size_t)k * nch * row, row, cv.as<uint8_t>() + k * row,
+                               c->nc * 32, row, nch, hipMemcpyDeviceToDevice, c->s));
+  }
+  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  return LCPC_OK;
+}
+
+Xop op_cv_exchange(lcpc_sharded_commit *c) {
+  Xop op{Xop::ALL_TO_ALL};
+  const size_t nch_me = c->part[c->me].c_hi - c->part[c->me].c_lo;
+  op.send = c->cv_send.as<uint8_t>();
+  op.recv = c->cv_recv.as<uint8_t>();
+  op.sb.assign(c->G, nch_me * c->B * 32);
+  op.rb.resize(c->G);
+  for (int k = 0; k < c->G; k++) op.rb[k] = (c->part[k].c_hi - c->part[k].c_lo) * c->B * 32;
+  op.ready = c->ev_ready;
+  return op;
+}
+
+// leaves of my column block from all chunks' chaining values, and the block's subtree
+lcpc_status stage_post_cv(lcpc_sharded_commit *c) {
+  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(salloc(c, c->sub, (2 * c->B - 1) * 32));
+  HIP_TRY(leaves_from_cvs(c->cv_recv.as<uint32_t>(), c->B, (int)c->n_chunks, c->sub.as<uint8_t>(), c->s));
+  if (c->B > 1) HIP_TRY(merkle_tree(c->sub.as<uint8_t>(), c->B, c->s));
+  HIP_TRY(salloc(c, c->subs, (size_t)c->G * (2 * c->B - 1) * 32));
+  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  return LCPC_OK;
+}
+
+Xop op_subtree_exchange(lcpc_sharded_commit *c) {
+  Xop op{Xop::ALL_GATHER};
+  op.send = c->sub.as<uint8_t>();
+  op.recv = c->subs.as<uint8_t>();
+  op.bytes = (2 * c->B - 1) * 32;
+  op.ready = c->ev_ready;
+  return op;
+}
+
+// every rank: the whole tree [leaves | level 1 | ... | root] from the G subtrees + top levels
+lcpc_status stage_post_subtrees(lcpc_sharded_commit *c) {
+  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  const size_t nc = c->nc, B = c->B, G = c->G;
+  HIP_TRY(salloc(c, c->hashes, (2 * nc - 1) * 32));
+  uint8_t *h = c->hashes.as<uint8_t>();
+  for (size_t l = 0; (B >> l) >= 1; l++) {
+    const size_t w = (B >> l) * 32;
+    HIP_TRY(hipMemcpy2DAsync(h + (2 * nc - 2 * (nc >> l)) * 32, w, c->subs.as<uint8_t>() + (2 * B - 2 * (B >> l)) * 32,
+                             (2 * B - 1) * 32, w, G, hipMemcpyDeviceToDevice, c->s));
+    if ((B >> l) == 1) break;
+  }
+  if (G > 1) HIP_TRY(merkle_tree_io(h + (2 * nc - 2 * G) * 32, G, h + (2 * nc - G) * 32, c->s));
+  lcpc_status st = c->h_root.get(c->dev, 32);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(c->h_root.p, h + (2 * nc - 2) * 32, 32, hipMemcpyDeviceToHost, c->s));
+  HIP_TRY(hipEventRecord(c->ev_host, c->s));
+  return LCPC_OK;
+}
+
+// commit scratch no longer needed once the root is known
+lcpc_status finish_commit(lcpc_sharded_commit *c) {
+  HIP_TRY(hipEventSynchronize(c->ev_host));
+  std::memcpy(c->root, c->h_root.p, 32);
+  c->cv_send.reset();
+  c->cv_recv.reset();
+  c->sub.reset();
+  c->subs.reset();
+  return LCPC_OK;
+}
+
+// ---- prove
+lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank, lcpc_transcript *tr,
+                       bool own_tr) {
+  c->root_rank = root_rank;
+  c->ndt = c->e->n_degree_tests;
+  c->nco = c->e->n_col_opens;
+  c->rounds = std::max<size_t>(c->ndt, 1);
+  c->tr = tr;
+  c->own_tr = own_tr;
+  const size_t wb = c->wb, np = c->np;
+  lcpc_status st;
+  HIP_TRY(salloc(c, c->bt, c->n_rows * wb));
+  HIP_TRY(salloc(c, c->tens, 2 * std::max<size_t>(c->nr, 1) * wb));
+  HIP_TRY(salloc(c, c->part_d, 2 * np * wb));
+  HIP_TRY(salloc(c, c->scratch, collapse_scratch_bytes(c->fid, std::max<size_t>(c->nr, 1), np, 2)));
+  HIP_TRY(salloc(c, c->didx, std::max<size_t>(c->nco, 1) * 8));
+  HIP_TRY(salloc(c, c->mycols, std::max<size_t>(c->nco * c->nr, 1) * wb));
+  // the outer tensor's slice (host -> device once per proof)
+  if ((st = c->h_t.get(c->dev, c->n_rows * wb))) return st;
+  if ((st = c->h_idx.get(c->dev, std::max<size_t>(c->nco, 1) * 8))) return st;
+  if (c->nr) {
+    HostBuf h_outer;
+    if ((st = h_outer.get(c->dev, c->nr * wb))) return st;
+    std::memcpy(h_outer.p, (const uint8_t *)outer + c->part[c->me].r_lo * wb, c->nr * wb);
+    HIP_TRY(hipMemcpyAsync(c->tens.as<uint8_t>() + c->nr * wb, h_outer.p, c->nr * wb, hipMemcpyHostToDevice, c->s));
+    HIP_TRY(hipStreamSynchronize(c->s));  // before h_outer returns to the pool
+  }
+  if (c->me == root_rank) {
+    HIP_TRY(salloc(c, c->allpart, (size_t)c->G * 2 * np * wb));
+    HIP_TRY(salloc(c, c->sum, 2 * np * wb));
+    HIP_TRY(salloc(c, c->canon, 2 * np * wb));
+    size_t all_rows = c->n_rows;
+    HIP_TRY(salloc(c, c->allcols, std::max<size_t>(c->nco * all_rows, 1) * wb));
+    HIP_TRY(salloc(c, c->dpaths, std::max<size_t>(c->nco * log2_np2(c->nc), 1) * 32));
+    if ((st = c->h_sum.get(c->dev, 2 * np * wb))) return st;
+    if ((st = c->h_repr.get(c->dev, 2 * np * wb))) return st;
+    if ((st = c->h_repr_eval.get(c->dev, np * wb))) return st;
+    if ((st = c->h_cols.get(c->dev, std::max<size_t>(c->nco * all_rows, 1) * wb))) return st;
+    if ((st = c->h_paths.get(c->dev, std::max<size_t>(c->nco * log2_np2(c->nc), 1) * 32))) return st;
+    c->p_random.resize(c->ndt * np * (wb / 8));
+    c->p_eval.resize(np * (wb / 8));
+  }
+  return LCPC_OK;
+}
+
+// root rank, host: the first challenge (degree-test tensor 0, or the column choice if there
+// are no degree tests and no... -- with n_degree_tests = 0 round 0 is the evaluation alone)
+lcpc_status challenge_first(lcpc_sharded_commit *c) {
+  if (c->ndt) {
+    std::vector<uint64_t> t;
+    challenge_tensor(c->tr->t, c->fid, c->n_rows, t);
+    std::memcpy(c->h_t.p, t.data(), c->n_rows * c->wb);
+  }
+  return LCPC_OK;
+}
+
+int round_tensors(const lcpc_sharded_commit *c, size_t r) { return (r == 0 && c->ndt) ? 2 : 1; }
+
+Xop op_tensor_bcast(lcpc_sharded_commit *c, size_t r) {
+  // round r's challenge vector (round 0 without degree tests has none: a zero-byte broadcast)
+  Xop op{Xop::BROADCAST};
+  op.recv = c->bt.as<uint8_t>();
+  op.bytes = (r < c->ndt) ? c->n_rows * c->wb : 0;
+  op.root = c->root_rank;
+  return op;
+}
+
+// root: the challenge vector onto the comm stream before the exchange group is issued
+lcpc_status stage_tensor_upload(lcpc_sharded_commit *c, size_t r) {
+  if (c->me != c->root_rank || r >= c->ndt) return LCPC_OK;
+  HIP_TRY(hipMemcpyAsync(c->bt.p, c->h_t.p, c->n_rows * c->wb, hipMemcpyHostToDevice, c->comm->cs));
+  return LCPC_OK;
+}
+
+// partial row combinations over my rows: [t_r slice | outer slice] (round 0) or t_r slice
+lcpc_status stage_collapse(lcpc_sharded_commit *c, size_t r) {
+  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  const size_t wb = c->wb, np = c->np, nr = c->nr;
+  const int nt = round_tensors(c, r);
+  const bool eval_only = c->ndt == 0;  // round 0 = the evaluation tensor alone
+  if (nr == 0) {
+    HIP_TRY(hipMemsetAsync(c->part_d.p, 0, nt * np * wb, c->s));
+  } else {
+    const uint32_t *tens = c->tens.as<uint32_t>();
+    if (!eval_only) {
+      HIP_TRY(hipMemcpyAsync(c->tens.p, c->bt.as<uint8_t>() + c->part[c->me].r_lo * wb, nr * wb,
+                             hipMemcpyDeviceToDevice, c->s));
+    } else {
+      tens = (const uint32_t *)(c->tens.as<uint8_t>() + nr * wb);
+    }
+    HIP_TRY(collapse_rows(c->fid, c->coeffs.as<uint32_t>(), nr, np, tens, nt, c->part_d.as<uint32_t>(), c->scratch.p,
+                          c->s));
+  }
+  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  return LCPC_OK;
+}
+
+Xop op_partial_gather(lcpc_sharded_commit *c, size_t r) {
+  Xop op{Xop::ALL_TO_ALL};
+  const size_t bytes = (size_t)round_tensors(c, r) * c->np * c->wb;
+  op.send = c->part_d.as<uint8_t>();
+  op.recv = c->me == c->root_rank ? c->allpart.as<uint8_t>() : nullptr;
+  op.sb.assign(c->G, 0);
+  op.rb.assign(c->G, 0);
+  op.sb[c->root_rank] = bytes;
+  if (c->me == c->root_rank) op.rb.assign(c->G, bytes);
+  op.ready = c->ev_ready;
+  return op;
+}
+
+// root: fold the G partials mod p; Montgomery sums (the proof) and canonical reprs (the
+// transcript) to the host
+lcpc_status stage_fold(lcpc_sharded_commit *c, size_t r) {
+  if (c->me != c->root_rank) return LCPC_OK;
+  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  const size_t wb = c->wb, np = c->np;
+  const size_t len = (size_t)round_tensors(c, r) * np;
+  HIP_TRY(collapse_fold_rows(c->fid, c->allpart.as<uint32_t>(), c->G, len, c->sum.as<uint32_t>(), c->s));
+  HIP_TRY(convert(c->fid, c->sum.as<uint32_t>(), c->canon.as<uint32_t>(), len, false, c->s));
+  HIP_TRY(hipMemcpyAsync(c->h_sum.p, c->sum.p, len * wb, hipMemcpyDeviceToHost, c->s));
+  HIP_TRY(hipMemcpyAsync(c->h_repr.p, c->canon.p, len * wb, hipMemcpyDeviceToHost, c->s));
+  HIP_TRY(hipEventRecord(c->ev_host, c->s));
+  return LCPC_OK;
+}
+
+void repr_order(int fid, uint8_t *h, size_t n, int wb) {
+  if (fid == LCPC_FT253_192)  // PrimeFieldReprEndianness = "big" (ft253_192.rs:9)
+    for (size_t i = 0; i < n; i++) std::reverse(h + i * wb, h + (i + 1) * wb);
+}
+
+// root, host: absorb round r's row combination(s) (lib.rs:1075-1077, 1096-1098) and draw the
+// next challenge: tensor r + 1 (:1056-1062) or, after the last round, the columns (:1101-1110)
+lcpc_status host_absorb(lcpc_sharded_commit *c, size_t r) {
+  HIP_TRY(hipEventSynchronize(c->ev_host));
+  const size_t wb = c->wb, np = c->np, limbs = wb / 8;
+  uint8_t *repr = c->h_repr.p;
+  repr_order(c->fid, repr, (size_t)round_tensors(c, r) * np, (int)wb);
+  if (c->ndt == 0) {  // the evaluation round
+    std::memcpy(c->p_eval.data(), c->h_sum.p, np * wb);
+    std::memcpy(c->h_repr_eval.p, repr, np * wb);
+  } else {
+    std::memcpy(c->p_random.data() + r * np * limbs, c->h_sum.p, np * wb);
+    if (r == 0) {
+      std::memcpy(c->p_eval.data(), c->h_sum.p + np * wb, np * wb);
+      std::memcpy(c->h_repr_eval.p, repr + np * wb, np * wb);
+    }
+    prof::HostScope hs("host_prove_transcript");
+    c->tr->t.append_messages(LABEL_PR, 6, repr, wb, np);
+  }
+  if (r + 1 < c->rounds) {
+    std::vector<uint64_t> t;
+    challenge_tensor(c->tr->t, c->fid, c->n_rows, t);
+    std::memcpy(c->h_t.p, t.data(), c->n_rows * wb);
+    return LCPC_OK;
+  }
+  {
+    prof::HostScope hs("host_prove_transcript");
+    c->tr->t.append_messages(LABEL_PE, 6, c->h_repr_eval.p, wb, np);
+  }
+  challenge_columns(c->tr->t, c->nc, c->nco, c->col_idx);
+  std::memcpy(c->h_idx.p, c->col_idx.data(), c->nco * 8);
+  return LCPC_OK;
+}
+
+Xop op_idx_bcast(lcpc_sharded_commit *c) {
+  Xop op{Xop::BROADCAST};
+  op.recv = c->didx.as<uint8_t>();
+  op.bytes = c->nco * 8;
+  op.root = c->root_rank;
+  return op;
+}
+
+lcpc_status stage_idx_upload(lcpc_sharded_commit *c) {
+  if (c->me != c->root_rank || !c->nco) return LCPC_OK;
+  HIP_TRY(hipMemcpyAsync(c->didx.p, c->h_idx.p, c->nco * 8, hipMemcpyHostToDevice, c->comm->cs));
+  return LCPC_OK;
+}
+
+// my rows of the opened columns (open_column, :818-855): [col][my rows], Montgomery
+lcpc_status stage_gather_cols(lcpc_sharded_commit *c) {
+  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  if (c->nco && c->nr)
+    HIP_TRY(gather_columns(c->fid, c->comm_rows.as<uint32_t>(), c->nr, c->nc, c->didx.as<uint64_t>(), c->nco,
+                           c->mycols.as<uint32_t>(), c->s, false, true));
+  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  return LCPC_OK;
+}
+
+Xop op_cols_gather(lcpc_sharded_commit *c) {
+  Xop op{Xop::ALL_TO_ALL};
+  op.send = c->mycols.as<uint8_t>();
+  op.recv = c->me == c->root_rank ? c->allcols.as<uint8_t>() : nullptr;
+  op.sb.assign(c->G, 0);
+  op.rb.assign(c->G, 0);
+  op.sb[c->root_rank] = c->nco * c->nr * c->wb;
+  if (c->me == c->root_rank)
+    for (int k = 0; k < c->G; k++) op.rb[k] = c->nco * (c->part[k].r_hi - c->part[k].r_lo) * c->wb;
+  op.ready = c->ev_ready;
+  return op;
+}
+
+// root: Merkle paths off the whole tree, everything to the host
+lcpc_status stage_paths(lcpc_sharded_commit *c) {
+  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  if (c->me != c->root_rank) {
+    HIP_TRY(hipEventRecord(c->ev_host, c->s));
+    return LCPC_OK;
+  }
+  const size_t pl = log2_np2(c->nc);
+  if (c->nco) {
+    HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), 2 * c->nc - 1, c->didx.as<uint64_t>(), c->nco, pl,
+                         c->dpaths.as<uint8_t>(), c->s));
+    HIP_TRY(hipMemcpyAsync(c->h_cols.p, c->allcols.p, c->nco * c->n_rows * c->wb, hipMemcpyDeviceToHost, c->s));
+    if (pl) HIP_TRY(hipMemcpyAsync(c->h_paths.p, c->dpaths.p, c->nco * pl * 32, hipMemcpyDeviceToHost, c->s));
+  }
+  HIP_TRY(hipEventRecord(c->ev_host, c->s));
+  return LCPC_OK;
+}
+
+// root, host: the LcEvalProof (:1117-1122); columns reassembled from the ranks' row pieces
+lcpc_status host_proof(lcpc_sharded_commit *c, lcpc_proof **out) {
+  HIP_TRY(hipEventSynchronize(c->ev_host));
+  if (c->me != c->root_rank) {
+    if (out) *out = nullptr;
+    return LCPC_OK;
+  }
+  auto p = std::make_unique<lcpc_proof>();
+  const size_t wb = c->wb, nco = c->nco, n_rows = c->n_rows;
+  p->fid = c->fid;
+  p->n_cols = c->nc;
+  p->n_per_row = c->np;
+  p->n_rows = n_rows;
+  p->ndt = c->ndt;
+  p->nco = nco;
+  p->path_len = log2_np2(c->nc);
+  p->p_eval = c->p_eval;
+  p->p_random = c->p_random;
+  p->col_idx = c->col_idx;
+  p->cols.resize(nco * n_rows * (wb / 8));
+  uint8_t *dst = (uint8_t *)p->cols.data();
+  const uint8_t *src = c->h_cols.p;
+  for (int k = 0; k < c->G; k++) {
+    const size_t r0 = c->part[k].r_lo, nr = c->part[k].r_hi - r0;
+    for (size_t j = 0; j < nco; j++) std::memcpy(dst + (j * n_rows + r0) * wb, src + j * nr * wb, nr * wb);
+    src += nco * nr * wb;
+  }
+  p->paths.assign(c->h_paths.p, c->h_paths.p + nco * p->path_len * 32);
+  if (out) *out = p.release();
+  return LCPC_OK;
+}
+
+void prove_release(lcpc_sharded_commit *c) {
+  for (DBuf *b : {&c->bt, &c->tens, &c->part_d, &c->allpart, &c->sum, &c->canon, &c->didx, &c->mycols,
+                  &c->allcols, &c->dpaths, &c->scratch})
+    b->reset();
+  if (c->own_tr) delete c->tr;
+  c->tr = nullptr;
+  c->own_tr = false;
+}
+
+lcpc_status one_group(lcpc_sharded_commit *c, Xop op) {
+  std::vector<Xop> ops{std::move(op)};
+  return run_group(c->comm, ops, {c->ev_done});
+}
+
+}  // namespace
+
+// ================================================================= C ABI
+extern "C" {
+
+lcpc_status lcpc_comm_rccl_unique_id(uint8_t id[LCPC_COMM_UNIQUE_ID_BYTES]) {
+  if (!id) return fail(LCPC_ERR_INVALID_ARG, "null id");
+  Rccl &R = rccl();
+  if (!R.ok) return fail(LCPC_ERR_UNSUPPORTED, R.err);
+  ncclUniqueId u;
+  NCCL_TRY(R.GetUniqueId(&u));
+  std::memcpy(id, u.internal, LCPC_COMM_UNIQUE_ID_BYTES);
+  return LCPC_OK;
+}
+
+static lcpc_status comm_common(lcpc_comm *c) {
+  lcpc_status st;
+  c->dev = current_device(&st);
+  if (!c->dev) return st;
+  HIP_TRY(hipSetDevice(c->dev->id));
+  HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_comm_rccl_new(const uint8_t id[LCPC_COMM_UNIQUE_ID_BYTES], int nranks, int rank, lcpc_comm **out) {
+  if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  Rccl &R = rccl();
+  if (!R.ok) return fail(LCPC_ERR_UNSUPPORTED, R.err);
+  auto c = std::make_unique<lcpc_comm>();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->is_rccl = true;
+  lcpc_status st = comm_common(c.get());
+  if (st) return st;
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, LCPC_COMM_UNIQUE_ID_BYTES);
+  NCCL_TRY(R.CommInitRank(&c->nc, nranks, u, rank));
+  *out = c.release();
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_comm_from_ops(const lcpc_comm_ops *ops, int nranks, int rank, lcpc_comm **out) {
+  if (!ops || !out || nranks < 1 || rank < 0 || rank >= nranks) return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  if (nranks > 1 && (!ops->all_gather || !ops->all_to_all_v || !ops->broadcast))
+    return fail(LCPC_ERR_INVALID_ARG, "every collective must be supplied");
+  auto c = std::make_unique<lcpc_comm>();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->ops = *ops;
+  lcpc_status st = comm_common(c.get());
+  if (st) return st;
+  *out = c.release();
+  return LCPC_OK;
+}
+
+int lcpc_comm_nranks(const lcpc_comm *c) { return c ? c->nranks : 0; }
+int lcpc_comm_rank(const lcpc_comm *c) { return c ? c->rank : -1; }
+int lcpc_comm_is_rccl(const lcpc_comm *c) { return c && c->is_rccl ? 1 : 0; }
+void lcpc_comm_free(lcpc_comm *c) { delete c; }
+
+lcpc_status lcpc_sharded_rows(lcpc_field f, size_t n_rows, int nranks, int rank, size_t *row0, size_t *n_shard_rows) {
+  if (!valid_field(f) || nranks < 1 || rank < 0 || rank >= nranks || !row0 || !n_shard_rows)
+    return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  const Part p = partition(f, n_rows, nranks)[rank];
+  *row0 = p.r_lo;
+  *n_shard_rows = p.r_hi - p.r_lo;
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_sharded_commit_new_device(const lcpc_encoding *e, const void *d_rows, size_t n_rows, lcpc_comm *comm,
+                                           lcpc_sharded_commit **out) {
+  prof::HostScope hs_total("host_sharded_commit_total");
+  lcpc_status st = check_shardable(e, comm, n_rows);
+  if (st) return st;
+  if (!out) return fail(LCPC_ERR_INVALID_ARG, "null out");
+  std::lock_guard<std::mutex> lk(comm->mu);
+  ShardPtr c;
+  if ((st = shard_init(e, comm, n_rows, c))) return st;
+  if ((st = stage_pre_commit(c.get(), d_rows))) return st;
+  if ((st = one_group(c.get(), op_cv_exchange(c.get())))) return st;
+  if ((st = stage_post_cv(c.get()))) return st;
+  if ((st = one_group(c.get(), op_subtree_exchange(c.get())))) return st;
+  if ((st = stage_post_subtrees(c.get()))) return st;
+  if ((st = finish_commit(c.get()))) return st;
+  *out = c.release();
+  return LCPC_OK;
+}
+
+void lcpc_sharded_commit_free(lcpc_sharded_commit *c) { ShardDeleter()(c); }
+
+lcpc_status lcpc_sharded_commit_get_root(const lcpc_sharded_commit *c, uint8_t root[32]) {
+  if (!c || !root) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  std::memcpy(root, c->root, 32);
+  return LCPC_OK;
+}
+
+size_t lcpc_sharded_commit_n_hashes(const lcpc_sharded_commit *c) { return c ? 2 * c->nc - 1 : 0; }
+
+lcpc_status lcpc_sharded_commit_copy_hashes(const lcpc_sharded_commit *c, uint8_t *out) {
+  if (!c || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  HIP_TRY(hipSetDevice(c->dev->id));
+  HIP_TRY(hipMemcpyAsync(out, c->hashes.p, (2 * c->nc - 1) * 32, hipMemcpyDeviceToHost, c->s));
+  HIP_TRY(hipStreamSynchronize(c->s));
+  return LCPC_OK;
+}
+
+lcpc_status lcpc_sharded_prove(lcpc_sharded_commit *c, const uint64_t *outer, size_t outer_len, const lcpc_encoding *e,
+                               lcpc_transcript *tr, int root, lcpc_proof **out) {
+  prof::HostScope hs_total("host_sharded_prove_total");
+  if (!c || !e || !out || (!outer && outer_len)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  if (e != c->e && (e->n_per_row != c->np || e->n_cols != c->nc || e->fid != c->fid))
+    return fail(LCPC_PROVER_COMMIT, "ProverError::Commit");
+  if (outer_len != c->n_rows) return fail(LCPC_PROVER_OUTER_TENSOR, "ProverError::OuterTensor");
+  if (root < 0 || root >= c->G) return fail(LCPC_ERR_INVALID_ARG, "root rank");
+  if (c->me == root && !tr) return fail(LCPC_ERR_INVALID_ARG, "the root rank needs the transcript");
+  std::lock_guard<std::mutex> lk(c->comm->mu);
+  HIP_TRY(hipSetDevice(c->dev->id));
+  lcpc_status st;
+  struct Cleanup {
+    lcpc_sharded_commit *c;
+    ~Cleanup() { prove_release(c); }
+  } cleanup{c};
+  if ((st = prove_init(c, outer, root, c->me == root ? tr : nullptr, false))) return st;
+  if (c->me == root && (st = challenge_first(c))) return st;
+  for (size_t r = 0; r < c->rounds; r++) {
+    if ((st = stage_tensor_upload(c, r))) return st;
+    if ((st = one_group(c, op_tensor_bcast(c, r)))) return st;
+    if ((st = stage_collapse(c, r))) return st;
+    if ((st = one_group(c, op_partial_gather(c, r)))) return st;
+    if ((st = stage_fold(c, r))) return st;
+    if (c->me == root && (st = host_absorb(c, r))) return st;
+  }
+  if ((st = stage_idx_upload(c))) return st;
+  if ((st = one_group(c, op_idx_bcast(c)))) return st;
+  if ((st = stage_gather_cols(c))) return st;
+  if ((st = one_group(c, op_cols_gather(c)))) return st;
+  if ((st = stage_paths(c))) return st;
+  return host_proof(c, out);
+}
+
+// ---------------------------------------------------------------- the pipelined driver
+// Stages of polynomial k: 0 = chaining-value all-to-all, 1 = subtree all-gather, then for each
+// round r a tensor broadcast and a partial-sum gather, then the column-index broadcast and the
+// column gather.  Stage s of polynomial k goes out in tick k + off[s]; off[] leaves `lag` ticks
+// wherever the root rank absorbs one row combination before the next exchange needs its
+// challenge.  Every rank computes the same schedule, so the exchange groups match.
+lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *const *d_rows, size_t n_polys,
+                                           size_t n_rows, const uint64_t *outer, lcpc_comm *comm,
+                                           lcpc_make_transcript_fn make_transcript, void *user, size_t lag,
+                                           lcpc_proof **proofs, uint8_t *roots) {
+  lcpc_status st = check_shardable(e, comm, n_rows);
+  if (st) return st;
+  if (!d_rows || !outer || !make_transcript) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (proofs)
+    for (size_t i = 0; i < n_polys; i++) proofs[i] = nullptr;
+  if (n_polys == 0) return LCPC_OK;
+  std::lock_guard<std::mutex> lk(comm->mu);
+  HIP_TRY(hipSetDevice(e->dev->id));
+  const int G = comm->nranks, me = comm->rank;
+  if (lag == 0) lag = 1 + (size_t)G;  // ~1.3 ms of absorption per round over ~1.1 ms / G per tick (cfg3)
+  const size_t ndt = e->n_degree_tests, rounds = std::max<size_t>(ndt, 1);
+  // stage offsets
+  enum { S_CV = 0, S_SUB = 1, S_R0 = 2 };
+  const size_t n_stages = 2 + 2 * rounds + 2;
+  std::vector<size_t> off(n_stages);
+  off[S_CV] = 0;
+  off[S_SUB] = 1;
+  off[S_R0] = 3;  // the root rank needs the root on the host and the first challenge
+  off[S_R0 + 1] = off[S_R0] + 1;
+  for (size_t r = 1; r < rounds; r++) {
+    off[S_R0 + 2 * r] = off[S_R0 + 2 * r - 1] + lag;
+    off[S_R0 + 2 * r + 1] = off[S_R0 + 2 * r] + 1;
+  }
+  const size_t S_IDX = S_R0 + 2 * rounds, S_COLS = S_IDX + 1;
+  off[S_IDX] = off[S_IDX - 1] + (ndt ? 2 : 1) * lag;
+  off[S_COLS] = off[S_IDX] + 1;
+  const size_t n_ticks = n_polys + off[S_COLS];
+
+  TaskPool pool(std::min<size_t>(16, std::max(2u, std::thread::hardware_concurrency())));
+  std::vector<ShardPtr> cs(n_polys);
+  std::vector<std::future<lcpc_status>> finals;
+  auto start = [&](size_t k) -> lcpc_status {
+    lcpc_status s2 = shard_init(e, comm, n_rows, cs[k]);
+    if (s2) return s2;
+    return stage_pre_commit(cs[k].get(), d_rows[k]);
+  };
+  auto fail_all = [&](lcpc_status s2) {
+    const std::string msg = g_err;
+    for (auto &f : finals) f.wait();
+    for (auto &c : cs)
+      if (c && c->next.valid()) c->next.wait();
+    return fail(s2, msg);
+  };
+  if ((st = start(0))) return st;
+  for (size_t t = 0; t < n_ticks; t++) {
+    std::vector<Xop> ops;
+    std::vector<hipEvent_t> done;
+    std::vector<std::pair<size_t, size_t>> items;  // (poly, stage)
+    for (size_t s = 0; s < n_stages; s++) {
+      if (t < off[s] || t - off[s] >= n_polys) continue;
+      const size_t k = t - off[s];
+      lcpc_sharded_commit *c = cs[k].get();
+      if (s == S_CV) {
+        ops.push_back(op_cv_exchange(c));
+      } else if (s == S_SUB) {
+        ops.push_back(op_subtree_exchange(c));
+      } else if (s == S_IDX) {
+        if (c->me == c->root_rank) {
+          if ((st = c->next.get())) return fail_all(st);
+        }
+        if ((st = stage_idx_upload(c))) return fail_all(st);
+        ops.push_back(op_idx_bcast(c));
+      } else if (s == S_COLS) {
+        ops.push_back(op_cols_gather(c));
+      } else {
+        const size_t r = (s - S_R0) / 2;
+        if ((s - S_R0) % 2 == 0) {
+          if (r == 0) {
+            // the commit is complete (root on the host) and the transcript exists
+            if ((st = finish_commit(c))) return fail_all(st);
+            if (roots) std::memcpy(roots + 32 * k, c->root, 32);
+            lcpc_transcript *tr = nullptr;
+            if (me == (int)(k % G)) {
+              tr = make_transcript(user, k, c->root);
+              if (!tr) return fail_all(fail(LCPC_ERR_INVALID_ARG, "make_transcript returned NULL"));
+            }
+            if ((st = prove_init(c, outer, (int)(k % G), tr, true))) return fail_all(st);
+            if (me == c->root_rank && (st = challenge_first(c))) return fail_all(st);
+          } else if (c->me == c->root_rank) {
+            if ((st = c->next.get())) return fail_all(st);
+          }
+          if ((st = stage_tensor_upload(c, r))) return fail_all(st);
+          ops.push_back(op_tensor_bcast(c, r));
+        } else {
+          ops.push_back(op_partial_gather(c, r));
+        }
+      }
+      done.push_back(c->ev_done);
+      items.emplace_back(k, s);
+    }
+    if (!ops.empty() && (st = run_group(comm, ops, done))) return fail_all(st);
+    // the compute each exchange feeds, on the polynomials' own streams
+    for (auto [k, s] : items) {
+      lcpc_sharded_commit *c = cs[k].get();
+      if (s == S_CV) {
+        st = stage_post_cv(c);
+      } else if (s == S_SUB) {
+        st = stage_post_subtrees(c);
+      } else if (s == S_IDX) {
+        st = stage_gather_cols(c);
+      } else if (s == S_COLS) {
+        if ((st = stage_paths(c))) return fail_all(st);
+        lcpc_proof **dst = proofs ? proofs + k : nullptr;
+        finals.push_back(pool.submit([c, dst, &cs, k]() -> lcpc_status {
+          lcpc_proof *p = nullptr;
+          lcpc_status s2 = host_proof(c, &p);
+          if (dst) *dst = p;
+          else delete p;
+          cs[k].reset();  // every exchange of k is complete (its last one landed on the host)
+          return s2;
+        }));
+      } else {
+        const size_t r = (s - S_R0) / 2;
+        if ((s - S_R0) % 2 == 0) {
+          st = stage_collapse(c, r);
+        } else {
+          if ((st = stage_fold(c, r))) return fail_all(st);
+          if (c->me == c->root_rank) c->next = pool.submit([c, r] { return host_absorb(c, r); });
+        }
+      }
+      if (st) return fail_all(st);
+    }
+    if (t + 1 < n_polys && (st = start(t + 1))) return fail_all(st);
+  }
+  lcpc_status first = LCPC_OK;
+  std::string msg;
+  for (auto &f : finals) {
+    lcpc_status s2 = f.get();
+    if (s2 && !first) {
+      first = s2;
+      msg = g_err;
+    }
+  }
+  HIP_TRY(hipStreamSynchronize(comm->cs));
+  return first ? fail(first, msg) : LCPC_OK;
+}
+
+}  // extern "C"

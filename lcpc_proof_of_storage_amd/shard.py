@@ -1,31 +1,31 @@
 """Row-sharded Ligero commit / prove across GPUs (one process per GPU).
 
-One commitment's n_rows rows are split across the ranks.  Every rank encodes its rows and
-hashes what it can of the column leaves; the exchanges are small and go over RCCL (torch
-"nccl") or gloo:
+The product path is native: liblcpc_mi.so's lcpc_comm (RCCL over xGMI, or caller-supplied
+collectives) and lcpc_sharded_* run the whole protocol in C++ on device buffers
+(csrc/shard_native.cpp); this module's `NativeComm`, `ShardedCommit` and
+`sharded_commit_prove_many` are thin drivers over those entry points.
+
+The protocol (identical in both forms):
 
   commit  (lcpc-2d/src/lib.rs:651-815)
-    1. rank g encodes rows [r_g, r_g+1) -- the cut points fall on BLAKE3 chunk boundaries of
-       the leaf message (32 zero bytes || column), so rank g can compute the chaining values
-       of its chunks [c_g, c_g+1) for every column by itself;
+    1. rank g encodes rows [r_g, r_g+1) -- the cut points fall on BLAKE3 chunk boundaries of the
+       leaf message (32 zero bytes || column), so rank g can compute the chaining values of its
+       chunks [c_g, c_g+1) for every column by itself;
     2. all-to-all: rank g sends the chaining values of column block k to rank k
        ((chunks of g) x n_cols/G x 32 B -- 2-4 MiB at cfg3, not the 64 MiB codeword shard);
     3. rank k merges the chunks of its column block into leaves and builds that subtree;
-    4. all-gather of the G subtree roots; every rank finishes the top log2(G) levels.
+    4. all-gather of the subtrees; every rank holds the whole tree (native form) or the G
+       subtree roots and the top levels (RowShardedCommit below).
   prove   (lcpc-2d/src/lib.rs:1034-1123)
-    rank 0 owns the Merlin transcript; it broadcasts each degree-test tensor (the challenge
-    vector, n_rows elements), every rank returns its partial row combination, rank 0 folds
-    them mod p and absorbs the result, and so on; the opened columns are assembled from every
-    rank's rows and the Merkle paths from the owners' subtrees and the shared top tree.
+    the root rank owns the Merlin transcript; it broadcasts each degree-test tensor (the
+    challenge vector, n_rows elements), every rank returns its partial row combination, the root
+    folds them mod p and absorbs the result, and so on; the opened columns are assembled from
+    every rank's rows and the Merkle paths from the tree.
 
-With the GPU backend and a device communicator (Comm(dist, "cuda:k"), backend "nccl") the
-exchanged buffers never leave HBM: the chaining values, partial row combinations and opened
-column pieces are torch tensors the library writes through device pointers
-(lcpc_*_device), and RCCL moves them over xGMI; only the folded row combinations (which the
-transcript absorbs on rank 0) and the 2B - 1 digests of each rank's subtree reach the host.
-
-The proof is bit-identical to the single-GPU LcCommit.prove (tests/test_shard.py runs the
-protocol over gloo at world_size 2 against a single-process commit).
+`RowShardedCommit` is the same protocol written over a pluggable compute backend and
+torch.distributed; it is what the CPU tests run against the oracle (tests/test_shard.py), the
+restatement the native form is checked against.  The proof is bit-identical to the single-GPU
+LcCommit.prove either way.
 """
 from __future__ import annotations
 
@@ -508,3 +508,202 @@ class RowShardedCommit:
         if self.sh is not None:
             self.b.shard_free(self.sh)
             self.sh = None
+
+
+# ================================================================ native driver (the product path)
+class NativeComm:
+    """An lcpc_comm handle.
+
+    * ``NativeComm.rccl(dist, group)``: RCCL over xGMI, one rank per GPU.  Rank 0 draws the
+      unique id (lcpc_comm_rccl_unique_id) and sends it over `dist` (any backend).
+    * ``NativeComm.host(dist, group)``: the collectives supplied from here over a CPU process
+      group (gloo): device buffers are staged through the host.  For several ranks sharing one
+      GPU (RCCL refuses duplicate GPUs) and for tests.
+    * ``NativeComm.single()``: one rank, no exchanges.
+    """
+
+    def __init__(self, handle, keep=None):
+        self._h = handle
+        self._keep = keep  # ctypes callbacks must outlive the handle
+        L = _lib()
+        self.rank = L.lcpc_comm_rank(handle)
+        self.world = L.lcpc_comm_nranks(handle)
+        self.is_rccl = bool(L.lcpc_comm_is_rccl(handle))
+
+    def __del__(self):
+        try:
+            _lib().lcpc_comm_free(self._h)
+        except Exception:
+            pass
+
+    @classmethod
+    def single(cls):
+        from . import _native as N
+        ops = N.CommOps()
+        h = C.c_void_p()
+        _check(_lib().lcpc_comm_from_ops(C.byref(ops), 1, 0, C.byref(h)))
+        return cls(h.value, ops)
+
+    @classmethod
+    def rccl(cls, dist, group=None):
+        import torch
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            _check(_lib().lcpc_comm_rccl_unique_id(uid))
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group, device=torch.device("cpu") if dist.get_backend(group) == "gloo"
+                                   else None)
+        uid = (C.c_uint8 * 128).from_buffer_copy(obj[0])
+        h = C.c_void_p()
+        _check(_lib().lcpc_comm_rccl_new(uid, world, rank, C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def host(cls, dist, group=None):
+        from . import _native as N
+        t = _HostTransport(dist, group)
+        ops = N.CommOps(None, N.ALL_GATHER_FN(t.all_gather), N.ALL_TO_ALL_V_FN(t.all_to_all_v),
+                        N.BROADCAST_FN(t.broadcast))
+        h = C.c_void_p()
+        _check(_lib().lcpc_comm_from_ops(C.byref(ops), t.world, t.rank, C.byref(h)))
+        return cls(h.value, (ops, t))
+
+
+class _HostTransport:
+    """lcpc_comm_ops over a CPU torch.distributed group: device bytes -> host -> gloo -> device."""
+
+    def __init__(self, dist, group=None):
+        self.dist, self.group = dist, group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.hip = C.CDLL("libamdhip64.so.7")  # the runtime liblcpc_mi.so itself uses
+        self.hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+
+    def _d2h(self, ptr, n):
+        import torch
+        t = torch.empty(n, dtype=torch.uint8)
+        if n and self.hip.hipMemcpy(t.data_ptr(), ptr, n, 2):
+            raise RuntimeError("hipMemcpy D2H failed")
+        return t
+
+    def _h2d(self, ptr, t):
+        n = t.numel()
+        if n and self.hip.hipMemcpy(ptr, t.data_ptr(), n, 1):
+            raise RuntimeError("hipMemcpy H2D failed")
+
+    def all_gather(self, user, send, recv, nbytes):
+        try:
+            import torch
+            src = self._d2h(send, nbytes)
+            out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+            self.dist.all_gather(out, src, group=self.group)
+            self._h2d(recv, torch.cat(out))
+            return 0
+        except Exception:  # a C caller cannot take a Python exception
+            return 1
+
+    def all_to_all_v(self, user, send, sb, recv, rb):
+        try:
+            import torch
+            sbl = [int(sb[k]) for k in range(self.world)]
+            rbl = [int(rb[k]) for k in range(self.world)]
+            src = self._d2h(send, sum(sbl))
+            out = torch.empty(sum(rbl), dtype=torch.uint8)
+            self.dist.all_to_all_single(out, src, rbl, sbl, group=self.group)
+            self._h2d(recv, out)
+            return 0
+        except Exception:
+            return 1
+
+    def broadcast(self, user, buf, nbytes, root):
+        try:
+            if nbytes:
+                t = self._d2h(buf, nbytes)
+                src = self.dist.get_global_rank(self.group, root) if self.group is not None else root
+                self.dist.broadcast(t, src, group=self.group)
+                self._h2d(buf, t)
+            return 0
+        except Exception:
+            return 1
+
+
+def _lib():
+    from . import _native as N
+    return N.load()
+
+
+def _check(rc):
+    from .lcpc2d import _raise
+    _raise(rc)
+
+
+def sharded_rows(field: int, n_rows: int, world: int, rank: int):
+    """(row0, n_shard_rows) of `rank` (lcpc_sharded_rows): cut on BLAKE3 chunk boundaries."""
+    r0, n = C.c_size_t(), C.c_size_t()
+    _check(_lib().lcpc_sharded_rows(field, n_rows, world, rank, C.byref(r0), C.byref(n)))
+    return r0.value, n.value
+
+
+class ShardedCommit:
+    """lcpc_sharded_commit: this rank's share of a row-sharded commitment (collective)."""
+
+    def __init__(self, enc, comm: NativeComm, d_rows: int, n_rows: int):
+        h = C.c_void_p()
+        _check(_lib().lcpc_sharded_commit_new_device(enc._h, C.c_void_p(d_rows) if d_rows else None, n_rows,
+                                                     comm._h, C.byref(h)))
+        self._h, self.enc, self.comm, self.n_rows = h.value, enc, comm, n_rows
+
+    def __del__(self):
+        try:
+            _lib().lcpc_sharded_commit_free(self._h)
+        except Exception:
+            pass
+
+    def get_root(self) -> bytes:
+        out = (C.c_uint8 * 32)()
+        _check(_lib().lcpc_sharded_commit_get_root(self._h, out))
+        return bytes(out)
+
+    @property
+    def hashes(self) -> bytes:
+        n = _lib().lcpc_sharded_commit_n_hashes(self._h)
+        out = (C.c_uint8 * (32 * n))()
+        _check(_lib().lcpc_sharded_commit_copy_hashes(self._h, out))
+        return bytes(out)
+
+    def prove(self, outer, tr=None, root: int = 0):
+        """Collective; returns the LcEvalProof on rank `root` (which passes the transcript)."""
+        from .lcpc2d import LcEvalProof, _elems
+        o = np.ascontiguousarray(_elems(outer, self.enc.field))
+        h = C.c_void_p()
+        _check(_lib().lcpc_sharded_prove(self._h, o.ctypes.data_as(C.POINTER(C.c_uint64)), o.shape[0], self.enc._h,
+                                         tr._h if tr is not None else None, root, C.byref(h)))
+        return LcEvalProof(h.value) if h.value else None
+
+
+def sharded_commit_prove_many(enc, comm: NativeComm, d_rows: Sequence[int], n_rows: int, outer, make_transcript,
+                              lag: int = 0, keep_proofs: bool = True):
+    """lcpc_sharded_commit_prove_many: pipelined commit + prove of len(d_rows) polynomials.
+
+    make_transcript(i, root) -> Transcript for polynomial i (called on its root rank, i % world);
+    returns (roots, proofs) with proofs[i] an LcEvalProof on the root rank of i, else None."""
+    from . import _native as N
+    from .lcpc2d import LcEvalProof, _elems
+    L = _lib()
+    n = len(d_rows)
+    o = np.ascontiguousarray(_elems(outer, enc.field))
+    rows = (C.c_void_p * max(n, 1))(*[C.c_void_p(p) for p in d_rows])
+    proofs = (C.c_void_p * max(n, 1))()
+    roots = (C.c_uint8 * max(32 * n, 1))()
+
+    def mk(user, i, root):
+        tr = make_transcript(int(i), bytes(root[:32]))
+        return L.lcpc_transcript_clone(tr._h)  # the library owns (and frees) the clone
+
+    cb = N.MAKE_TRANSCRIPT_FN(mk)
+    _check(L.lcpc_sharded_commit_prove_many(enc._h, rows, n, n_rows, o.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                            comm._h, cb, None, lag, proofs if keep_proofs else None, roots))
+    rb = bytes(roots)
+    return ([rb[32 * i:32 * i + 32] for i in range(n)],
+            [LcEvalProof(proofs[i]) if proofs[i] else None for i in range(n)])
