@@ -23,8 +23,8 @@ The protocol (identical in both forms):
     every rank's rows and the Merkle paths from the tree.
 
 `RowShardedCommit` is the same protocol written over a pluggable compute backend and
-torch.distributed; it is what the CPU tests run against the oracle (tests/test_shard.py), the
-restatement the native form is checked against.  The proof is bit-identical to the single-GPU
+torch.distributed; the CPU tests run it with the CPU restatement as the backend (tests/test_shard.py):
+the protocol the native form restates.  The proof is bit-identical to the single-GPU
 LcCommit.prove either way.
 """
 from __future__ import annotations
