@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """bench.py -- committed field-elements/s (commit + open) of a 2^24-coefficient Ligero
-commitment over Ft127 on MI355X (BASELINE.json metric, config 3 at N = 1).
+commitment over Ft127 on MI355X (BASELINE.json metric; config 3).
 
 One step = LcCommit::commit of 2^24 Ft127 coefficients already resident in HBM (encode every
 row with the R-S NTT, hash every column with BLAKE3, build the Merkle tree) followed by
@@ -8,18 +8,24 @@ LcCommit::prove (2 degree tests + evaluation row combination, Merlin transcript 
 row-combination coefficient, 309 column openings with Merkle paths): lcpc-2d/src/lib.rs:651-700
 and :1034-1123, dims 512 x 32768 -> 65536 (rho = 1/2, lcpc-ligero-pc/src/lib.rs:70-112).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
-committing and opening its own 2^24-coefficient polynomial (independent commitments, e.g. the
-proof-of-storage server's files): no data-path collective, "scaling": "weak".  The barrier and
-the max-over-ranks reduction of the timed region use torch.distributed.
+Engines (--mode):
+  sharded (default, cfg3): every step is ONE commitment whose rows are split over the N ranks
+    (one process per GPU, RCCL over xGMI through liblcpc_mi's own communicator), run by the
+    library's pipelined driver lcpc_sharded_commit_prove_many (csrc/shard_native.cpp): the
+    exchanges of the steps in flight go out in one fixed order per tick, the transcript of step
+    i runs on rank i % N.  At N = 1 the same driver runs with no exchanges.  "scaling": "strong"
+    (the work of a step is fixed as N grows).
+  replicas: every rank commits and opens its own polynomial (independent objects), host
+    threads keep --pipeline commitments in flight; "scaling": "weak".
 
-Printed JSON line: the metric, a "roofline" object for the dominant kernel (HIP events on the
-launching stream, taken on serial steps run right after the timed region, where each launch has
-the GPU to itself; with --prof-timed the per-kernel averages of the pipelined timed region are
-reported beside it -- recording events on every launch costs throughput, so the timed region
-runs without them by default)
-and a "cpu_baseline" object (the C restatement under oracle/, run on the host cores of rank 0 at
-N = 1, which doubles as the bit-exactness check of the root).
+Launch: `python bench.py --gpus N` spawns N ranks under torch.distributed.run itself (before any
+torch / HIP import); under torch.distributed.run (WORLD_SIZE set) --gpus must equal the world
+size.  The barrier and the max-over-ranks reduction of the timed region use torch.distributed.
+
+Printed JSON line: the metric, a "roofline" object for the dominant kernel (the encode; HIP
+events on the launching stream, on serial launches after the timed region) and a
+"cpu_baseline" object (the C restatement under oracle/, run on the host cores of rank 0 at
+N = 1: warm-up + median of 5, which doubles as the bit-exactness check of the root).
 """
 import argparse
 import glob
@@ -42,8 +48,18 @@ SEED = 0x1CDC2024       # coefficients = F::random(ChaCha20Rng
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1024)
-    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--mode", choices=["sharded", "replicas"], default="sharded",
+                    help="sharded: one commitment per step, rows split over the ranks (the library's "
+                         "pipelined driver; the BASELINE cfg3 configuration); replicas: independent "
+                         "commitments per rank on host threads (ligero only)")
+    ap.add_argument("--lag", type=int, default=0,
+                    help="sharded driver: ticks between a row-combination gather and the next challenge "
+                         "broadcast (0: the library's choice)")
+    ap.add_argument("--plumbing-only", action="store_true",
+                    help="multi-process plumbing check without a GPU (spawn, world size, barrier, "
+                         "max-over-ranks over gloo); prints the JSON line with value null")
     ap.add_argument("--log-len", type=int, default=None, help="log2 coefficients (24; 20 for --code encode)")
     ap.add_argument("--field", default="Ft127")
     ap.add_argument("--code", choices=["ligero", "sdig", "pos", "encode"], default="ligero",
@@ -51,11 +67,10 @@ def parse():
                          "SdigCode3 expander code, seed 0 (cfg4); pos: proof-of-storage request "
                          "on a resident file (cfg5); encode: the Ligero R-S encode alone (cfg2)")
     ap.add_argument("--pos-bytes", type=int, default=1 << 30, help="file size for --code pos")
-    ap.add_argument("--shard", choices=["none", "rows"], default="none",
-                    help="rows: one Ligero commitment per step with its rows split across the "
-                         "ranks (shard.py; RCCL exchanges; strong scaling)")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the cores available (max 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every core this process may use (affinity and cgroup quota)")
+    ap.add_argument("--cpu-reps", type=int, default=5, help="cpu_baseline: timed runs after one warm-up (median)")
     ap.add_argument("--cpu-baseline-1core", choices=["auto", "on", "off"], default="auto",
                     help="also time the oracle on one thread (auto: the ligero workload)")
     ap.add_argument("--no-prof", action="store_true", help="disable HIP-event kernel timing")
@@ -76,6 +91,8 @@ def parse():
                          "4 for --code pos (a 1 GiB request's 2.3 GiB codeword per slot: deeper "
                          "pipelines only contend for HBM)")
     args = ap.parse_args()
+    if args.code != "ligero":
+        args.mode = "replicas"  # cfg2 / cfg4 / cfg5 run as independent steps per rank
     if args.log_len is None:
         args.log_len = 20 if args.code == "encode" else 24
     if args.pipeline <= 0:
@@ -182,6 +199,26 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
     inner = L.field_random(fid, n_per_row, 8)  # verify returns sum_c inner[c] p_eval[c]
     cpu_verify = []  # (ms, accepted, evaluation) per cpu_baseline call
 
+    def latency(reps):
+        """one commitment, serial: commit and prove wall clock (median of reps)"""
+        cs, ps = [], []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+            root = c.get_root()
+            t2 = time.perf_counter()
+            tr = L.Transcript(b"test transcript")
+            tr.append_message(b"polycommit", root)
+            tr.append_message(b"ncols", nco.to_bytes(8, "big"))
+            c.prove(outer, enc, tr)
+            cs.append(1e3 * (t2 - t1))
+            ps.append(1e3 * (time.perf_counter() - t2))
+        cs.sort()
+        ps.sort()
+        return {"commit_ms": cs[len(cs) // 2], "prove_ms": ps[len(ps) // 2],
+                "what": f"one commitment, serial: LcCommit::commit_device and LcCommit::prove (median of {reps})"}
+
     def cpu_baseline(O):
         o_enc = (O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3) if sdig
                  else O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt))
@@ -228,7 +265,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
                                    f"BLAKE3 Merkle",
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                 "n_col_opens": nco, "n_degree_tests": ndt},
-        step=step, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify,
+        step=step, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify, latency=latency,
         enc_kernels=("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=("sdig_encode = transpose + 13 SpMM / Reed-Solomon levels (per commit, all rows)" if sdig
                          else f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
@@ -291,73 +328,13 @@ def encode_workload(args, L, torch, rank, local_rank):
         config={"workload": f"Ligero R-S encode, {args.field}, 2^{args.log_len} coeffs, "
                             f"{n_rows}x{n_per_row}->{n_cols}",
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols},
-        step=step, cpu_baseline=cpu_baseline, cpu_cores=1, root_is_parity=True,
+        step=step, cpu_baseline=cpu_baseline, cpu_cores=1, root_is_parity=True, cpu_reps_ok=False,
         enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per step, all {n_rows} rows)",
         algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B,
         traffic_key=(n, args.field, "encode"),
         mul_count=n_rows * ntt_muls(n_cols),
         mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row")
-
-
-def shard_workload(args, L, torch, rank, local_rank, dist):
-    """cfg3 with one commitment's rows sharded across the ranks (shard.py): strong scaling."""
-    from lcpc_proof_of_storage_amd.shard import Comm, GpuBackend, RowShardedCommit
-    fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
-    nl = L.limbs(fid)
-    n = 1 << args.log_len
-    enc = L.LigeroEncoding.new(fid, n)
-    n_rows, n_per_row, n_cols = enc.get_dims(n)
-    nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
-    coeffs = L.field_random(fid, n, SEED)           # the same polynomial on every rank
-    rows = np.zeros((n_rows * n_per_row, nl), np.uint64)
-    rows[:n] = coeffs
-    rows = rows.reshape(n_rows, n_per_row * nl)
-    outer = L.field_random(fid, n_rows, 7)
-    be = GpuBackend(enc)
-    # device-resident exchanges (RCCL at N > 1); every pipeline slot has a process group of its
-    # own, so the collectives of commitments in flight never interleave within one communicator
-    dev = f"cuda:{local_rank}"
-    groups = [dist.new_group(list(range(dist.get_world_size()))) for _ in range(max(1, args.pipeline))] \
-        if dist is not None else [None] * max(1, args.pipeline)
-    comms = [Comm(dist, dev, group=g) for g in groups]
-    comm = comms[0]
-    sc0 = RowShardedCommit(be, comm, n_rows, 8 * nl)
-    mine = np.ascontiguousarray(rows[sc0.r_lo:sc0.r_hi])  # this rank's rows stay resident in HBM
-    d_mine = torch.from_numpy(mine.view(np.int64)).to(f"cuda:{local_rank}")
-
-    def step(slot):
-        comm = comms[slot]
-        sc = RowShardedCommit(be, comm, n_rows, 8 * nl)
-        root = sc.commit((d_mine.data_ptr(), sc.r_hi - sc.r_lo))
-        tr = None
-        if comm.rank == 0:
-            tr = L.Transcript(b"test transcript")
-            tr.append_message(b"polycommit", root)
-            tr.append_message(b"ncols", nco.to_bytes(8, "big"))
-        sc.prove(outer, tr)
-        sc.close()
-        return root
-
-    def cpu_baseline(O):
-        o_enc = O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
-        t1 = time.perf_counter()
-        oc = O.Commit(o_enc, coeffs.reshape(-1))
-        oc.prove(o_enc, outer.reshape(-1), O.standard_transcript(nco, oc.root()))
-        return time.perf_counter() - t1, oc.root(), f"one full commit+open of the same 2^{args.log_len} {args.field} workload"
-
-    return Workload(
-        units=n, unit="field-elements/s", bytes_per_unit=8 * nl, scaling="strong",
-        metric="committed field-elements/s (commit+open), 2^24-coeff Ligero, rows sharded across GPUs",
-        dtype=f"u64x{nl} ({args.field} Montgomery limbs)",
-        data=f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x})), one polynomial, rows split over ranks",
-        config={"workload": f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, {n_rows}x{n_per_row}->"
-                            f"{n_cols}, rows sharded at BLAKE3 chunk boundaries",
-                "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
-                "n_col_opens": nco, "n_degree_tests": ndt},
-        step=step, cpu_baseline=cpu_baseline, enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
-        enc_kernel_desc="ntt_encode = ntt_pass_a + ntt_pass_b (this rank's rows)",
-        algo_bytes=0, traffic_key=None, mul_count=0, mul_model="")
 
 
 def pos_workload(args, L, torch, rank, local_rank):
@@ -422,34 +399,386 @@ def pos_workload(args, L, torch, rank, local_rank):
         mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row")
 
 
+# ---------------------------------------------------------------- launch, cores, shared output
+def spawn_ranks(args):
+    """`bench.py --gpus N` outside torch.distributed.run: start N ranks ourselves (no torch or HIP
+    has been imported in this process) and exit with their status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def available_cores():
+    """(cores, basis): the CPUs this process may run on -- its affinity, capped by a cgroup CPU
+    quota when one is set (the GPU box grants each job a share of a large host)."""
+    n = len(os.sched_getaffinity(0))
+    basis = f"sched_getaffinity = {n}"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            c = max(1, int(int(q) / int(per)))
+            if c < n:
+                n, basis = c, basis + f", cgroup cpu.max quota = {c}"
+    except (OSError, ValueError):
+        pass
+    return n, basis
+
+
+def plumbing_check(args, rank, world):
+    """--plumbing-only: the multi-process contract without a GPU (CPU tests): gloo group, world
+    size check, barrier, max-over-ranks, rank-0 JSON line."""
+    dist = init_dist(world, 0, backend="gloo")
+    formed = dist.get_world_size() if dist else 1
+    sync_barrier(dist)
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (1 + rank))
+    sync_barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing check", "value": None, "unit": None, "n_gpus": formed,
+                          "world_formed": formed, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": 1e3 * elapsed / max(args.steps, 1), "plumbing_only": True}))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if formed == args.gpus else 3
+
+
+def roofline_objects(wl, iso, stats, args, traffic_rows_frac=1.0):
+    """roofline (HBM) + roofline_valu of the encode, roofline_leaf of the column hashing."""
+    out = {}
+    if not iso or not wl.algo_bytes:
+        return out
+    ki = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in iso.items()}
+    out["kernels"] = ki
+    enc_ms = sum(ki[k]["avg_ms"] for k in wl.enc_kernels if k in ki)
+    traffic, tsrc = None, None
+    for tpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+        try:
+            tj = json.load(open(tpath))
+        except (OSError, ValueError):
+            continue
+        if (tj.get("config_len"), tj.get("field"), tj.get("code", "ligero")) == wl.traffic_key:
+            traffic = tj.get("ntt_encode_bytes_per_launch")
+            if traffic is not None:
+                traffic *= traffic_rows_frac
+            tsrc = (f"{os.path.relpath(tpath, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
+                    f"workload's encode (a separate profiling run, not this process)")
+            break
+    achieved = wl.algo_bytes / (enc_ms * 1e-3) / 1e9 if enc_ms else None
+    tr_ms = None
+    if stats:
+        tr_ms = sum(stats[k][0] / max(stats[k][1], 1) for k in wl.enc_kernels if k in stats)
+    out["roofline"] = {
+        "kernel": wl.enc_kernel_desc, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic, "traffic_source": tsrc,
+        "algorithmic_bytes": wl.algo_bytes, "avg_ms": enc_ms,
+        "launches": min((ki[k]["launches"] for k in wl.enc_kernels if k in ki), default=0),
+        "measured": f"HIP events on the launching stream, {args.roofline_steps} serial steps after the timed "
+                    f"region (same process, inputs and kernels)",
+        "timed_region_avg_ms": tr_ms,
+    }
+    if wl.mul_count:
+        # the encode is bound by the 32-bit multiply-add pipe, not HBM: its VALU roofline is the
+        # Montgomery-multiply rate of the field measured in isolation (tools/microbench/femul2.hip
+        # on MI355X: Ft63 1701, Ft127 503, Ft255 137 G/s; profiles/r01_femul2.txt); the hardware
+        # v_mad_u64_u32 issue ceiling (20.6 T lane-ops/s, profiles/r01_mulbench.txt) over the 28
+        # mads of an Ft127 product is the second peak
+        field = args.field if args.code != "pos" else "Ft63"
+        peak = {"Ft63": 1701.0, "Ft127": 503.0, "Ft255": 137.0}.get(field)
+        ach = wl.mul_count / (enc_ms * 1e-3) / 1e9 if enc_ms else None
+        out["roofline_valu"] = {
+            "kernel": wl.enc_kernel_desc, "bound": "valu (v_mad_u64_u32 Montgomery products)",
+            "achieved": ach, "peak": peak, "unit": "G field-mul/s",
+            "frac": ach / peak if ach and peak else None, "muls_per_launch": wl.mul_count, "model": wl.mul_model,
+        }
+        if field == "Ft127" and ach:
+            out["roofline_valu"]["mad_issue_peak"] = 20600.0 / 28
+            out["roofline_valu"]["frac_of_mad_issue_peak"] = ach / (20600.0 / 28)
+    lc = getattr(wl, "leaf_compressions", 0)
+    if lc and "leaf_chunks" in iso:
+        leaf_ms = sum(iso[k][0] / max(iso[k][1], 1) for k in ("leaf_chunks", "leaf_merge") if k in iso)
+        ach = lc / (leaf_ms * 1e-3) / 1e9
+        out["roofline_leaf"] = {
+            "kernel": "leaf_chunks + leaf_merge (BLAKE3 column leaves)", "bound": "valu (BLAKE3 compressions)",
+            "achieved": ach, "peak": LEAF_PEAK_GCPS, "unit": "G compressions/s", "frac": ach / LEAF_PEAK_GCPS,
+            "compressions_per_launch": lc, "avg_ms": leaf_ms,
+            "peak_source": "tools/microbench/leafbench.hip compress-only twin of the leaf kernel, MI355X"}
+    return out
+
+
+def time_cpu_baseline(wl, O, cores, reps):
+    """one warm-up, then the median of `reps` timed runs on `cores` threads"""
+    O.lib().of_set_threads(cores)
+    wl.cpu_baseline(O)  # warm-up (page faults, thread start)
+    runs = []
+    oroot = sample = None
+    for _ in range(max(1, reps)):
+        dt, oroot, sample = wl.cpu_baseline(O)
+        runs.append(dt)
+    runs.sort()
+    return runs[len(runs) // 2], runs, oroot, sample
+
+
+# ---------------------------------------------------------------- the sharded engine (cfg3)
+def ligero_sharded(args, L, torch, dist, rank, world, device, backend, share):
+    """cfg3 at any N: steps are single 2^24 commitments, rows split over the ranks, driven by
+    lcpc_sharded_commit_prove_many (one RCCL group per pipeline tick)."""
+    from lcpc_proof_of_storage_amd import shard
+    fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
+    nl = L.limbs(fid)
+    n = 1 << args.log_len
+    enc = L.LigeroEncoding.new(fid, n)
+    n_rows, n_per_row, n_cols = enc.get_dims(n)
+    nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
+    coeffs = L.field_random(fid, n, SEED)                    # one polynomial; rank g keeps its rows
+    outer = L.field_random(fid, n_rows, 7)
+    inner = L.field_random(fid, n_per_row, 8)
+    rows = np.zeros((n_rows * n_per_row, nl), np.uint64)
+    rows[:n] = coeffs
+    rows = rows.reshape(n_rows, n_per_row * nl)
+    r0, nr = shard.sharded_rows(fid, n_rows, world, rank)
+    d_mine = torch.from_numpy(np.ascontiguousarray(rows[r0:r0 + nr]).view(np.int64)).to(device)
+    d_out = torch.empty(max(nr, 1) * n_cols * nl, dtype=torch.int64, device=device)  # roofline encode target
+    torch.cuda.synchronize()
+    if world == 1:
+        comm, comm_kind = shard.NativeComm.single(), "none (one rank)"
+    elif backend == "nccl" and not share:
+        comm, comm_kind = shard.NativeComm.rccl(dist), "RCCL (liblcpc_mi lcpc_comm_rccl_new, device send/recv)"
+    else:
+        comm, comm_kind = shard.NativeComm.host(dist), "host-staged gloo collectives (ranks share one GPU)"
+    assert comm.world == world and comm.rank == rank, (comm.world, comm.rank)
+
+    def make_tr(i, root):
+        tr = L.Transcript(b"test transcript")
+        tr.append_message(b"polycommit", root)
+        tr.append_message(b"ncols", nco.to_bytes(8, "big"))
+        return tr
+
+    def run(k, keep=False):
+        return shard.sharded_commit_prove_many(enc, comm, [d_mine.data_ptr()] * k, n_rows, outer, make_tr,
+                                               lag=args.lag, keep_proofs=keep)
+
+    def serial_commit():
+        return shard.ShardedCommit(enc, comm, d_mine.data_ptr(), n_rows)
+
+    def serial_prove(sc):
+        root = sc.get_root()
+        return sc.prove(outer, make_tr(0, root) if rank == 0 else None, root=0)
+
+    B = 8 * nl
+    return dict(
+        fid=fid, enc=enc, n=n, n_rows=n_rows, n_per_row=n_per_row, n_cols=n_cols, nco=nco, ndt=ndt, nr=nr,
+        coeffs=coeffs, outer=outer, inner=inner, run=run, serial_commit=serial_commit,
+        serial_prove=serial_prove, make_tr=make_tr,
+        comm_kind=comm_kind, d_mine=d_mine, d_out=d_out, B=B)
+
+
 def main():
     args = parse()
     rank, local_rank, world = dist_env()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher formed WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.plumbing_only:
+        sys.exit(plumbing_check(args, rank, world))
     os.environ["LCPC_STREAM_MODE"] = args.stream_mode  # read when the library creates streams
     import torch
 
     # LCPC_BENCH_BACKEND=gloo with LCPC_BENCH_SHARE_GPU=1 rehearses N ranks on one GPU (a
-    # one-GPU box); the default is one rank per GPU over RCCL
+    # one-GPU box; the exchanges then go over host-staged gloo collectives); the default is one
+    # rank per GPU over RCCL
     backend = os.environ.get("LCPC_BENCH_BACKEND", "nccl")
-    if os.environ.get("LCPC_BENCH_SHARE_GPU") == "1":
-        local_rank = 0
-    dist = init_dist(world, local_rank, backend=backend)
-    torch.cuda.set_device(local_rank)
+    share = os.environ.get("LCPC_BENCH_SHARE_GPU") == "1"
+    device_idx = 0 if share else local_rank
+    dist = init_dist(world, device_idx, backend=backend)
+    formed = dist.get_world_size() if dist is not None else 1
+    if formed != args.gpus:
+        print(f"bench.py: formed a world of {formed} ranks, --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    torch.cuda.set_device(device_idx)
+    device = f"cuda:{device_idx}"
 
     import lcpc_proof_of_storage_amd as L
 
-    L.set_device(local_rank)
-    if args.shard == "rows":
-        wl = shard_workload(args, L, torch, rank, local_rank, dist)
+    L.set_device(device_idx)
+    if args.mode == "sharded":
+        out = run_sharded(args, L, torch, dist, rank, world, device, backend, share)
     else:
-        wl = {"pos": pos_workload, "encode": encode_workload}.get(args.code, ligero_or_sdig)(
-            args, L, torch, rank, local_rank)
-    torch.cuda.synchronize()
+        out = run_replicas(args, L, torch, dist, rank, world, device_idx, backend)
+    if rank == 0:
+        out["world_formed"] = formed
+        print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
 
+
+def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
+    S = ligero_sharded(args, L, torch, dist, rank, world, device, backend, share)
+    n, B, nr = S["n"], S["B"], S["nr"]
+    fid, enc = S["fid"], S["enc"]
+    n_rows, n_per_row, n_cols, nco, ndt = S["n_rows"], S["n_per_row"], S["n_cols"], S["nco"], S["ndt"]
+
+    def barrier():
+        sync_barrier(dist, torch.cuda.synchronize)
+
+    # warm-up (pools, streams, RCCL connections); polynomial 0's proof is kept on rank 0
+    roots, proofs = S["run"](max(1, args.warmup), keep=True)
+    warm_proof = proofs[0]
+    assert all(r == roots[0] for r in roots), "nondeterministic root across steps"
+    prof_timed = args.prof_timed and not args.no_prof
+    L.prof_enable(prof_timed)
+    L.prof_reset()
+    barrier()
+    t0 = time.perf_counter()
+    troots, _ = S["run"](args.steps)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    L.prof_enable(False)
+    stats = L.prof_stats() if prof_timed else {}
+    assert all(r == roots[0] for r in troots), "timed-region roots differ from the warm-up's"
+    elapsed = max_over_ranks(dist, elapsed, "cpu" if backend == "gloo" else device)
+
+    # one commitment's latency (serial, median of 3) and the roofline launches (HIP events on the
+    # launching streams, every kernel of those serial steps)
+    lat_c, lat_p, iso = [], [], {}
+    sc = pf = None
+    for rep in range(1 + args.roofline_steps):
+        if rep == 1 and not args.no_prof:
+            L.prof_reset()
+            L.prof_enable(True)
+        barrier()
+        t1 = time.perf_counter()
+        sc = S["serial_commit"]()
+        t2 = time.perf_counter()
+        pf = S["serial_prove"](sc)
+        t3 = time.perf_counter()
+        if rep >= 1:
+            lat_c.append(1e3 * (t2 - t1))
+            lat_p.append(1e3 * (t3 - t2))
+    if not args.no_prof:
+        L.prof_enable(False)
+        iso = L.prof_stats()
+    lat_c.sort()
+    lat_p.sort()
+    value = job_throughput(n, args.steps, 1, elapsed)
+    out = {
+        "metric": "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU",
+        "value": value, "unit": "field-elements/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": f"u64x{B // 8} ({args.field} Montgomery limbs)",
+        "data": f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x})), one polynomial, each rank's rows "
+                f"resident in its HBM",
+        "config": {"workload": f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho=1/2, {n_rows}x"
+                               f"{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, BLAKE3 Merkle",
+                   "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
+                   "n_col_opens": nco, "n_degree_tests": ndt,
+                   "parallelism": (f"rows sharded x{world} (one commitment per step; lcpc_sharded_commit_prove_many, "
+                                   f"transcript of step i on rank i % {world})" if world > 1 else
+                                   "one GPU (lcpc_sharded_commit_prove_many with one rank: pipelined steps)"),
+                   "exchanges": S["comm_kind"], "lag": args.lag or None, "rows_on_rank0": nr},
+        "mb_per_s": value * B / 1e6,
+        "latency": {"commit_ms": lat_c[len(lat_c) // 2] if lat_c else None,
+                    "prove_ms": lat_p[len(lat_p) // 2] if lat_p else None,
+                    "what": "one commitment, serial: lcpc_sharded_commit_new_device and lcpc_sharded_prove "
+                            "(host wall clock, median of the roofline steps)"},
+    }
+    if stats:
+        out["kernels_timed_region"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]}
+                                       for k, v in stats.items()}
+    # the dominant kernel, the encode, over THIS rank's rows
+    wl = Workload(
+        algo_bytes=nr * n_per_row * B + nr * n_cols * B, enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
+        enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, this rank's {nr} rows)",
+        traffic_key=(n, args.field, "ligero"), mul_count=nr * ntt_muls(n_cols),
+        mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row",
+        leaf_compressions=leaf_compressions(n_rows, n_cols, B) if world == 1 else 0)
+    out.update(roofline_objects(wl, iso, stats, args, traffic_rows_frac=nr / n_rows))
+
+    # the verifier (outside the timed region): the serial step's proof, verified again
+    if rank == 0 and args.verify_reps > 0 and pf is not None:
+        root = sc.get_root()
+        ev = pf.verify(root, S["outer"], S["inner"], enc, S["make_tr"](0, root))
+        t1 = time.perf_counter()
+        for _ in range(args.verify_reps):
+            pf.verify(root, S["outer"], S["inner"], enc, S["make_tr"](0, root))
+        out["verify"] = {"ms": 1e3 * (time.perf_counter() - t1) / args.verify_reps, "reps": args.verify_reps,
+                         "what": "LcEvalProof::verify of one proof of this workload (host + GPU, serial)"}
+    else:
+        ev = None
+
+    # CPU baseline: the oracle (C restatement) on the same workload, rank 0 at N = 1
+    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    if rank == 0 and want_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ffi as O  # checker / CPU baseline only
+        o_enc = O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
+        keep = {}
+
+        def cpu_once(O_):
+            t1 = time.perf_counter()
+            oc = O_.Commit(o_enc, S["coeffs"].reshape(-1))
+            op = oc.prove(o_enc, S["outer"].reshape(-1), O_.standard_transcript(nco, oc.root()))
+            dt = time.perf_counter() - t1
+            keep["oc"], keep["op"] = oc, op
+            return dt, oc.root(), f"one full commit+open of the same 2^{args.log_len} {args.field} workload"
+
+        cores, basis = available_cores()
+        if args.cpu_threads:
+            cores, basis = args.cpu_threads, "--cpu-threads"
+        med, runs, oroot, sample = time_cpu_baseline(Workload(cpu_baseline=cpu_once), O, cores, args.cpu_reps)
+        out["cpu_baseline"] = {"value": n / med, "unit": "field-elements/s", "cores": cores, "kind": "port",
+                               "sample": f"{sample}: median of {len(runs)} runs after a warm-up on {cores} threads "
+                                         f"({', '.join(f'{r:.3f}' for r in runs)} s)", "cores_basis": basis}
+        out["parity_root_vs_oracle"] = oroot == roots[0]
+        op = keep["op"]
+        if warm_proof is not None:
+            out["parity_proof_vs_oracle"] = bool(
+                np.array_equal(warm_proof.p_eval.reshape(-1), op.p_eval)
+                and np.array_equal(np.concatenate(warm_proof.p_random_vec).reshape(-1), op.p_random)
+                and np.array_equal(np.stack([c.col for c in warm_proof.columns]).reshape(-1), op.cols)
+                and b"".join(b"".join(c.path) for c in warm_proof.columns) == op.paths.tobytes())
+        if ev is not None:
+            t2 = time.perf_counter()
+            rc, oev = op.verify(keep["oc"].root(), S["outer"].reshape(-1), S["inner"].reshape(-1), o_enc,
+                                O.standard_transcript(nco, keep["oc"].root()))
+            out["verify"]["cpu_ms"] = 1e3 * (time.perf_counter() - t2)
+            out["verify"]["parity_vs_oracle"] = bool(rc == 0 and np.array_equal(np.asarray(ev).reshape(-1), oev))
+        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto"):
+            O.lib().of_set_threads(1)
+            dt1, oroot1, sample1 = cpu_once(O)
+            out["cpu_baseline_1core"] = {"value": n / dt1, "unit": "field-elements/s", "cores": 1, "kind": "port",
+                                         "sample": f"{sample1}: one run on 1 thread ({dt1:.2f} s)"}
+            out["parity_root_vs_oracle"] = out["parity_root_vs_oracle"] and oroot1 == roots[0]
+    return out
+
+
+# ---------------------------------------------------------------- the replica engine
+def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
+    """Independent commitments per rank (cfg3 replicas, cfg4 Brakedown, cfg5 PoS, cfg2 encode),
+    kept in flight on host threads over the library's pooled streams."""
+    wl = {"pos": pos_workload, "encode": encode_workload}.get(args.code, ligero_or_sdig)(
+        args, L, torch, rank, device_idx)
+    torch.cuda.synchronize()
     prof = not args.no_prof
-    n_workers = max(1, args.pipeline)
-    warm_each = max(1, -(-args.warmup // n_workers))  # every worker warms its own pinned
-    warmup_done = warm_each * n_workers                # staging and pool blocks first
+    # in-flight depth: every step in flight at once for short runs, else a divisor of steps, so
+    # the timed region never ends on a partial wave
+    P = max(1, args.pipeline)
+    if args.steps <= 2 * P:
+        P = max(1, args.steps)
+    else:
+        P = max(d for d in range(1, P + 1) if args.steps % d == 0)
+    n_workers = P
+    warm_each = max(1, -(-args.warmup // n_workers))  # every worker warms its own pinned staging
+    warmup_done = warm_each * n_workers
 
     def barrier():
         sync_barrier(dist, torch.cuda.synchronize)
@@ -468,19 +797,11 @@ def main():
             errors.append(e)
         ready.wait()
         start.wait()
-        # row shards: a static schedule (slot i runs steps i, i + P, ...), so that every rank
-        # issues the same collectives on each slot's process group
-        mine = len(range(slot, args.steps, n_workers)) if args.shard == "rows" else None
         while not errors:
             with lock:
-                if mine is not None:
-                    if mine <= 0:
-                        return
-                    mine -= 1
-                elif todo[0] <= 0:
+                if todo[0] <= 0:
                     return
-                else:
-                    todo[0] -= 1
+                todo[0] -= 1
             try:
                 roots.append(wl.step(slot))
             except Exception as e:
@@ -511,9 +832,8 @@ def main():
     iso = {}
     if prof:
         # The roofline launches: the same step run serially after the timed region, so each
-        # encode launch has the GPU to itself (inside the pipelined region, kernels of
-        # different commitments share the CUs and a launch's duration measures the sharing).
-        # One untimed step first: this (main) thread's pinned staging is allocated on first use.
+        # encode launch has the GPU to itself.  One untimed step first: this (main) thread's
+        # pinned staging is allocated on first use.
         wl.step(0)
         L.prof_reset()
         L.prof_enable(True)
@@ -521,145 +841,62 @@ def main():
             wl.step(0)
         L.prof_enable(False)
         iso = L.prof_stats()
-    elapsed = max_over_ranks(dist, elapsed, "cpu" if backend == "gloo" else f"cuda:{local_rank}")
+    lat = wl.latency(3) if getattr(wl, "latency", None) else None
+    elapsed = max_over_ranks(dist, elapsed, "cpu" if backend == "gloo" else f"cuda:{device_idx}")
     scaling = getattr(wl, "scaling", "weak")
     value = job_throughput(wl.units, args.steps, world if scaling == "weak" else 1, elapsed)
     out = {
-        "metric": wl.metric,
-        "value": value,
-        "unit": wl.unit,
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": warmup_done,
-        "ms_per_step": 1e3 * elapsed / args.steps,
-        "pipeline": args.pipeline,
-        "higher_is_better": True,
-        "scaling": scaling,
-        "vs_baseline": None,
-        "dtype": wl.dtype,
-        "data": wl.data,
-        "config": dict(wl.config, parallelism=(f"rows sharded x{world} (one commitment, shard.py)" if scaling == "strong"
-                                               else f"replicas x{world} (independent commitments per GPU, "
-                                                    f"{args.pipeline} in flight, {args.stream_mode} streams)")),
+        "metric": wl.metric, "value": value, "unit": wl.unit, "n_gpus": world, "steps": args.steps,
+        "warmup": warmup_done, "ms_per_step": 1e3 * elapsed / args.steps, "pipeline": P, "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": wl.dtype, "data": wl.data,
+        "config": dict(wl.config, parallelism=f"replicas x{world} (independent commitments per GPU, {P} in flight, "
+                                              f"{args.stream_mode} streams)"),
         "mb_per_s": value * wl.bytes_per_unit / 1e6,
     }
-
-    # ---- roofline of the dominant kernel (the encode, HIP events on the launching stream)
+    if lat:
+        out["latency"] = lat
     if stats:
         out["kernels_timed_region"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]}
                                        for k, v in stats.items()}
-    if iso and wl.algo_bytes:
-        ki = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in iso.items()}
-        out["kernels"] = ki
-        enc_ms = sum(ki[k]["avg_ms"] for k in wl.enc_kernels if k in ki)
-        traffic = None
-        for tpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
-            try:
-                tj = json.load(open(tpath))
-            except (OSError, ValueError):
-                continue
-            if (tj.get("config_len"), tj.get("field"), tj.get("code", "ligero")) == wl.traffic_key:
-                traffic = tj.get("ntt_encode_bytes_per_launch")
-                break
-        achieved = wl.algo_bytes / (enc_ms * 1e-3) / 1e9 if enc_ms else None
-        tr_ms = None
-        if stats:
-            tr_ms = sum(stats[k][0] / max(stats[k][1], 1) for k in wl.enc_kernels if k in stats)
-        out["roofline"] = {
-            "kernel": wl.enc_kernel_desc,
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS if achieved else None,
-            "traffic": traffic,
-            "algorithmic_bytes": wl.algo_bytes,
-            "avg_ms": enc_ms,
-            "launches": min((ki[k]["launches"] for k in wl.enc_kernels if k in ki), default=0),
-            "measured": f"HIP events on the launching stream, {args.roofline_steps} serial steps after the "
-                        f"timed region (same process, inputs and kernels)",
-            "timed_region_avg_ms": tr_ms,
-        }
-        if wl.mul_count:  # noqa: E501
-            # the encode is bound by the 32-bit multiply-add pipe, not HBM: its VALU roofline is
-            # the Montgomery-multiply rate of the field measured in isolation
-            # (the library multiply in isolation, tools/microbench/femul2.hip on MI355X:
-            # Ft63 1701, Ft127 503, Ft255 137 G/s; profiles/r01_femul2.txt)
-            peak = {"Ft63": 1701.0, "Ft127": 503.0, "Ft255": 137.0}.get(args.field if args.code != "pos" else "Ft63")
-            ach = wl.mul_count / (enc_ms * 1e-3) / 1e9 if enc_ms else None
-            out["roofline_valu"] = {
-                "kernel": wl.enc_kernel_desc, "bound": "valu (v_mad_u64_u32 Montgomery products)",
-                "achieved": ach, "peak": peak, "unit": "G field-mul/s",
-                "frac": ach / peak if ach and peak else None, "muls_per_launch": wl.mul_count,
-                "model": wl.mul_model,
-            }
+    out.update(roofline_objects(wl, iso, stats, args))
 
-    # ---- the column-leaf kernels against the BLAKE3 compression rate (VALU-issue bound)
-    lc = getattr(wl, "leaf_compressions", 0)
-    if iso and lc and "leaf_chunks" in iso:
-        leaf_ms = sum(iso[k][0] / max(iso[k][1], 1) for k in ("leaf_chunks", "leaf_merge") if k in iso)
-        ach = lc / (leaf_ms * 1e-3) / 1e9
-        out["roofline_leaf"] = {
-            "kernel": "leaf_chunks + leaf_merge (BLAKE3 column leaves)", "bound": "valu (BLAKE3 compressions)",
-            "achieved": ach, "peak": LEAF_PEAK_GCPS, "unit": "G compressions/s", "frac": ach / LEAF_PEAK_GCPS,
-            "compressions_per_launch": lc, "avg_ms": leaf_ms,
-            "peak_source": "tools/microbench/leafbench.hip compress-only twin of the leaf kernel, MI355X"}
-
-    # ---- the verifier (outside the timed region): one proof of this workload, verified again
     gev = None
     if getattr(wl, "verify_bench", None) and args.verify_reps > 0:
         vms, gev = wl.verify_bench(args.verify_reps)
         out["verify"] = {"ms": vms, "reps": args.verify_reps,
                          "what": "LcEvalProof::verify of one proof of this workload (host + GPU, serial)"}
-
-    # ---- CPU baseline: the oracle (C restatement) on the same workload, rank 0 at N = 1
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
     if rank == 0 and want_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ffi as O  # checker / CPU baseline only
-
-        cores = getattr(wl, "cpu_cores", None) or args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        O.lib().of_set_threads(cores)
-        cpu_s, oroot, sample = wl.cpu_baseline(O)
-        out["cpu_baseline"] = {
-            "value": wl.units / cpu_s,
-            "unit": wl.unit,
-            "cores": cores,
-            "kind": "port",
-            "sample": f"{sample} ({cpu_s:.2f} s on {cores} threads)",
-        }
+        cores, basis = available_cores()
+        if getattr(wl, "cpu_cores", None):
+            cores, basis = wl.cpu_cores, "this workload runs the oracle single-threaded"
+        elif args.cpu_threads:
+            cores, basis = args.cpu_threads, "--cpu-threads"
+        reps = args.cpu_reps if getattr(wl, "cpu_reps_ok", True) else 1
+        med, runs, oroot, sample = time_cpu_baseline(wl, O, cores, reps)
+        out["cpu_baseline"] = {"value": wl.units / med, "unit": wl.unit, "cores": cores, "kind": "port",
+                               "sample": f"{sample}: median of {len(runs)} runs after a warm-up on {cores} threads "
+                                         f"({', '.join(f'{r:.3f}' for r in runs)} s)", "cores_basis": basis}
         if getattr(wl, "root_is_parity", False):
-            out["parity_vs_oracle"] = bool(oroot)  # every encoded row equal to the oracle's
+            out["parity_vs_oracle"] = bool(oroot)
         elif oroot is not None:
             out["parity_root_vs_oracle"] = oroot == root if root is not None else None
-        # the CPU path on all host cores (above) and on one core
-        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and args.code == "ligero"
-                                                and args.shard == "none"):
+        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and args.code == "ligero"):
             O.lib().of_set_threads(1)
             cpu1_s, oroot1, sample1 = wl.cpu_baseline(O)
-            out["cpu_baseline_1core"] = {
-                "value": wl.units / cpu1_s,
-                "unit": wl.unit,
-                "cores": 1,
-                "kind": "port",
-                "sample": f"{sample1} ({cpu1_s:.2f} s on 1 thread)",
-            }
+            out["cpu_baseline_1core"] = {"value": wl.units / cpu1_s, "unit": wl.unit, "cores": 1, "kind": "port",
+                                         "sample": f"{sample1}: one run on 1 thread ({cpu1_s:.2f} s)"}
             if oroot1 is not None and root is not None:
                 out["parity_root_vs_oracle"] = out.get("parity_root_vs_oracle", True) and oroot1 == root
-
     cv = getattr(wl, "cpu_verify", None)
     if cv and "verify" in out:
-        out["verify"]["cpu_ms"] = cv[0][0]
-        if len(cv) > 1:
-            out["verify"]["cpu_1core_ms"] = cv[1][0]
+        out["verify"]["cpu_ms"] = cv[-1][0]
         out["verify"]["parity_vs_oracle"] = bool(all(a for _, a, _ in cv) and gev is not None and
-                                                 np.array_equal(np.asarray(cv[0][2]).reshape(-1),
+                                                 np.array_equal(np.asarray(cv[-1][2]).reshape(-1),
                                                                 np.asarray(gev).reshape(-1)))
-    if rank == 0:
-        print(json.dumps(out))
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":

@@ -56,6 +56,33 @@ def test_bench_plumbing_world2():
         assert thr == (1 << 24) * 10 * 2 / 2.0     # whole-job units / slowest rank's time
 
 
+@pytest.mark.timeout(240)
+def test_bench_gpus2_spawns_two_ranks():
+    """`bench.py --gpus 2` outside torch.distributed.run launches 2 ranks itself (before any torch
+    import) and the rank-0 line reports the world they formed."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--plumbing-only"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=220)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_formed"] == 2 and d["plumbing_only"] is True
+
+
+@pytest.mark.timeout(120)
+def test_bench_rejects_world_mismatch():
+    """under a launcher, --gpus must equal the world size it formed"""
+    import subprocess
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--plumbing-only"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
 def test_single_process_has_no_group():
     sys.path.insert(0, ROOT)
     import bench

@@ -52,6 +52,37 @@ def test_bench_ligero_small(gpu):
     assert d["parity_root_vs_oracle"] is True
     assert d["verify"]["parity_vs_oracle"] is True and d["verify"]["ms"] > 0
     assert d["config"]["n_rows"] * d["config"]["n_per_row"] == 1 << 16
+    # the default (sharded driver) line: the kept proof equals the oracle's, one commitment's latency
+    assert d["scaling"] == "strong" and d["parity_proof_vs_oracle"] is True
+    assert d["latency"]["commit_ms"] > 0 and d["latency"]["prove_ms"] > 0
+    assert "traffic_source" in d["roofline"] and d["world_formed"] == 1
+
+
+def test_bench_ligero_replicas_small(gpu):
+    d = _bench("--mode", "replicas", "--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1")
+    _check_common(d, 4)
+    _check_cpu(d)
+    assert d["scaling"] == "weak" and d["parity_root_vs_oracle"] is True and d["pipeline"] == 4
+    assert d["latency"]["commit_ms"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_sharded_two_ranks_one_gpu(gpu):
+    """`bench.py --gpus 2` spawns two ranks; on a one-GPU box they share the GPU and exchange over
+    host-staged gloo collectives (RCCL refuses two ranks on one device)."""
+    env = dict(os.environ, LCPC_BENCH_BACKEND="gloo", LCPC_BENCH_SHARE_GPU="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup",
+                        "2", "--log-len", "16", "--verify-reps", "1", "--cpu-baseline", "on"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_formed"] == 2 and d["scaling"] == "strong"
+    assert d["parity_root_vs_oracle"] is True and d["parity_proof_vs_oracle"] is True
+    assert "gloo" in d["config"]["exchanges"]
 
 
 def test_bench_encode_small(gpu):
