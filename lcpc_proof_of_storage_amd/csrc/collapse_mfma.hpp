@@ -94,6 +94,43 @@ __device__ __forceinline__ Fe<F> redc_plus(const uint32_t x[4], uint32_t top) {
   return o;
 }
 
+// The field element of a digit-position accumulator column: sum_u Y[u] 2^(8u) R^-1 mod p, for
+// |Y[u]| < 2^27 (at most 512 x 16 products of balanced digits per accumulator).
+template <class F>
+__device__ __forceinline__ Fe<F> recombine_redc(const int (&Y)[16]) {
+  // Y = sum_u Y_u 2^(8u) as S_w = sum_j Y_(4w+j) 2^(8j) (int64), then signed carries
+  int64_t S[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    int64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) sum += (int64_t)Y[4 * w + j] * ((int64_t)1 << (8 * j));
+    S[w] = sum;
+  }
+  uint32_t y[4];
+  int64_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const int64_t v = S[w] + carry;
+    y[w] = (uint32_t)v;
+    carry = v >> 32;  // arithmetic
+  }
+  // Y = y + carry 2^128 with |Y| < 512 2^18 2^120.01 < 2^147.01; add OFF = p 2^22 (a multiple
+  // of p, > 2^148.8 > |Y|) so that Y + OFF is nonnegative
+  constexpr uint32_t O0 = F::P[0] << 22;
+  constexpr uint32_t O1 = (F::P[1] << 22) | (F::P[0] >> 10);
+  constexpr uint32_t O2 = (F::P[2] << 22) | (F::P[1] >> 10);
+  constexpr uint32_t O3 = (F::P[3] << 22) | (F::P[2] >> 10);
+  constexpr uint32_t O4 = F::P[3] >> 10;
+  uint32_t cc = 0;
+  y[0] = __builtin_addc(y[0], O0, cc, &cc);
+  y[1] = __builtin_addc(y[1], O1, cc, &cc);
+  y[2] = __builtin_addc(y[2], O2, cc, &cc);
+  y[3] = __builtin_addc(y[3], O3, cc, &cc);
+  const uint32_t top = (uint32_t)(carry + (int64_t)O4 + (int64_t)cc);
+  return redc_plus<F>(y, top);
+}
+
 // One wave = 64 columns x the split's rows; 4 waves per block on adjacent column ranges.
 // partial[(split T + t) n_per_row + c] = sum over the split's rows (a field element).
 template <class F, int T>
@@ -170,37 +207,10 @@ __global__ __launch_bounds__(256) void k_collapse_mfma(const uint32_t *__restric
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // Y = sum_u Y_u 2^(8u) as S_w = sum_j Y_(4w+j) 2^(8j) (int64), then signed carries
-    int64_t S[4];
+    int Y[16];
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
-      int64_t sum = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) sum += (int64_t)rw[k][4 * w + j][n] * ((int64_t)1 << (8 * j));
-      S[w] = sum;
-    }
-    uint32_t y[4];
-    int64_t carry = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      const int64_t v = S[w] + carry;
-      y[w] = (uint32_t)v;
-      carry = v >> 32;  // arithmetic
-    }
-    // Y = y + carry 2^128 with |Y| < 512 2^18 2^120.01 < 2^147.01 (at most MAX_SPLIT_ROWS rows);
-    // add OFF = p 2^22 (a multiple of p, > 2^148.8 > |Y|) so that Y + OFF is nonnegative
-    constexpr uint32_t O0 = F::P[0] << 22;
-    constexpr uint32_t O1 = (F::P[1] << 22) | (F::P[0] >> 10);
-    constexpr uint32_t O2 = (F::P[2] << 22) | (F::P[1] >> 10);
-    constexpr uint32_t O3 = (F::P[3] << 22) | (F::P[2] >> 10);
-    constexpr uint32_t O4 = F::P[3] >> 10;
-    uint32_t cc = 0;
-    y[0] = __builtin_addc(y[0], O0, cc, &cc);
-    y[1] = __builtin_addc(y[1], O1, cc, &cc);
-    y[2] = __builtin_addc(y[2], O2, cc, &cc);
-    y[3] = __builtin_addc(y[3], O3, cc, &cc);
-    const uint32_t top = (uint32_t)(carry + (int64_t)O4 + (int64_t)cc);
-    if (c < n_per_row) fe_store<F>(partial, (split * T + t) * n_per_row + c, redc_plus<F>(y, top));
+    for (int u = 0; u < 16; u++) Y[u] = rw[k][u][n];
+    if (c < n_per_row) fe_store<F>(partial, (split * T + t) * n_per_row + c, recombine_redc<F>(Y));
   }
 }
 

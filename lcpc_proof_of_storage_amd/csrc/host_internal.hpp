@@ -164,17 +164,17 @@ struct Device {
   std::multimap<size_t, void *> pinned_free;
   std::map<void *, size_t> pinned_sizes;
   void *pinned_get(size_t bytes) {
-    bytes = std::max<size_t>(bytes, 4096);
+    // blocks are whole 2 MiB multiples; a cached block up to twice the rounded size is reused
+    const size_t want = (std::max<size_t>(bytes, 1) + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
     {
       std::lock_guard<std::mutex> lk(mu);
-      auto it = pinned_free.lower_bound(bytes);
-      if (it != pinned_free.end() && it->first <= 2 * bytes) {
+      auto it = pinned_free.lower_bound(want);
+      if (it != pinned_free.end() && it->first <= 2 * want) {
         void *p = it->second;
         pinned_free.erase(it);
         return p;
       }
     }
-    const size_t want = (bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
     void *p = nullptr;
     if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(mu);

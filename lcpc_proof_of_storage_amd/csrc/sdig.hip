@@ -6,6 +6,21 @@
 // threads of one output read the same nonzero (one broadcast load) and R adjacent elements of
 // one input (a coalesced R * B-byte run), so no gather is scattered even though the matrix is.
 // Field sums are exact, so the CSR order (vs sprs' CSC dot) cannot change a bit.
+//
+// Ft127 runs the levels on the int8 matrix cores instead (k_spmm_mfma), with the digit
+// decomposition of collapse_mfma.hpp: the matrix values are the small, reused operand (each one
+// multiplies R codeword elements), so every nonzero val_k is expanded once per encoding into the
+// balanced digits h[k][a][u] of H_ka = val_k 2^(8a) mod p, and an output is
+//     Y[u][b] = sum_(k, a) h[k][a][u] d_a(x[idx_k][b])          (one exact int32 GEMM per output)
+//     y[b]   = REDC(sum_u Y[u][b] 2^(8u)) = sum_k val_k x[idx_k][b]  (Montgomery, bit-identical)
+// A wave owns one output and TILES x 16 rows; each v_mfma_i32_16x16x64_i8 takes 4 nonzeros
+// (K = 4 x 16 digits) x 16 rows (N) x the 16 digit positions (M).  A 16-byte codeword element
+// is one lane's B fragment straight from the element-major layout, so the only VALU work per
+// (nonzero, row) is the 8-op balanced-digit conversion, against ~22 v_mad_u64_u32 + carries of
+// the VALU product.
+#include <cstdlib>
+
+#include "collapse_mfma.hpp"
 #include "field.hpp"
 #include "kernels.hpp"
 #include "prof.hpp"
@@ -44,6 +59,118 @@ __global__ __launch_bounds__(256) void k_spmm(const uint32_t *__restrict__ ptr,
   fe_store<F>(y, t, acc);
 }
 
+// hd[(kk 16 + u) 16 + a] = byte u of the balanced digits of val[src[kk]] 2^(8a) mod p, zero for
+// a padding slot (src = ~0).  One thread per (padded nonzero kk, a).
+template <class F>
+__global__ __launch_bounds__(256) void k_sdig_hdig(const uint32_t *__restrict__ val,
+                                                   const uint32_t *__restrict__ src, size_t n_pad,
+                                                   uint8_t *__restrict__ hd) {
+  static_assert(F::N == 4, "Ft127 layout");
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_pad * 16) return;
+  const int a = (int)(g & 15);
+  const size_t kk = g >> 4;
+  const uint32_t k = src[kk];
+  uint32_t w[4] = {0, 0, 0, 0};
+  if (k != ~0u) {
+    Fe<F> pw = fe_zero<F>();  // 2^(8a) as an integer, then to Montgomery form
+    pw.v[a >> 2] = 1u << (8 * (a & 3));
+    const Fe<F> h = fe_mul<F>(fe_load<F>(val, k), fe_to_mont<F>(pw));
+    const cmfma::v4i d = cmfma::balanced_digits(h.v[0], h.v[1], h.v[2], h.v[3]);
+    w[0] = (uint32_t)d.x;
+    w[1] = (uint32_t)d.y;
+    w[2] = (uint32_t)d.z;
+    w[3] = (uint32_t)d.w;
+  }
+#pragma unroll
+  for (int u = 0; u < 16; u++) hd[(kk * 16 + u) * 16 + a] = (uint8_t)(w[u >> 2] >> (8 * (u & 3)));
+}
+
+// One wave per output j (4 per block), rows [b0, b0 + 16 TILES) with b0 = 16 TILES blockIdx.y.
+// Lane (n = lane & 15, g = lane >> 4): A fragment = h of padded nonzero 4q + g at digit
+// position n; B fragment of tile t = the digits of x[idx][b0 + 16 t + n].  The output's
+// neighbour list (pidx) is staged in LDS first.  |Y| < 2^27 needs at most 512 nonzeros per
+// output (checked when the plan is built).
+constexpr int SPMM_MAX_GROUPS = 128;  // 512 nonzeros
+template <class F, int TILES>
+__global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ gptr,
+                                                   const uint32_t *__restrict__ pidx,
+                                                   const uint8_t *__restrict__ hd,
+                                                   const uint32_t *__restrict__ x,
+                                                   uint32_t *__restrict__ y, size_t m, uint32_t R) {
+  static_assert(F::N == 4, "Ft127 layout");
+  __shared__ int red[4][TILES][16][17];
+  __shared__ uint32_t nbr[4][4 * SPMM_MAX_GROUPS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t j = (size_t)blockIdx.x * 4 + wave;
+  if (j >= m) return;  // whole waves only: the kernel synchronises within a wave
+  const int n = lane & 15, g = lane >> 4;
+  const size_t b0 = (size_t)blockIdx.y * TILES * 16;
+  const uint32_t q0 = gptr[j], nq = gptr[j + 1] - q0;
+  uint32_t *nb = nbr[wave];
+  for (uint32_t i = lane; i < 4 * nq; i += 64) nb[i] = pidx[4 * (size_t)q0 + i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint4 *x4 = reinterpret_cast<const uint4 *>(x);
+  const uint4 *h4 = reinterpret_cast<const uint4 *>(hd);
+  bool rowok[TILES];
+#pragma unroll
+  for (int t = 0; t < TILES; t++) rowok[t] = b0 + 16 * t + n < R;
+  cmfma::v4i acc[TILES];
+#pragma unroll
+  for (int t = 0; t < TILES; t++) acc[t] = cmfma::v4i{0, 0, 0, 0};
+  auto load = [&](uint32_t q, uint4 *xv, uint4 &av) {
+    const size_t kk = 4 * ((size_t)q0 + q) + g;
+    const size_t id = nb[4 * q + g];
+    av = h4[kk * 16 + n];
+#pragma unroll
+    for (int t = 0; t < TILES; t++)
+      xv[t] = rowok[t] ? x4[id * R + b0 + 16 * t + n] : make_uint4(0, 0, 0, 0);
+  };
+  uint4 xc[TILES], xn[TILES], ac, an;
+  if (nq) load(0, xc, ac);
+  for (uint32_t q = 0; q < nq; q++) {
+    const bool more = q + 1 < nq;
+    if (more) load(q + 1, xn, an);
+    const cmfma::v4i av = cmfma::v4i{(int)ac.x, (int)ac.y, (int)ac.z, (int)ac.w};
+#pragma unroll
+    for (int t = 0; t < TILES; t++) {
+      const cmfma::v4i d = cmfma::balanced_digits(xc[t].x, xc[t].y, xc[t].z, xc[t].w);
+      acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, d, acc[t], 0, 0, 0);
+    }
+    if (more) {
+#pragma unroll
+      for (int t = 0; t < TILES; t++) xc[t] = xn[t];
+      ac = an;
+    }
+  }
+  // C/D layout: lane holds digit positions u = 4 g + i of row n of each tile; through this
+  // wave's LDS slice, then one output row per lane (tiles 4 at a time)
+  int(*rw)[16][17] = red[wave];
+#pragma unroll
+  for (int t = 0; t < TILES; t++) {
+    rw[t][4 * g + 0][n] = acc[t].x;
+    rw[t][4 * g + 1][n] = acc[t].y;
+    rw[t][4 * g + 2][n] = acc[t].z;
+    rw[t][4 * g + 3][n] = acc[t].w;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int p = 0; p < TILES; p += 4) {
+    const int t = p + g;
+    const size_t b = b0 + 16 * (size_t)t + n;
+    if (t < TILES && b < R) {
+      int Y[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) Y[u] = rw[t][u][n];
+      fe_store<F>(y, j * R + b, cmfma::recombine_redc<F>(Y));
+    }
+  }
+}
+
 // encode::reed_solomon (encode.rs:97-110): out[k] = sum_j in[j] (k+1)^j by Horner, per row b
 template <class F>
 __global__ __launch_bounds__(256) void k_reed_solomon(const uint32_t *__restrict__ in, size_t m,
@@ -53,9 +180,9 @@ __global__ __launch_bounds__(256) void k_reed_solomon(const uint32_t *__restrict
   if (t >= n_out * R) return;
   const size_t k = t / R;
   const uint32_t b = (uint32_t)(t - k * R);
-  const Fe<F> one = fe_one<F>();
-  Fe<F> x = one;
-  for (size_t i = 0; i < k; i++) x = fe_add<F>(x, one);
+  Fe<F> x = fe_zero<F>();  // the point k + 1 (k < 2^32), into Montgomery form by one multiply
+  x.v[0] = (uint32_t)(k + 1);
+  x = fe_to_mont<F>(x);
   Fe<F> r = fe_zero<F>();
   for (size_t jj = m; jj-- > 0;) r = fe_add<F>(fe_mul<F>(r, x), fe_load<F>(in, jj * R + b));
   fe_store<F>(out, t, r);
@@ -97,10 +224,41 @@ __global__ __launch_bounds__(256) void k_transpose(const uint32_t *__restrict__ 
   }
 }
 
+// rows per wave of k_spmm_mfma: chunks of at most 8 tiles (128 rows), as few 16-row tiles as cover R
+inline void mfma_tiling(size_t R, int &tiles, unsigned &chunks) {
+  chunks = (unsigned)((R + 127) / 128);
+  tiles = (int)((R + 16 * chunks - 1) / (16 * chunks));
+}
+
+template <class F, int TILES>
+void launch_spmm_mfma(const CsrDev &M, const uint32_t *x, uint32_t *y, size_t R, unsigned chunks,
+                      hipStream_t s) {
+  hipLaunchKernelGGL((k_spmm_mfma<F, TILES>), dim3((unsigned)((M.rows + 3) / 4), chunks), dim3(256), 0, s,
+                     M.gptr, M.pidx, M.hd, x, y, M.rows, (uint32_t)R);
+}
+
 template <class F>
-hipError_t spmm(const CsrDev &M, const uint32_t *x, uint32_t *y, size_t R, hipStream_t s) {
+hipError_t spmm(const SdigPlan &p, const CsrDev &M, const uint32_t *x, uint32_t *y, size_t R, hipStream_t s) {
   const size_t n = M.rows * R;
   if (!n) return hipSuccess;
+  if constexpr (F::N == 4 && F::ID == 1) {
+    if (p.mfma) {
+      int tiles;
+      unsigned chunks;
+      mfma_tiling(R, tiles, chunks);
+      switch (tiles) {
+        case 1: launch_spmm_mfma<F, 1>(M, x, y, R, chunks, s); break;
+        case 2: launch_spmm_mfma<F, 2>(M, x, y, R, chunks, s); break;
+        case 3: launch_spmm_mfma<F, 3>(M, x, y, R, chunks, s); break;
+        case 4: launch_spmm_mfma<F, 4>(M, x, y, R, chunks, s); break;
+        case 5: launch_spmm_mfma<F, 5>(M, x, y, R, chunks, s); break;
+        case 6: launch_spmm_mfma<F, 6>(M, x, y, R, chunks, s); break;
+        case 7: launch_spmm_mfma<F, 7>(M, x, y, R, chunks, s); break;
+        default: launch_spmm_mfma<F, 8>(M, x, y, R, chunks, s); break;
+      }
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((k_spmm<F>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M.ptr, M.idx,
                      M.val, x, y, M.rows, (uint32_t)R);
   return hipGetLastError();
@@ -117,13 +275,13 @@ hipError_t encode_cm(const SdigPlan &p, uint32_t *cw, size_t R, uint32_t *tmp, h
   for (int i = 0; i + 1 < L; i++) {
     const CsrDev &M = p.pre[i];
     const size_t in_end = in_start + M.cols;
-    if ((e = spmm<F>(M, cw + in_start * R * N, cw + in_end * R * N, R, s)) != hipSuccess) return e;
+    if ((e = spmm<F>(p, M, cw + in_start * R * N, cw + in_end * R * N, R, s)) != hipSuccess) return e;
     in_start = in_end;
   }
   // last precode into scratch, then Reed-Solomon into the codeword (:61-74)
   const CsrDev &ML = p.pre[L - 1];
   const size_t in_end = in_start + ML.cols;
-  if ((e = spmm<F>(ML, cw + in_start * R * N, tmp, R, s)) != hipSuccess) return e;
+  if ((e = spmm<F>(p, ML, cw + in_start * R * N, tmp, R, s)) != hipSuccess) return e;
   const size_t n_rs = p.post[L - 1].cols;
   if (n_rs * R) {
     hipLaunchKernelGGL((k_reed_solomon<F>), dim3((unsigned)((n_rs * R + 255) / 256)), dim3(256), 0,
@@ -136,7 +294,7 @@ hipError_t encode_cm(const SdigPlan &p, uint32_t *cw, size_t R, uint32_t *tmp, h
     in_pos -= p.pre[i].rows;
     const CsrDev &Q = p.post[i];
     if (out_pos - in_pos != Q.cols) return hipErrorInvalidValue;
-    if ((e = spmm<F>(Q, cw + in_pos * R * N, cw + out_pos * R * N, R, s)) != hipSuccess) return e;
+    if ((e = spmm<F>(p, Q, cw + in_pos * R * N, cw + out_pos * R * N, R, s)) != hipSuccess) return e;
     out_pos += Q.rows;
   }
   if (in_pos != p.pre[0].cols || out_pos != p.n_cols) return hipErrorInvalidValue;
@@ -144,6 +302,9 @@ hipError_t encode_cm(const SdigPlan &p, uint32_t *cw, size_t R, uint32_t *tmp, h
 }
 
 }  // namespace
+
+hipError_t sdig_plan_mfma(SdigPlan &plan, const std::vector<CsrHost> &pre, const std::vector<CsrHost> &post,
+                          hipStream_t s);
 
 hipError_t sdig_plan_upload(SdigPlan &plan, int fid, const std::vector<CsrHost> &pre,
                             const std::vector<CsrHost> &post, hipStream_t s) {
@@ -188,12 +349,85 @@ hipError_t sdig_plan_upload(SdigPlan &plan, int fid, const std::vector<CsrHost> 
     if ((e = put(pre[i], plan.pre[i])) != hipSuccess) return e;
   for (size_t i = 0; i < post.size(); i++)
     if ((e = put(post[i], plan.post[i])) != hipSuccess) return e;
+  if ((e = sdig_plan_mfma(plan, pre, post, s)) != hipSuccess) return e;
   return hipStreamSynchronize(s);  // host vectors may be freed after return
+}
+
+// The matrix-core forms of every level (Ft127; LCPC_SDIG_VALU=1 keeps the VALU kernel for A/B
+// runs).  Every output needs at most 4 SPMM_MAX_GROUPS nonzeros (the int32 accumulator bound).
+hipError_t sdig_plan_mfma(SdigPlan &plan, const std::vector<CsrHost> &pre, const std::vector<CsrHost> &post,
+                          hipStream_t s) {
+  plan.mfma = false;
+  const char *env = std::getenv("LCPC_SDIG_VALU");
+  if (plan.fid != Ft127::ID || (env && env[0] == '1')) return hipSuccess;
+  std::vector<const CsrHost *> hs;
+  std::vector<CsrDev *> ds;
+  for (size_t i = 0; i < pre.size(); i++) hs.push_back(&pre[i]), ds.push_back(&plan.pre[i]);
+  for (size_t i = 0; i < post.size(); i++) hs.push_back(&post[i]), ds.push_back(&plan.post[i]);
+  struct Form {
+    std::vector<uint32_t> gptr, pidx, src;
+  };
+  std::vector<Form> f(hs.size());
+  size_t total = 0, src_total = 0;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  for (size_t m = 0; m < hs.size(); m++) {
+    const CsrHost &h = *hs[m];
+    Form &F = f[m];
+    F.gptr.assign(h.rows + 1, 0);
+    for (size_t j = 0; j < h.rows; j++) {
+      const size_t nz = h.ptr[j + 1] - h.ptr[j];
+      if (nz > 4 * (size_t)SPMM_MAX_GROUPS) return hipSuccess;  // VALU kernel for this plan
+      F.gptr[j + 1] = F.gptr[j] + (uint32_t)((nz + 3) / 4);
+    }
+    const size_t groups = F.gptr[h.rows];
+    F.pidx.assign(4 * groups, 0);
+    F.src.assign(4 * groups, ~0u);
+    for (size_t j = 0; j < h.rows; j++)
+      for (uint32_t k = h.ptr[j], q = 4 * F.gptr[j]; k < h.ptr[j + 1]; k++, q++) {
+        F.pidx[q] = h.idx[k];
+        F.src[q] = k;
+      }
+    total += al((h.rows + 1) * 4) + al(4 * groups * 4) + al(4 * groups * 256);
+    src_total = std::max(src_total, al(4 * groups * 4));
+  }
+  hipError_t e = hipMalloc(&plan.d_mfma, total ? total : 256);
+  if (e != hipSuccess) return e;
+  void *d_src = nullptr;
+  if ((e = hipMalloc(&d_src, src_total ? src_total : 256)) != hipSuccess) return e;
+  uint8_t *cur = (uint8_t *)plan.d_mfma;
+  for (size_t m = 0; m < hs.size() && e == hipSuccess; m++) {
+    const CsrHost &h = *hs[m];
+    CsrDev &d = *ds[m];
+    const Form &F = f[m];
+    d.groups = F.gptr[h.rows];
+    d.gptr = (const uint32_t *)cur;
+    d.pidx = (const uint32_t *)(cur + al((h.rows + 1) * 4));
+    d.hd = cur + al((h.rows + 1) * 4) + al(4 * d.groups * 4);
+    e = hipMemcpyAsync((void *)d.gptr, F.gptr.data(), F.gptr.size() * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && d.groups)
+      e = hipMemcpyAsync((void *)d.pidx, F.pidx.data(), F.pidx.size() * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && d.groups)
+      e = hipMemcpyAsync(d_src, F.src.data(), F.src.size() * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && d.groups) {
+      const size_t n = 4 * d.groups * 16;
+      hipLaunchKernelGGL((k_sdig_hdig<Ft127>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d.val,
+                         (const uint32_t *)d_src, 4 * d.groups, (uint8_t *)d.hd);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // d_src is reused by the next matrix
+    cur += al((h.rows + 1) * 4) + al(4 * d.groups * 4) + al(4 * d.groups * 256);
+  }
+  (void)hipFree(d_src);
+  if (e == hipSuccess) plan.mfma = true;
+  return e;
 }
 
 void sdig_plan_free(SdigPlan &plan) {
   if (plan.d_buf) (void)hipFree(plan.d_buf);
+  if (plan.d_mfma) (void)hipFree(plan.d_mfma);
   plan.d_buf = nullptr;
+  plan.d_mfma = nullptr;
+  plan.mfma = false;
   plan.pre.clear();
   plan.post.clear();
 }

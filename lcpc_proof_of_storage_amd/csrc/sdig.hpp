@@ -54,6 +54,12 @@ size_t sdig_codeword_length(const std::vector<CsrHost> &pre, const std::vector<C
 struct CsrDev {
   size_t rows = 0, cols = 0, nnz = 0;
   const uint32_t *ptr = nullptr, *idx = nullptr, *val = nullptr;
+  // Ft127 matrix-core form (sdig.hip, k_spmm_mfma): every output's nonzeros padded to groups of
+  // 4; gptr[j] = first group of output j, pidx = input index per padded nonzero, hd = the
+  // balanced digits h[k][a][u] of val_k 2^(8a) mod p, 256 B per padded nonzero (zero for pads)
+  const uint32_t *gptr = nullptr, *pidx = nullptr;
+  const uint8_t *hd = nullptr;
+  size_t groups = 0;
 };
 struct SdigPlan {
   int fid = -1;
@@ -61,6 +67,8 @@ struct SdigPlan {
   std::vector<CsrDev> pre, post;
   size_t tmp_elems = 0;      // scratch elements per row (last precode output)
   void *d_buf = nullptr;     // one allocation holding every matrix
+  void *d_mfma = nullptr;    // the matrix-core forms (Ft127), when every level has one
+  bool mfma = false;
 };
 hipError_t sdig_plan_upload(SdigPlan &plan, int fid, const std::vector<CsrHost> &pre,
                             const std::vector<CsrHost> &post, hipStream_t s);

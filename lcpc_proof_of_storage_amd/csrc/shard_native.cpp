@@ -164,13 +164,27 @@ struct Xop {
   std::vector<size_t> sb, rb;  // ALL_TO_ALL: bytes to / from each rank
   int root = 0;
   hipEvent_t ready = nullptr;
+  hipStream_t s = nullptr;  // the producing polynomial's compute stream
 };
 
 // Issues one group of exchanges on the comm stream; `done` events are recorded after it.
 lcpc_status run_group(lcpc_comm *c, std::vector<Xop> &ops, const std::vector<hipEvent_t> &done) {
   const int G = c->nranks, me = c->rank;
   hipStream_t cs = c->cs;
-  if (c->is_rccl || G == 1) {
+  if (G == 1) {
+    // one rank: nothing crosses a process, so each exchange is its own-piece copy on the
+    // polynomial's stream (no comm stream: polynomials in flight do not wait for each other)
+    for (size_t i = 0; i < ops.size(); i++) {
+      const Xop &op = ops[i];
+      if (op.kind == Xop::ALL_GATHER && op.bytes)
+        HIP_TRY(hipMemcpyAsync(op.recv, op.send, op.bytes, hipMemcpyDeviceToDevice, op.s));
+      if (op.kind == Xop::ALL_TO_ALL && op.rb[0])
+        HIP_TRY(hipMemcpyAsync(op.recv, op.send, op.rb[0], hipMemcpyDeviceToDevice, op.s));
+      if (i < done.size()) HIP_TRY(hipEventRecord(done[i], op.s));
+    }
+    return LCPC_OK;
+  }
+  if (c->is_rccl) {
     for (auto &op : ops)
       if (op.ready) HIP_TRY(hipStreamWaitEvent(cs, op.ready, 0));
     // own pieces: device copies on the comm stream
@@ -280,7 +294,8 @@ struct HostBuf {
   ~HostBuf() {
     if (p) d->pinned_put(p);
   }
-  lcpc_status get(Device *dev, size_t n) {
+  lcpc_status get(Device *dev, size_t n) {  // (any previous block: its copies have completed)
+    if (p) d->pinned_put(p);
     d = dev;
     p = (uint8_t *)dev->pinned_get(n);
     return p ? LCPC_OK : fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
@@ -302,7 +317,7 @@ struct lcpc_sharded_commit {
   hipEvent_t ev_done = nullptr;   // the last exchange completed (comm stream)
   hipEvent_t ev_host = nullptr;   // device -> host copies of the last stage landed
   DBuf coeffs, comm_rows, hashes;  // kept for prove
-  DBuf cv_send, cv_recv, sub, subs;  // commit scratch
+  DBuf cv, cv_send, cv_recv, sub, subs;  // commit scratch
   uint8_t root[32] = {0};
   // prove state
   int root_rank = 0;
@@ -310,7 +325,7 @@ struct lcpc_sharded_commit {
   lcpc_transcript *tr = nullptr;
   bool own_tr = false;
   DBuf bt, tens, part_d, allpart, sum, canon, didx, mycols, allcols, dpaths, scratch;
-  HostBuf h_root, h_t, h_sum, h_repr, h_repr_eval, h_idx, h_cols, h_paths;
+  HostBuf h_root, h_t, h_sum, h_repr, h_repr_eval, h_idx, h_cols, h_paths, h_outer;
   std::vector<uint64_t> p_random, p_eval, col_idx;
   std::future<lcpc_status> next;  // root rank: the next challenge vector is in h_t / h_idx
   ~lcpc_sharded_commit() {
@@ -408,8 +423,9 @@ lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
                      c->s, c->coeffs.as<uint32_t>(), c->np, true));
   }
   if (nch) {
-    DBuf cv;
-    HIP_TRY(salloc(c, cv, nch * c->nc * 32));
+    // (a member, released once the commit is complete: a local would drain the stream here)
+    HIP_TRY(salloc(c, c->cv, nch * c->nc * 32));
+    DBuf &cv = c->cv;
     HIP_TRY(leaf_chunk_cvs(c->fid, c->comm_rows.as<uint32_t>(), pm.r_lo, c->n_rows, c->nc, c->nc, pm.c_lo, pm.c_hi,
                            cv.as<uint32_t>(), c->s, true));
     // [chunk][G][B] -> [G][chunk][B]
@@ -431,6 +447,7 @@ Xop op_cv_exchange(lcpc_sharded_commit *c) {
   op.rb.resize(c->G);
   for (int k = 0; k < c->G; k++) op.rb[k] = (c->part[k].c_hi - c->part[k].c_lo) * c->B * 32;
   op.ready = c->ev_ready;
+  op.s = c->s;
   return op;
 }
 
@@ -451,6 +468,7 @@ Xop op_subtree_exchange(lcpc_sharded_commit *c) {
   op.recv = c->subs.as<uint8_t>();
   op.bytes = (2 * c->B - 1) * 32;
   op.ready = c->ev_ready;
+  op.s = c->s;
   return op;
 }
 
@@ -478,6 +496,9 @@ lcpc_status stage_post_subtrees(lcpc_sharded_commit *c) {
 lcpc_status finish_commit(lcpc_sharded_commit *c) {
   HIP_TRY(hipEventSynchronize(c->ev_host));
   std::memcpy(c->root, c->h_root.p, 32);
+  // every use of the commit scratch precedes ev_host on the stream: no drain on release
+  for (DBuf *b : {&c->cv, &c->cv_send, &c->cv_recv, &c->sub, &c->subs}) b->settle();
+  c->cv.reset();
   c->cv_send.reset();
   c->cv_recv.reset();
   c->sub.reset();
@@ -505,12 +526,11 @@ lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_r
   // the outer tensor's slice (host -> device once per proof)
   if ((st = c->h_t.get(c->dev, c->n_rows * wb))) return st;
   if ((st = c->h_idx.get(c->dev, std::max<size_t>(c->nco, 1) * 8))) return st;
-  if (c->nr) {
-    HostBuf h_outer;
-    if ((st = h_outer.get(c->dev, c->nr * wb))) return st;
-    std::memcpy(h_outer.p, (const uint8_t *)outer + c->part[c->me].r_lo * wb, c->nr * wb);
-    HIP_TRY(hipMemcpyAsync(c->tens.as<uint8_t>() + c->nr * wb, h_outer.p, c->nr * wb, hipMemcpyHostToDevice, c->s));
-    HIP_TRY(hipStreamSynchronize(c->s));  // before h_outer returns to the pool
+  if (c->nr) {  // (h_outer lives until the proof is released, so the copy needs no drain here)
+    if ((st = c->h_outer.get(c->dev, c->nr * wb))) return st;
+    std::memcpy(c->h_outer.p, (const uint8_t *)outer + c->part[c->me].r_lo * wb, c->nr * wb);
+    HIP_TRY(hipMemcpyAsync(c->tens.as<uint8_t>() + c->nr * wb, c->h_outer.p, c->nr * wb, hipMemcpyHostToDevice,
+                           c->s));
   }
   if (c->me == root_rank) {
     HIP_TRY(salloc(c, c->allpart, (size_t)c->G * 2 * np * wb));
@@ -549,13 +569,17 @@ Xop op_tensor_bcast(lcpc_sharded_commit *c, size_t r) {
   op.recv = c->bt.as<uint8_t>();
   op.bytes = (r < c->ndt) ? c->n_rows * c->wb : 0;
   op.root = c->root_rank;
+  op.s = c->s;
   return op;
 }
+
+// the root's host -> device challenge copies go on the stream its exchanges run on
+hipStream_t upload_stream(const lcpc_sharded_commit *c) { return c->G == 1 ? c->s : c->comm->cs; }
 
 // root: the challenge vector onto the comm stream before the exchange group is issued
 lcpc_status stage_tensor_upload(lcpc_sharded_commit *c, size_t r) {
   if (c->me != c->root_rank || r >= c->ndt) return LCPC_OK;
-  HIP_TRY(hipMemcpyAsync(c->bt.p, c->h_t.p, c->n_rows * c->wb, hipMemcpyHostToDevice, c->comm->cs));
+  HIP_TRY(hipMemcpyAsync(c->bt.p, c->h_t.p, c->n_rows * c->wb, hipMemcpyHostToDevice, upload_stream(c)));
   return LCPC_OK;
 }
 
@@ -592,6 +616,7 @@ Xop op_partial_gather(lcpc_sharded_commit *c, size_t r) {
   op.sb[c->root_rank] = bytes;
   if (c->me == c->root_rank) op.rb.assign(c->G, bytes);
   op.ready = c->ev_ready;
+  op.s = c->s;
   return op;
 }
 
@@ -654,12 +679,13 @@ Xop op_idx_bcast(lcpc_sharded_commit *c) {
   op.recv = c->didx.as<uint8_t>();
   op.bytes = c->nco * 8;
   op.root = c->root_rank;
+  op.s = c->s;
   return op;
 }
 
 lcpc_status stage_idx_upload(lcpc_sharded_commit *c) {
   if (c->me != c->root_rank || !c->nco) return LCPC_OK;
-  HIP_TRY(hipMemcpyAsync(c->didx.p, c->h_idx.p, c->nco * 8, hipMemcpyHostToDevice, c->comm->cs));
+  HIP_TRY(hipMemcpyAsync(c->didx.p, c->h_idx.p, c->nco * 8, hipMemcpyHostToDevice, upload_stream(c)));
   return LCPC_OK;
 }
 
@@ -683,6 +709,7 @@ Xop op_cols_gather(lcpc_sharded_commit *c) {
   if (c->me == c->root_rank)
     for (int k = 0; k < c->G; k++) op.rb[k] = c->nco * (c->part[k].r_hi - c->part[k].r_lo) * c->wb;
   op.ready = c->ev_ready;
+  op.s = c->s;
   return op;
 }
 
@@ -944,8 +971,13 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
       if (c && c->next.valid()) c->next.wait();
     return fail(s2, msg);
   };
-  if ((st = start(0))) return st;
+  // polynomial k's encode is launched two ticks before its chaining-value exchange, so a tick's
+  // exchange group (which waits for every producer in it) does not wait on a just-launched encode
+  constexpr size_t AHEAD = 2;
+  for (size_t k = 0; k < std::min(AHEAD, n_polys); k++)
+    if ((st = start(k))) return k ? fail_all(st) : st;
   for (size_t t = 0; t < n_ticks; t++) {
+    prof::HostScope hs_tick("tick_total");
     std::vector<Xop> ops;
     std::vector<hipEvent_t> done;
     std::vector<std::pair<size_t, size_t>> items;  // (poly, stage)
@@ -959,6 +991,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
         ops.push_back(op_subtree_exchange(c));
       } else if (s == S_IDX) {
         if (c->me == c->root_rank) {
+          prof::HostScope hs("tick_wait_challenge");
           if ((st = c->next.get())) return fail_all(st);
         }
         if ((st = stage_idx_upload(c))) return fail_all(st);
@@ -970,16 +1003,21 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
         if ((s - S_R0) % 2 == 0) {
           if (r == 0) {
             // the commit is complete (root on the host) and the transcript exists
-            if ((st = finish_commit(c))) return fail_all(st);
+            {
+              prof::HostScope hs("tick_wait_root");
+              if ((st = finish_commit(c))) return fail_all(st);
+            }
             if (roots) std::memcpy(roots + 32 * k, c->root, 32);
             lcpc_transcript *tr = nullptr;
             if (me == (int)(k % G)) {
               tr = make_transcript(user, k, c->root);
               if (!tr) return fail_all(fail(LCPC_ERR_INVALID_ARG, "make_transcript returned NULL"));
             }
+            prof::HostScope hs("tick_prove_init");
             if ((st = prove_init(c, outer, (int)(k % G), tr, true))) return fail_all(st);
             if (me == c->root_rank && (st = challenge_first(c))) return fail_all(st);
           } else if (c->me == c->root_rank) {
+            prof::HostScope hs("tick_wait_challenge");
             if ((st = c->next.get())) return fail_all(st);
           }
           if ((st = stage_tensor_upload(c, r))) return fail_all(st);
@@ -991,8 +1029,12 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
       done.push_back(c->ev_done);
       items.emplace_back(k, s);
     }
-    if (!ops.empty() && (st = run_group(comm, ops, done))) return fail_all(st);
+    if (!ops.empty()) {
+      prof::HostScope hs("tick_run_group");
+      if ((st = run_group(comm, ops, done))) return fail_all(st);
+    }
     // the compute each exchange feeds, on the polynomials' own streams
+    prof::HostScope hs_compute("tick_compute");
     for (auto [k, s] : items) {
       lcpc_sharded_commit *c = cs[k].get();
       if (s == S_CV) {
@@ -1023,7 +1065,8 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
       }
       if (st) return fail_all(st);
     }
-    if (t + 1 < n_polys && (st = start(t + 1))) return fail_all(st);
+    prof::HostScope hs_start("tick_start");
+    if (t + AHEAD < n_polys && (st = start(t + AHEAD))) return fail_all(st);
   }
   lcpc_status first = LCPC_OK;
   std::string msg;

@@ -14,7 +14,11 @@
 
 namespace lcpc {
 
-void keccak_f1600(uint64_t st[25]);
+void keccak_f1600(uint64_t st[25]);         // the fastest the host CPU runs (AVX-512F if present)
+void keccak_f1600_scalar(uint64_t st[25]);  // any x86-64
+void keccak_f1600_avx512(uint64_t st[25]);  // needs AVX-512F
+const char *keccak_impl();                  // "avx512" or "scalar"
+
 
 class Strobe128 {
  public:
@@ -22,9 +26,8 @@ class Strobe128 {
   void meta_ad(const uint8_t *d, size_t n, bool more);
   void ad(const uint8_t *d, size_t n, bool more);
   void prf(uint8_t *d, size_t n, bool more);
-  // meta_AD(label); meta_AD(len, more); AD(msg) in one XOR pass when the record fits before the
-  // rate boundary (r = prepared record with label/len/flag bytes filled in); false otherwise
-  bool append_record_fast(uint8_t *r, size_t rec, size_t ln, const uint8_t *msg, size_t msg_len);
+  // n merlin append_message(label, msg_i) records (ln, ml <= 64), absorbed block by block
+  void append_records(const uint8_t *label, size_t ln, const uint8_t *msgs, size_t ml, size_t n);
 
  private:
   void run_f();
