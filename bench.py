@@ -50,10 +50,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=16)
-    ap.add_argument("--mode", choices=["sharded", "replicas"], default="sharded",
+    ap.add_argument("--mode", choices=["auto", "sharded", "replicas"], default="auto",
                     help="sharded: one commitment per step, rows split over the ranks (the library's "
                          "pipelined driver; the BASELINE cfg3 configuration); replicas: independent "
-                         "commitments per rank on host threads (ligero only)")
+                         "commitments per rank on host threads; auto (default): sharded for --gpus > 1, "
+                         "replicas on one GPU, where there is nothing to split and independent "
+                         "commitments in flight are the faster single-GPU engine")
     ap.add_argument("--lag", type=int, default=0,
                     help="sharded driver: ticks between a row-combination gather and the next challenge "
                          "broadcast (0: the library's choice)")
@@ -85,6 +87,12 @@ def parse():
                     help="verifies of one proof timed after the timed region (ligero/sdig; 0: skip)")
     ap.add_argument("--roofline-steps", type=int, default=3,
                     help="serial steps after the timed region whose encode launches give the roofline")
+    ap.add_argument("--commit-slots", type=int, default=-1,
+                    help="replicas (ligero / sdig): commits admitted to the GPU at once, first come first "
+                         "served (0: no limit; default 4, 2 for --code sdig, from a sweep on the box).  "
+                         "Commits then finish in order and each proof's serial host "
+                         "transcript starts while later commits run, instead of every commit of a wave "
+                         "finishing together at its end")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="independent commitments in flight per GPU (host threads); the serial "
                          "Merlin transcript of one overlaps the kernels of the others.  0: 16, or "
@@ -93,8 +101,12 @@ def parse():
     args = ap.parse_args()
     if args.code != "ligero":
         args.mode = "replicas"  # cfg2 / cfg4 / cfg5 run as independent steps per rank
+    if args.mode == "auto":
+        args.mode = "sharded" if args.gpus > 1 else "replicas"
     if args.log_len is None:
         args.log_len = 20 if args.code == "encode" else 24
+    if args.commit_slots < 0:
+        args.commit_slots = 2 if args.code == "sdig" else 4
     if args.pipeline <= 0:
         args.pipeline = 4 if args.code == "pos" else 16
     return args
@@ -187,8 +199,14 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
     outer = L.field_random(fid, n_rows, 7)  # prove accepts any outer tensor of n_rows elements
     d_coeffs = torch.from_numpy(coeffs.view(np.int64)).to(f"cuda:{local_rank}")
 
+    gate = threading.Semaphore(args.commit_slots) if args.commit_slots > 0 else None
+
     def step(slot):
-        c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+        if gate is not None:
+            with gate:
+                c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+        else:
+            c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
         root = c.get_root()
         tr = L.Transcript(b"test transcript")
         tr.append_message(b"polycommit", root)
@@ -266,6 +284,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                 "n_col_opens": nco, "n_degree_tests": ndt},
         step=step, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify, latency=latency,
+        prepare=lambda: enc.prepare_thread(n_rows), reserve=lambda count: enc.reserve(n, count),
         enc_kernels=("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=("sdig_encode = transpose + 13 SpMM / Reed-Solomon levels (per commit, all rows)" if sdig
                          else f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
@@ -777,8 +796,8 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     else:
         P = max(d for d in range(1, P + 1) if args.steps % d == 0)
     n_workers = P
-    warm_each = max(1, -(-args.warmup // n_workers))  # every worker warms its own pinned staging
-    warmup_done = warm_each * n_workers
+    warm_left = [max(0, args.warmup)]  # exactly --warmup untimed steps, over whichever workers
+    warmup_done = warm_left[0]
 
     def barrier():
         sync_barrier(dist, torch.cuda.synchronize)
@@ -791,7 +810,13 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
 
     def worker(slot):
         try:
-            for _ in range(warm_each):
+            if getattr(wl, "prepare", None):
+                wl.prepare()  # this thread's pinned staging (the library's per-thread slots)
+            while True:
+                with lock:
+                    if warm_left[0] <= 0:
+                        break
+                    warm_left[0] -= 1
                 wl.step(slot)
         except Exception as e:  # surface after the join
             errors.append(e)
@@ -808,6 +833,8 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
                 errors.append(e)
                 return
 
+    if getattr(wl, "reserve", None):
+        wl.reserve(n_workers + 1)  # device pool blocks and streams of every concurrent step (not steps)
     workers = [threading.Thread(target=worker, args=(i,)) for i in range(n_workers)]
     for w in workers:
         w.start()

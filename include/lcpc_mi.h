@@ -137,6 +137,14 @@ size_t lcpc_encoding_n_col_opens(const lcpc_encoding *e);
 size_t lcpc_encoding_n_degree_tests(const lcpc_encoding *e);
 size_t lcpc_encoding_n_per_row(const lcpc_encoding *e);
 size_t lcpc_encoding_n_cols(const lcpc_encoding *e);
+/* Pre-allocates the calling thread's page-locked staging for lcpc_prove on commitments of
+ * n_rows rows under e (host only).  Optional: a thread's first prove otherwise pays the
+ * hipHostMalloc.  No reference counterpart (rayon threads have no device staging). */
+lcpc_status lcpc_prepare_thread(const lcpc_encoding *e, size_t n_rows);
+/* Pre-allocates into the device pool the buffers and streams of `count` concurrent
+ * commit + prove calls on `len` coefficients under e (otherwise the first calls at a new
+ * concurrency pay hipMalloc / hipStreamCreate).  Optional. */
+lcpc_status lcpc_reserve(const lcpc_encoding *e, size_t len, size_t count);
 /* LcEncoding::encode (lcpc-2d/src/lib.rs:92; Ligero: fft_io_pc, lcpc-ligero-pc/src/lib.rs:
  * 162-164): in place on `len` elements (must equal n_cols) of host memory. */
 lcpc_status lcpc_encode(const lcpc_encoding *e, uint64_t *inp, size_t len);

@@ -68,6 +68,8 @@ SIGNATURES = {
     "lcpc_encoding_dims_ok": (i32, [vp, sz, sz]),
     "lcpc_encoding_n_col_opens": (sz, [vp]),
     "lcpc_encoding_n_degree_tests": (sz, [vp]),
+    "lcpc_prepare_thread": (i32, [vp, sz]),
+    "lcpc_reserve": (i32, [vp, sz, sz]),
     "lcpc_encoding_n_per_row": (sz, [vp]),
     "lcpc_encoding_n_cols": (sz, [vp]),
     "lcpc_encode": (i32, [vp, u64p, sz]),

@@ -443,6 +443,35 @@ hipError_t merkle_tree(uint8_t *hashes, size_t np2, hipStream_t s) {
   return hipSuccess;
 }
 
+namespace {
+// Row shards: rank g's subtree over column block g ([B leaves | B/2 | ... | 1], B a power of
+// two) is level l, positions [g B/2^l, (g + 1) B/2^l) of the whole tree.  One thread per
+// 16 bytes of digest.
+__global__ __launch_bounds__(256) void k_assemble_subtrees(const uint4 *__restrict__ subs, size_t B, size_t G,
+                                                           uint4 *__restrict__ tree) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t per = 2 * B - 1;
+  if (t >= 2 * G * per) return;
+  const size_t dig = t >> 1, g = dig / per, sidx = dig - g * per;
+  size_t off = 0, w = B, l = 0;
+  while (sidx >= off + w) {
+    off += w;
+    w >>= 1;
+    l++;
+  }
+  const size_t nc = G * B, lvl_off = 2 * nc - 2 * (nc >> l);
+  tree[2 * (lvl_off + g * w + (sidx - off)) + (t & 1)] = subs[t];
+}
+}  // namespace
+
+hipError_t assemble_subtrees(const uint8_t *subs, size_t B, size_t G, uint8_t *tree, hipStream_t s) {
+  const size_t n = 2 * G * (2 * B - 1);
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_assemble_subtrees, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const uint4 *)subs, B,
+                     G, (uint4 *)tree);
+  return hipGetLastError();
+}
+
 hipError_t merkle_tree_io(const uint8_t *ins, size_t n_ins, uint8_t *outs, hipStream_t s) {
   // requires outs to directly follow ins in one buffer (as lcpc-2d's `hashes` split)
   if (outs != ins + 32 * n_ins) return hipErrorInvalidValue;

@@ -65,6 +65,9 @@ hipError_t leaf_hashes_cols(int fid, const uint32_t *cols, size_t n_rows, size_t
 hipError_t merkle_tree(uint8_t *hashes, size_t np2, hipStream_t s);
 // generic Merkle over ins (n_ins = outs + 1 nodes, power of two) -> outs
 hipError_t merkle_tree_io(const uint8_t *ins, size_t n_ins, uint8_t *outs, hipStream_t s);
+// row shards: G subtrees of 2B - 1 digests (column block g, levels leaves..root, B a power of
+// two) into levels 0..log2(B) of the whole tree of G B leaves ([leaves | level 1 | ...] layout)
+hipError_t assemble_subtrees(const uint8_t *subs, size_t B, size_t G, uint8_t *tree, hipStream_t s);
 
 // ------------------------------------------------------------------ prover helpers
 // out[t][c] = sum_r tensors[t][r] * coeffs[r][c]   (t < n_tensors, c < n_per_row)

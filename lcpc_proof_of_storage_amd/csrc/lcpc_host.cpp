@@ -332,10 +332,56 @@ size_t lcpc_encoding_n_degree_tests(const lcpc_encoding *e) { return e->n_degree
 size_t lcpc_encoding_n_per_row(const lcpc_encoding *e) { return e->n_per_row; }
 size_t lcpc_encoding_n_cols(const lcpc_encoding *e) { return e->n_cols; }
 
-lcpc_status lcpc_encode_rows(const lcpc_encoding *e, uint64_t *rows, size_t n_rows, size_t stride) {
-  if (!e || (!rows && n_rows)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
-  if (stride < e->n_cols) return fail(LCPC_ERR_INVALID_ARG, "row stride < n_cols");
-  if (n_rows == 0) return LCPC_OK;
+lcpc_status lcpc_reserve(const lcpc_encoding *e, size_t len, size_t count) {
+  if (!e || !len) return fail(LCPC_ERR_INVALID_ARG, "reserve arguments");
+  Device *dev = e->dev;
+  HIP_TRY(hipSetDevice(dev->id));
+  const size_t wb = (size_t)field_bytes(e->fid), np = e->n_per_row, nc = e->n_cols, nco = e->n_col_opens;
+  const size_t nr = (len + np - 1) / np, np2 = next_pow2(nc), pl = log2_np2(nc);
+  // the blocks commit_device and lcpc_prove ask of the pool, by size
+  std::vector<size_t> sizes = {nr * np * wb, nr * nc * wb, (2 * np2 - 1) * 32,
+                               leaf_hash_scratch_bytes(e->fid, nr, nc), 2 * nr * wb, 2 * np * wb,
+                               collapse_scratch_bytes(e->fid, nr, np, 2), np * wb, nco * 8, nco * nr * wb,
+                               nco * pl * 32};
+  if (e->kind == KIND_SDIG) sizes.push_back(e->sdig.tmp_elems * nr * wb);
+  std::vector<void *> blocks;
+  lcpc_status st = LCPC_OK;
+  for (size_t k = 0; k < count && !st; k++)
+    for (size_t b : sizes) {
+      void *p = nullptr;
+      if (dev->alloc(&p, b) != hipSuccess) {
+        st = fail(LCPC_ERR_OUT_OF_MEMORY, "reserve: device pool");
+        break;
+      }
+      blocks.push_back(p);
+    }
+  for (void *p : blocks) dev->release(p);
+  std::vector<hipStream_t> lo, hi;
+  for (size_t k = 0; k < count; k++) {
+    lo.push_back(dev->acquire_stream(false));
+    hi.push_back(dev->acquire_stream(true));
+  }
+  for (hipStream_t s : lo)
+    if (s) dev->release_stream(s, false);
+  for (hipStream_t s : hi)
+    if (s) dev->release_stream(s, true);
+  return st;
+}
+
+lcpc_status lcpc_prepare_thread(const lcpc_encoding *e, size_t n_rows) {
+  if (!e) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  // the sizes lcpc_prove asks of each thread-local slot
+  const size_t wb = (size_t)field_bytes(e->fid), np = e->n_per_row, nco = e->n_col_opens;
+  const size_t ndt = e->n_degree_tests, pl = log2_np2(e->n_cols);
+  const size_t want[PIN_N] = {2 * np * wb, std::max<size_t>(1, ndt) * np * wb, np * wb,
+                              std::max<size_t>(1, nco * n_rows * wb), nco * pl * 32 + nco * 8, n_rows * wb,
+                              n_rows * wb};
+  for (int i = 0; i < PIN_N; i++)
+    if (!t_pin[i].get(std::max<size_t>(1, want[i]))) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  return LCPC_OK;
+}
+
+static lcpc_status encode_rows_chunk(const lcpc_encoding *e, uint64_t *rows, size_t n_rows, size_t stride) {
   Device *dev = e->dev;
   Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
@@ -351,6 +397,42 @@ lcpc_status lcpc_encode_rows(const lcpc_encoding *e, uint64_t *rows, size_t n_ro
                            hipMemcpyDeviceToHost, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
+}
+
+lcpc_status lcpc_encode_rows(const lcpc_encoding *e, uint64_t *rows, size_t n_rows, size_t stride) {
+  if (!e || (!rows && n_rows)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (stride < e->n_cols) return fail(LCPC_ERR_INVALID_ARG, "row stride < n_cols");
+  if (n_rows == 0) return LCPC_OK;
+  // The rows are the caller's pageable memory, so one stream's H2D -> encode -> D2H runs
+  // serially.  Chunks of ~16 MiB on up to 8 host threads (each with its own leased stream)
+  // overlap one chunk's copies with another's kernels, as concurrent per-row callers do
+  // (tools/encode_rows_bench.py at the cfg3 row size: 62 GB/s of H2D + D2H for 16 callers
+  // against 52 GB/s for the whole batch on one stream).
+  const size_t row_bytes = e->n_cols * (size_t)field_bytes(e->fid);
+  const size_t chunk = std::max<size_t>(1, ((size_t)16 << 20) / row_bytes);
+  const size_t n_chunks = (n_rows + chunk - 1) / chunk;
+  if (n_chunks < 2) return encode_rows_chunk(e, rows, n_rows, stride);
+  const size_t T = std::min<size_t>(8, n_chunks);
+  std::atomic<size_t> next{0};
+  std::mutex mu;
+  lcpc_status first = LCPC_OK;
+  std::string msg;
+  auto work = [&] {
+    for (size_t k; (k = next.fetch_add(1)) < n_chunks;) {
+      const size_t r0 = k * chunk, nr = std::min(chunk, n_rows - r0);
+      const lcpc_status st = encode_rows_chunk(e, rows + r0 * stride * (size_t)field_info(e->fid).limbs, nr, stride);
+      if (st) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!first) first = st, msg = g_err;
+        next.store(n_chunks);
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < T; i++) th.emplace_back(work);
+  work();
+  for (auto &t : th) t.join();
+  return first ? fail(first, msg) : LCPC_OK;
 }
 
 lcpc_status lcpc_encode(const lcpc_encoding *e, uint64_t *inp, size_t len) {

@@ -35,11 +35,12 @@ __global__ __launch_bounds__(256) void k_spmm(const uint32_t *__restrict__ ptr,
                                               const uint32_t *__restrict__ idx,
                                               const uint32_t *__restrict__ val,
                                               const uint32_t *__restrict__ x,
-                                              uint32_t *__restrict__ y, size_t m, uint32_t R) {
+                                              uint32_t *__restrict__ y, size_t m, uint32_t R,
+                                              uint32_t b0, uint32_t nb) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= m * R) return;
-  const size_t j = t / R;
-  const uint32_t b = (uint32_t)(t - j * R);
+  if (t >= m * nb) return;
+  const size_t j = t / nb;
+  const uint32_t b = b0 + (uint32_t)(t - j * nb);
   Fe<F> acc = fe_zero<F>();
   const uint32_t k1 = ptr[j + 1];
   uint32_t k = ptr[j];
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(256) void k_spmm(const uint32_t *__restrict__ ptr,
   }
   for (; k < k1; k++)
     acc = fe_add<F>(acc, fe_mul<F>(fe_load<F>(val, k), fe_load<F>(x, (size_t)idx[k] * R + b)));
-  fe_store<F>(y, t, acc);
+  fe_store<F>(y, j * R + b, acc);
 }
 
 // hd[(kk 16 + u) 16 + a] = byte u of the balanced digits of val[src[kk]] 2^(8a) mod p, zero for
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ 
                                                    const uint32_t *__restrict__ pidx,
                                                    const uint8_t *__restrict__ hd,
                                                    const uint32_t *__restrict__ x,
-                                                   uint32_t *__restrict__ y, size_t m, uint32_t R) {
+                                                   uint32_t *__restrict__ y, size_t m, uint32_t R,
+                                                   uint32_t row0, uint32_t row_end) {
   static_assert(F::N == 4, "Ft127 layout");
   __shared__ int red[4][TILES][16][17];
   __shared__ uint32_t nbr[4][4 * SPMM_MAX_GROUPS];
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ 
   const size_t j = (size_t)blockIdx.x * 4 + wave;
   if (j >= m) return;  // whole waves only: the kernel synchronises within a wave
   const int n = lane & 15, g = lane >> 4;
-  const size_t b0 = (size_t)blockIdx.y * TILES * 16;
+  const size_t b0 = row0 + (size_t)blockIdx.y * TILES * 16;
   const uint32_t q0 = gptr[j], nq = gptr[j + 1] - q0;
   uint32_t *nb = nbr[wave];
   for (uint32_t i = lane; i < 4 * nq; i += 64) nb[i] = pidx[4 * (size_t)q0 + i];
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ 
   const uint4 *h4 = reinterpret_cast<const uint4 *>(hd);
   bool rowok[TILES];
 #pragma unroll
-  for (int t = 0; t < TILES; t++) rowok[t] = b0 + 16 * t + n < R;
+  for (int t = 0; t < TILES; t++) rowok[t] = b0 + 16 * t + n < row_end;
   cmfma::v4i acc[TILES];
 #pragma unroll
   for (int t = 0; t < TILES; t++) acc[t] = cmfma::v4i{0, 0, 0, 0};
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ 
   for (int p = 0; p < TILES; p += 4) {
     const int t = p + g;
     const size_t b = b0 + 16 * (size_t)t + n;
-    if (t < TILES && b < R) {
+    if (t < TILES && b < row_end) {
       int Y[16];
 #pragma unroll
       for (int u = 0; u < 16; u++) Y[u] = rw[t][u][n];
@@ -175,17 +177,17 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ 
 template <class F>
 __global__ __launch_bounds__(256) void k_reed_solomon(const uint32_t *__restrict__ in, size_t m,
                                                       uint32_t *__restrict__ out, size_t n_out,
-                                                      uint32_t R) {
+                                                      uint32_t R, uint32_t b0, uint32_t nb) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_out * R) return;
-  const size_t k = t / R;
-  const uint32_t b = (uint32_t)(t - k * R);
+  if (t >= n_out * nb) return;
+  const size_t k = t / nb;
+  const uint32_t b = b0 + (uint32_t)(t - k * nb);
   Fe<F> x = fe_zero<F>();  // the point k + 1 (k < 2^32), into Montgomery form by one multiply
   x.v[0] = (uint32_t)(k + 1);
   x = fe_to_mont<F>(x);
   Fe<F> r = fe_zero<F>();
   for (size_t jj = m; jj-- > 0;) r = fe_add<F>(fe_mul<F>(r, x), fe_load<F>(in, jj * R + b));
-  fe_store<F>(out, t, r);
+  fe_store<F>(out, k * R + b, r);
 }
 
 // 32 x 32 element tiles through LDS (padded row: no repeated bank pattern down a column).
@@ -231,61 +233,74 @@ inline void mfma_tiling(size_t R, int &tiles, unsigned &chunks) {
 }
 
 template <class F, int TILES>
-void launch_spmm_mfma(const CsrDev &M, const uint32_t *x, uint32_t *y, size_t R, unsigned chunks,
-                      hipStream_t s) {
+void launch_spmm_mfma(const CsrDev &M, const uint32_t *x, uint32_t *y, size_t R, size_t b0, size_t nb,
+                      unsigned chunks, hipStream_t s) {
   hipLaunchKernelGGL((k_spmm_mfma<F, TILES>), dim3((unsigned)((M.rows + 3) / 4), chunks), dim3(256), 0, s,
-                     M.gptr, M.pidx, M.hd, x, y, M.rows, (uint32_t)R);
+                     M.gptr, M.pidx, M.hd, x, y, M.rows, (uint32_t)R, (uint32_t)b0, (uint32_t)(b0 + nb));
 }
 
+// y = M x on rows [b0, b0 + nb) of the element-major vectors (R rows)
 template <class F>
-hipError_t spmm(const SdigPlan &p, const CsrDev &M, const uint32_t *x, uint32_t *y, size_t R, hipStream_t s) {
-  const size_t n = M.rows * R;
+hipError_t spmm(const SdigPlan &p, const CsrDev &M, const uint32_t *x, uint32_t *y, size_t R, size_t b0,
+                size_t nb, hipStream_t s) {
+  const size_t n = M.rows * nb;
   if (!n) return hipSuccess;
   if constexpr (F::N == 4 && F::ID == 1) {
     if (p.mfma) {
       int tiles;
       unsigned chunks;
-      mfma_tiling(R, tiles, chunks);
+      mfma_tiling(nb, tiles, chunks);
       switch (tiles) {
-        case 1: launch_spmm_mfma<F, 1>(M, x, y, R, chunks, s); break;
-        case 2: launch_spmm_mfma<F, 2>(M, x, y, R, chunks, s); break;
-        case 3: launch_spmm_mfma<F, 3>(M, x, y, R, chunks, s); break;
-        case 4: launch_spmm_mfma<F, 4>(M, x, y, R, chunks, s); break;
-        case 5: launch_spmm_mfma<F, 5>(M, x, y, R, chunks, s); break;
-        case 6: launch_spmm_mfma<F, 6>(M, x, y, R, chunks, s); break;
-        case 7: launch_spmm_mfma<F, 7>(M, x, y, R, chunks, s); break;
-        default: launch_spmm_mfma<F, 8>(M, x, y, R, chunks, s); break;
+        case 1: launch_spmm_mfma<F, 1>(M, x, y, R, b0, nb, chunks, s); break;
+        case 2: launch_spmm_mfma<F, 2>(M, x, y, R, b0, nb, chunks, s); break;
+        case 3: launch_spmm_mfma<F, 3>(M, x, y, R, b0, nb, chunks, s); break;
+        case 4: launch_spmm_mfma<F, 4>(M, x, y, R, b0, nb, chunks, s); break;
+        case 5: launch_spmm_mfma<F, 5>(M, x, y, R, b0, nb, chunks, s); break;
+        case 6: launch_spmm_mfma<F, 6>(M, x, y, R, b0, nb, chunks, s); break;
+        case 7: launch_spmm_mfma<F, 7>(M, x, y, R, b0, nb, chunks, s); break;
+        default: launch_spmm_mfma<F, 8>(M, x, y, R, b0, nb, chunks, s); break;
       }
       return hipGetLastError();
     }
   }
   hipLaunchKernelGGL((k_spmm<F>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M.ptr, M.idx,
-                     M.val, x, y, M.rows, (uint32_t)R);
+                     M.val, x, y, M.rows, (uint32_t)R, (uint32_t)b0, (uint32_t)nb);
   return hipGetLastError();
 }
 
+// Rows per pass of the level chain (LCPC_SDIG_ROWS; 0 = all).  Rows are independent, so the
+// whole chain can run on a slice of the rows at a time: a smaller slice keeps each level's
+// input resident in the 256 MB infinity cache across its d re-reads (A/B runs).
+inline size_t sdig_rows_per_pass() {
+  static const size_t v = [] {
+    const char *e = std::getenv("LCPC_SDIG_ROWS");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)0;
+  }();
+  return v;
+}
+
 template <class F>
-hipError_t encode_cm(const SdigPlan &p, uint32_t *cw, size_t R, uint32_t *tmp, hipStream_t s) {
+hipError_t encode_rows_slice(const SdigPlan &p, uint32_t *cw, size_t R, size_t b0, size_t nb, uint32_t *tmp,
+                             hipStream_t s) {
   constexpr int N = F::N;
   const int L = (int)p.pre.size();
-  prof::Scope ps("sdig_encode", s);
   hipError_t e;
   // precodes all the way down (encode.rs:46-59): input [in_start, in_end), output right after
   size_t in_start = 0;
   for (int i = 0; i + 1 < L; i++) {
     const CsrDev &M = p.pre[i];
     const size_t in_end = in_start + M.cols;
-    if ((e = spmm<F>(p, M, cw + in_start * R * N, cw + in_end * R * N, R, s)) != hipSuccess) return e;
+    if ((e = spmm<F>(p, M, cw + in_start * R * N, cw + in_end * R * N, R, b0, nb, s)) != hipSuccess) return e;
     in_start = in_end;
   }
   // last precode into scratch, then Reed-Solomon into the codeword (:61-74)
   const CsrDev &ML = p.pre[L - 1];
   const size_t in_end = in_start + ML.cols;
-  if ((e = spmm<F>(p, ML, cw + in_start * R * N, tmp, R, s)) != hipSuccess) return e;
+  if ((e = spmm<F>(p, ML, cw + in_start * R * N, tmp, R, b0, nb, s)) != hipSuccess) return e;
   const size_t n_rs = p.post[L - 1].cols;
-  if (n_rs * R) {
-    hipLaunchKernelGGL((k_reed_solomon<F>), dim3((unsigned)((n_rs * R + 255) / 256)), dim3(256), 0,
-                       s, tmp, ML.rows, cw + in_end * R * N, n_rs, (uint32_t)R);
+  if (n_rs * nb) {
+    hipLaunchKernelGGL((k_reed_solomon<F>), dim3((unsigned)((n_rs * nb + 255) / 256)), dim3(256), 0,
+                       s, tmp, ML.rows, cw + in_end * R * N, n_rs, (uint32_t)R, (uint32_t)b0, (uint32_t)nb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // postcodes in reverse (:76-90): input [in_start, out_start), output at out_start
@@ -294,10 +309,21 @@ hipError_t encode_cm(const SdigPlan &p, uint32_t *cw, size_t R, uint32_t *tmp, h
     in_pos -= p.pre[i].rows;
     const CsrDev &Q = p.post[i];
     if (out_pos - in_pos != Q.cols) return hipErrorInvalidValue;
-    if ((e = spmm<F>(p, Q, cw + in_pos * R * N, cw + out_pos * R * N, R, s)) != hipSuccess) return e;
+    if ((e = spmm<F>(p, Q, cw + in_pos * R * N, cw + out_pos * R * N, R, b0, nb, s)) != hipSuccess) return e;
     out_pos += Q.rows;
   }
   if (in_pos != p.pre[0].cols || out_pos != p.n_cols) return hipErrorInvalidValue;
+  return hipSuccess;
+}
+
+template <class F>
+hipError_t encode_cm(const SdigPlan &p, uint32_t *cw, size_t R, uint32_t *tmp, hipStream_t s) {
+  prof::Scope ps("sdig_encode", s);
+  const size_t step = sdig_rows_per_pass() ? std::min(sdig_rows_per_pass(), R) : R;
+  for (size_t b0 = 0; b0 < R; b0 += step) {
+    const hipError_t e = encode_rows_slice<F>(p, cw, R, b0, std::min(step, R - b0), tmp, s);
+    if (e != hipSuccess) return e;
+  }
   return hipSuccess;
 }
 

@@ -478,12 +478,7 @@ lcpc_status stage_post_subtrees(lcpc_sharded_commit *c) {
   const size_t nc = c->nc, B = c->B, G = c->G;
   HIP_TRY(salloc(c, c->hashes, (2 * nc - 1) * 32));
   uint8_t *h = c->hashes.as<uint8_t>();
-  for (size_t l = 0; (B >> l) >= 1; l++) {
-    const size_t w = (B >> l) * 32;
-    HIP_TRY(hipMemcpy2DAsync(h + (2 * nc - 2 * (nc >> l)) * 32, w, c->subs.as<uint8_t>() + (2 * B - 2 * (B >> l)) * 32,
-                             (2 * B - 1) * 32, w, G, hipMemcpyDeviceToDevice, c->s));
-    if ((B >> l) == 1) break;
-  }
+  HIP_TRY(assemble_subtrees(c->subs.as<uint8_t>(), B, G, h, c->s));  // one launch for every level
   if (G > 1) HIP_TRY(merkle_tree_io(h + (2 * nc - 2 * G) * 32, G, h + (2 * nc - G) * 32, c->s));
   lcpc_status st = c->h_root.get(c->dev, 32);
   if (st) return st;
@@ -956,34 +951,89 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   off[S_COLS] = off[S_IDX] + 1;
   const size_t n_ticks = n_polys + off[S_COLS];
 
-  TaskPool pool(std::min<size_t>(16, std::max(2u, std::thread::hardware_concurrency())));
+  // Host threads: the main thread issues the exchange groups in schedule order; each
+  // polynomial's compute launches after an exchange (and its first encode) run on `launch`
+  // workers, one task per polynomial at a time (a task's launches precede that polynomial's next
+  // exchange: the main thread settles it first), so the main thread's tick is the group plus the
+  // waits; the root rank's transcript absorptions and the final proofs run on `pool`.
+  const size_t hw = std::max(2u, std::thread::hardware_concurrency());
+  TaskPool pool(std::min<size_t>(16, hw));
+  TaskPool launch(std::min<size_t>(4, hw));
   std::vector<ShardPtr> cs(n_polys);
-  std::vector<std::future<lcpc_status>> finals;
-  auto start = [&](size_t k) -> lcpc_status {
-    lcpc_status s2 = shard_init(e, comm, n_rows, cs[k]);
-    if (s2) return s2;
-    return stage_pre_commit(cs[k].get(), d_rows[k]);
+  std::vector<std::future<lcpc_status>> pending(n_polys);  // the polynomial's outstanding launch task
+  std::deque<std::pair<size_t, std::future<lcpc_status>>> finals;  // (poly, host_proof)
+  std::vector<size_t> to_finalize;
+  std::mutex err_mu;
+  std::string err_msg;  // the first failing worker's message (g_err is per thread)
+  auto wrap = [&](std::function<lcpc_status()> fn) {
+    return [fn = std::move(fn), &err_mu, &err_msg]() -> lcpc_status {
+      const lcpc_status s2 = fn();
+      if (s2) {
+        std::lock_guard<std::mutex> l2(err_mu);
+        if (err_msg.empty()) err_msg = g_err;
+      }
+      return s2;
+    };
   };
+  auto settle = [&](size_t k) -> lcpc_status { return pending[k].valid() ? pending[k].get() : LCPC_OK; };
   auto fail_all = [&](lcpc_status s2) {
-    const std::string msg = g_err;
-    for (auto &f : finals) f.wait();
+    std::string msg = g_err;
+    for (auto &f : pending)
+      if (f.valid()) f.wait();
     for (auto &c : cs)
       if (c && c->next.valid()) c->next.wait();
+    for (auto &f : finals) f.second.wait();
+    {
+      std::lock_guard<std::mutex> l2(err_mu);
+      if (!err_msg.empty()) msg = err_msg;
+    }
     return fail(s2, msg);
+  };
+  auto submit_final = [&](size_t k) {
+    lcpc_sharded_commit *c = cs[k].get();
+    lcpc_proof **dst = proofs ? proofs + k : nullptr;
+    finals.emplace_back(k, pool.submit(wrap([c, dst]() -> lcpc_status {
+                          lcpc_proof *p = nullptr;
+                          const lcpc_status s2 = host_proof(c, &p);
+                          if (dst) *dst = p;
+                          else delete p;
+                          return s2;
+                        })));
+  };
+  auto start = [&](size_t k) {
+    pending[k] = launch.submit(wrap([&, k]() -> lcpc_status {
+      lcpc_status s2 = shard_init(e, comm, n_rows, cs[k]);
+      if (s2) return s2;
+      return stage_pre_commit(cs[k].get(), d_rows[k]);
+    }));
   };
   // polynomial k's encode is launched two ticks before its chaining-value exchange, so a tick's
   // exchange group (which waits for every producer in it) does not wait on a just-launched encode
   constexpr size_t AHEAD = 2;
-  for (size_t k = 0; k < std::min(AHEAD, n_polys); k++)
-    if ((st = start(k))) return k ? fail_all(st) : st;
+  for (size_t k = 0; k < std::min(AHEAD, n_polys); k++) start(k);
   for (size_t t = 0; t < n_ticks; t++) {
     prof::HostScope hs_tick("tick_total");
+    // last tick's final stages: the proofs go to the pool; finished polynomials free their buffers
+    for (size_t k : to_finalize) {
+      if ((st = settle(k))) return fail_all(st);
+      submit_final(k);
+    }
+    to_finalize.clear();
+    while (!finals.empty() && finals.front().second.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
+      if ((st = finals.front().second.get())) return fail_all(st);
+      cs[finals.front().first].reset();  // every exchange of it is complete (the last landed on the host)
+      finals.pop_front();
+    }
     std::vector<Xop> ops;
     std::vector<hipEvent_t> done;
     std::vector<std::pair<size_t, size_t>> items;  // (poly, stage)
     for (size_t s = 0; s < n_stages; s++) {
       if (t < off[s] || t - off[s] >= n_polys) continue;
       const size_t k = t - off[s];
+      {
+        prof::HostScope hs("tick_wait_launch");
+        if ((st = settle(k))) return fail_all(st);
+      }
       lcpc_sharded_commit *c = cs[k].get();
       if (s == S_CV) {
         ops.push_back(op_cv_exchange(c));
@@ -1033,49 +1083,40 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
       prof::HostScope hs("tick_run_group");
       if ((st = run_group(comm, ops, done))) return fail_all(st);
     }
-    // the compute each exchange feeds, on the polynomials' own streams
-    prof::HostScope hs_compute("tick_compute");
+    // the compute each exchange feeds, on the polynomials' own streams (launch workers)
     for (auto [k, s] : items) {
       lcpc_sharded_commit *c = cs[k].get();
-      if (s == S_CV) {
-        st = stage_post_cv(c);
-      } else if (s == S_SUB) {
-        st = stage_post_subtrees(c);
-      } else if (s == S_IDX) {
-        st = stage_gather_cols(c);
-      } else if (s == S_COLS) {
-        if ((st = stage_paths(c))) return fail_all(st);
-        lcpc_proof **dst = proofs ? proofs + k : nullptr;
-        finals.push_back(pool.submit([c, dst, &cs, k]() -> lcpc_status {
-          lcpc_proof *p = nullptr;
-          lcpc_status s2 = host_proof(c, &p);
-          if (dst) *dst = p;
-          else delete p;
-          cs[k].reset();  // every exchange of k is complete (its last one landed on the host)
-          return s2;
-        }));
-      } else {
+      pending[k] = launch.submit(wrap([&pool, c, s = s, S_IDX, S_COLS]() -> lcpc_status {
+        if (s == S_CV) return stage_post_cv(c);
+        if (s == S_SUB) return stage_post_subtrees(c);
+        if (s == S_IDX) return stage_gather_cols(c);
+        if (s == S_COLS) return stage_paths(c);
         const size_t r = (s - S_R0) / 2;
-        if ((s - S_R0) % 2 == 0) {
-          st = stage_collapse(c, r);
-        } else {
-          if ((st = stage_fold(c, r))) return fail_all(st);
-          if (c->me == c->root_rank) c->next = pool.submit([c, r] { return host_absorb(c, r); });
-        }
-      }
-      if (st) return fail_all(st);
+        if ((s - S_R0) % 2 == 0) return stage_collapse(c, r);
+        const lcpc_status s2 = stage_fold(c, r);
+        if (s2) return s2;
+        if (c->me == c->root_rank) c->next = pool.submit([c, r] { return host_absorb(c, r); });
+        return LCPC_OK;
+      }));
+      if (s == S_COLS) to_finalize.push_back(k);
     }
-    prof::HostScope hs_start("tick_start");
-    if (t + AHEAD < n_polys && (st = start(t + AHEAD))) return fail_all(st);
+    if (t + AHEAD < n_polys) start(t + AHEAD);
+  }
+  for (size_t k : to_finalize) {
+    if ((st = settle(k))) return fail_all(st);
+    submit_final(k);
   }
   lcpc_status first = LCPC_OK;
   std::string msg;
-  for (auto &f : finals) {
-    lcpc_status s2 = f.get();
-    if (s2 && !first) {
-      first = s2;
-      msg = g_err;
-    }
+  while (!finals.empty()) {
+    const lcpc_status s2 = finals.front().second.get();
+    if (s2 && !first) first = s2;
+    cs[finals.front().first].reset();
+    finals.pop_front();
+  }
+  if (first) {
+    std::lock_guard<std::mutex> l2(err_mu);
+    msg = err_msg;
   }
   HIP_TRY(hipStreamSynchronize(comm->cs));
   return first ? fail(first, msg) : LCPC_OK;

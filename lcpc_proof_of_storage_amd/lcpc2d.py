@@ -224,6 +224,14 @@ class LcEncoding:
     def get_n_degree_tests(self) -> int:
         return N.load().lcpc_encoding_n_degree_tests(self._h)
 
+    def prepare_thread(self, n_rows: int):
+        """Pre-allocate the calling thread's pinned staging for prove (lcpc_prepare_thread)."""
+        _raise(N.load().lcpc_prepare_thread(self._h, n_rows))
+
+    def reserve(self, length: int, count: int):
+        """Pre-allocate device buffers and streams for `count` concurrent commit + prove calls."""
+        _raise(N.load().lcpc_reserve(self._h, length, count))
+
     @property
     def kind(self) -> str:
         return ["rs", "sdig"][N.load().lcpc_encoding_kind(self._h)]

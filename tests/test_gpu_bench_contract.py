@@ -45,25 +45,27 @@ def _check_cpu(d):
     assert cb["unit"] == d["unit"]
 
 
-def test_bench_ligero_small(gpu):
-    d = _bench("--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1")
+def test_bench_ligero_sharded_small(gpu):
+    d = _bench("--mode", "sharded", "--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1")
     _check_common(d, 4)
     _check_cpu(d)
     assert d["parity_root_vs_oracle"] is True
     assert d["verify"]["parity_vs_oracle"] is True and d["verify"]["ms"] > 0
     assert d["config"]["n_rows"] * d["config"]["n_per_row"] == 1 << 16
-    # the default (sharded driver) line: the kept proof equals the oracle's, one commitment's latency
+    # the sharded driver line: the kept proof equals the oracle's, one commitment's latency
     assert d["scaling"] == "strong" and d["parity_proof_vs_oracle"] is True
     assert d["latency"]["commit_ms"] > 0 and d["latency"]["prove_ms"] > 0
     assert "traffic_source" in d["roofline"] and d["world_formed"] == 1
 
 
-def test_bench_ligero_replicas_small(gpu):
-    d = _bench("--mode", "replicas", "--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1")
+def test_bench_ligero_default_small(gpu):
+    """the default engine at --gpus 1 is independent commitments in flight (replicas)"""
+    d = _bench("--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1")
     _check_common(d, 4)
     _check_cpu(d)
     assert d["scaling"] == "weak" and d["parity_root_vs_oracle"] is True and d["pipeline"] == 4
-    assert d["latency"]["commit_ms"] > 0
+    assert d["verify"]["parity_vs_oracle"] is True
+    assert d["latency"]["commit_ms"] > 0 and d["world_formed"] == 1
 
 
 @pytest.mark.timeout(300)

@@ -19,16 +19,23 @@ import json
 import os
 
 KERNELS = {"ntt_pass_a": "k_pass_a", "ntt_pass_b": "k_pass_b", "leaf_chunks": "k_leaf_chunks",
-           "collapse_partial": "k_collapse_partial", "collapse_mfma": "k_collapse_mfma"}
+           "collapse_partial": "k_collapse_partial", "collapse_mfma": "k_collapse_mfma",
+           # Brakedown (--code sdig): the transpose into element-major form, the SpMM levels
+           # (matrix-core or VALU kernel) and the Reed-Solomon base
+           "transpose": "k_transpose", "spmm": "k_spmm", "reed_solomon": "k_reed_solomon"}
+SDIG_ENCODE = ("transpose", "spmm", "reed_solomon")
 
 
 def per_kernel(path):
+    """mean bytes per launch and launch count per kernel; also the total bytes per kernel"""
     acc = collections.defaultdict(list)
     for row in csv.DictReader(open(path)):
         for short, pat in KERNELS.items():
             if pat in row["Kernel_Name"]:
                 acc[short].append(float(row["Counter_Value"]) * 1024.0)
-    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+                break
+    return ({k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()},
+            {k: sum(v) for k, v in acc.items()})
 
 
 def main():
@@ -41,15 +48,20 @@ def main():
     a = ap.parse_args()
     fpath = glob.glob(os.path.join(a.run_dir, "pmc_fetch", "*counter_collection.csv"))[0]
     wpath = glob.glob(os.path.join(a.run_dir, "pmc_write", "*counter_collection.csv"))[0]
-    fetch, nf = per_kernel(fpath)
-    write, nw = per_kernel(wpath)
+    fetch, nf, ftot = per_kernel(fpath)
+    write, nw, wtot = per_kernel(wpath)
     kern = {}
     for k in fetch:
         rd = 2.0 * fetch[k]
         wr = write.get(k, 0.0)
         kern[k] = {"fetch_bytes_raw": fetch[k], "read_bytes_corrected": rd, "write_bytes": wr,
                    "hbm_bytes": rd + wr, "launches": nf[k]}
-    enc = kern["ntt_pass_a"]["hbm_bytes"] + kern["ntt_pass_b"]["hbm_bytes"]
+    if a.code == "sdig":
+        # one encode = one transpose + every SpMM level + the R-S base: total over the run / encodes
+        n_enc = nf["transpose"]
+        enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in SDIG_ENCODE) / n_enc
+    else:
+        enc = kern["ntt_pass_a"]["hbm_bytes"] + kern["ntt_pass_b"]["hbm_bytes"]
     out = {
         "config_len": a.len, "field": a.field, "code": a.code,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
