@@ -93,6 +93,9 @@ def parse():
                          "Commits then finish in order and each proof's serial host "
                          "transcript starts while later commits run, instead of every commit of a wave "
                          "finishing together at its end")
+    ap.add_argument("--timeline", default=None,
+                    help="replicas (ligero / sdig): write every timed step's gate / commit / prove "
+                         "times (s, from the start of the timed region) to this JSON file")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="independent commitments in flight per GPU (host threads); the serial "
                          "Merlin transcript of one overlaps the kernels of the others.  0: 16, or "
@@ -201,17 +204,25 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
 
     gate = threading.Semaphore(args.commit_slots) if args.commit_slots > 0 else None
 
+    timeline = []  # (slot, t_gate, t_commit_start, t_commit_end, t_prove_end) with --timeline
+
     def step(slot):
+        t_a = time.perf_counter()
         if gate is not None:
             with gate:
+                t_b = time.perf_counter()
                 c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
         else:
+            t_b = t_a
             c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+        t_c = time.perf_counter()
         root = c.get_root()
         tr = L.Transcript(b"test transcript")
         tr.append_message(b"polycommit", root)
         tr.append_message(b"ncols", nco.to_bytes(8, "big"))
         c.prove(outer, enc, tr)
+        if args.timeline:
+            timeline.append((slot, t_a, t_b, t_c, time.perf_counter()))
         return root
 
     inner = L.field_random(fid, n_per_row, 8)  # verify returns sum_c inner[c] p_eval[c]
@@ -285,6 +296,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
                 "n_col_opens": nco, "n_degree_tests": ndt},
         step=step, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify, latency=latency,
         prepare=lambda: enc.prepare_thread(n_rows), reserve=lambda count: enc.reserve(n, count),
+        timeline=timeline,
         enc_kernels=("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=("sdig_encode = transpose + 13 SpMM / Reed-Solomon levels (per commit, all rows)" if sdig
                          else f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
@@ -854,6 +866,9 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     assert all(r == root for r in roots), "nondeterministic root across steps"
     barrier()
     elapsed = time.perf_counter() - t0
+    if args.timeline and getattr(wl, "timeline", None) is not None:
+        tl = [(s_, a - t0, b - t0, c - t0, d - t0) for s_, a, b, c, d in wl.timeline if a >= t0]
+        json.dump({"elapsed": elapsed, "steps": sorted(tl, key=lambda r: r[2])}, open(args.timeline, "w"))
     L.prof_enable(False)
     stats = L.prof_stats() if (prof and args.prof_timed) else {}
     iso = {}

@@ -201,6 +201,10 @@ lcpc_transcript *lcpc_transcript_clone(const lcpc_transcript *t);
 void lcpc_transcript_free(lcpc_transcript *t);
 void lcpc_transcript_append_message(lcpc_transcript *t, const uint8_t *label, size_t label_len,
                                     const uint8_t *msg, size_t msg_len);
+/* append_message(label, msgs + i * msg_len) for i < n_msgs (host bytes): the prover's per-element
+ * absorption (lcpc-2d/src/lib.rs:1075-1077, 1096-1098) in one call */
+void lcpc_transcript_append_messages(lcpc_transcript *t, const uint8_t *label, size_t label_len,
+                                     const uint8_t *msgs, size_t msg_len, size_t n_msgs);
 void lcpc_transcript_challenge_bytes(lcpc_transcript *t, const uint8_t *label, size_t label_len,
                                      uint8_t *dest, size_t dest_len);
 

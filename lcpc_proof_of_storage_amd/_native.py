@@ -96,6 +96,7 @@ SIGNATURES = {
     "lcpc_transcript_clone": (vp, [vp]),
     "lcpc_transcript_free": (None, [vp]),
     "lcpc_transcript_append_message": (None, [vp, u8p, sz, u8p, sz]),
+    "lcpc_transcript_append_messages": (None, [vp, u8p, sz, u8p, sz, sz]),
     "lcpc_transcript_challenge_bytes": (None, [vp, u8p, sz, u8p, sz]),
     "lcpc_prove": (i32, [vp, u64p, sz, vp, vp, C.POINTER(vp)]),
     "lcpc_proof_free": (None, [vp]),

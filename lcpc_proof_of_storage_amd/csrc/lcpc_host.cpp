@@ -584,6 +584,10 @@ void lcpc_transcript_append_message(lcpc_transcript *t, const uint8_t *l, size_t
                                     const uint8_t *m, size_t mn) {
   t->t.append_message(l, ln, m, mn);
 }
+void lcpc_transcript_append_messages(lcpc_transcript *t, const uint8_t *l, size_t ln, const uint8_t *msgs,
+                                     size_t msg_len, size_t n_msgs) {
+  t->t.append_messages(l, ln, msgs, msg_len, n_msgs);
+}
 void lcpc_transcript_challenge_bytes(lcpc_transcript *t, const uint8_t *l, size_t ln, uint8_t *d,
                                      size_t n) {
   t->t.challenge_bytes(l, ln, d, n);

@@ -97,85 +97,127 @@ void keccak_f1600_scalar(uint64_t s[25]) {
   s[20] = a20; s[21] = a21; s[22] = a22; s[23] = a23; s[24] = a24;
 }
 
-// Keccak-f[1600] on AVX-512F: plane y (lanes x = 0..4 of s[5y + x]) in one zmm register, lanes
-// 5..7 unused (no permute index ever reads them).  Per round: theta = 2 three-way XORs + 2 lane
-// rotations + 1 rotate + 5 ternlogs; rho = 5 variable rotates; pi = 14 two-/one-source lane
-// permutes; chi = 10 lane rotations + 5 ternlogs (a ^ (~b & c) = 0xD2); iota = 1 masked XOR.
-// That is ~45 vector ops per round against ~120 scalar ones, and the rows run in parallel.
-__attribute__((target("avx512f"))) void keccak_f1600_avx512(uint64_t s[25]) {
-  // rho offsets per plane, lane x = r[x][y]
-  const __m512i rho0 = _mm512_setr_epi64(0, 1, 62, 28, 27, 0, 0, 0);
-  const __m512i rho1 = _mm512_setr_epi64(36, 44, 6, 55, 20, 0, 0, 0);
-  const __m512i rho2 = _mm512_setr_epi64(3, 10, 43, 25, 39, 0, 0, 0);
-  const __m512i rho3 = _mm512_setr_epi64(41, 45, 15, 21, 8, 0, 0, 0);
-  const __m512i rho4 = _mm512_setr_epi64(18, 2, 61, 56, 14, 0, 0, 0);
-  const __m512i prev = _mm512_setr_epi64(4, 0, 1, 2, 3, 5, 6, 7);   // lane x <- x - 1
-  const __m512i next = _mm512_setr_epi64(1, 2, 3, 4, 0, 5, 6, 7);   // lane x <- x + 1
-  const __m512i next2 = _mm512_setr_epi64(2, 3, 4, 0, 1, 5, 6, 7);  // lane x <- x + 2
-  // pi: out plane Y, lane X = in plane X, lane (3Y + X) % 5.  W01 lanes (2Y, 2Y+1) hold the
-  // plane-0 / plane-1 elements of out planes Y = 0..3, W23 the plane-2 / plane-3 ones.
-  const __m512i w01 = _mm512_setr_epi64(0, 8 + 1, 3, 8 + 4, 1, 8 + 2, 4, 8 + 0);
-  const __m512i w23 = _mm512_setr_epi64(2, 8 + 3, 0, 8 + 1, 3, 8 + 4, 1, 8 + 2);
-  const __m512i o0 = _mm512_setr_epi64(0, 1, 8, 9, 0, 0, 0, 0);
-  const __m512i o1 = _mm512_setr_epi64(2, 3, 10, 11, 0, 0, 0, 0);
-  const __m512i o2 = _mm512_setr_epi64(4, 5, 12, 13, 0, 0, 0, 0);
-  const __m512i o3 = _mm512_setr_epi64(6, 7, 14, 15, 0, 0, 0, 0);
-  // lane 4 of out plane Y from plane 4, lane (3Y + 4) % 5
-  const __m512i l4_0 = _mm512_set1_epi64(4), l4_1 = _mm512_set1_epi64(2), l4_2 = _mm512_set1_epi64(0),
-                l4_3 = _mm512_set1_epi64(3), l4_4 = _mm512_set1_epi64(1);
-  // out plane 4: lanes 0..3 = A0[2], A1[3], A2[4], A3[0]
-  const __m512i x01 = _mm512_setr_epi64(2, 8 + 3, 0, 0, 0, 0, 0, 0);
-  const __m512i x23 = _mm512_setr_epi64(4, 8 + 0, 0, 0, 0, 0, 0, 0);
-  const __m512i o4 = _mm512_setr_epi64(0, 1, 8, 9, 0, 0, 0, 0);
-  const __mmask8 m5 = 0x1f, lane4 = 0x10;
-  __m512i a0 = _mm512_maskz_loadu_epi64(m5, s + 0), a1 = _mm512_maskz_loadu_epi64(m5, s + 5),
-          a2 = _mm512_maskz_loadu_epi64(m5, s + 10), a3 = _mm512_maskz_loadu_epi64(m5, s + 15),
-          a4 = _mm512_maskz_loadu_epi64(m5, s + 20);
+// Keccak-f[1600] on AVX-512VL, one lane per xmm register (the scalar schedule, but all 25
+// lanes and the temporaries fit the 32 vector registers where the 16 GPRs spill, and theta /
+// chi are one three-input ternlog per lane: ~90 vector ops per round).  (A 5-plane zmm layout
+// was tried first: its pi step costs 14 lane permutes per round and it ran at 249 against the
+// scalar 188 ns on the box's EPYC.)
+__attribute__((target("avx512f,avx512vl"))) void keccak_f1600_avx512(uint64_t s[25]) {
+  // one lane per xmm register: all 25 lanes and the temporaries stay in the 32 vector
+  // registers (no spills), and theta / chi are single three-input ternlogs
+  __m128i a00 = _mm_cvtsi64_si128((long long)s[0]);
+  __m128i a01 = _mm_cvtsi64_si128((long long)s[1]);
+  __m128i a02 = _mm_cvtsi64_si128((long long)s[2]);
+  __m128i a03 = _mm_cvtsi64_si128((long long)s[3]);
+  __m128i a04 = _mm_cvtsi64_si128((long long)s[4]);
+  __m128i a05 = _mm_cvtsi64_si128((long long)s[5]);
+  __m128i a06 = _mm_cvtsi64_si128((long long)s[6]);
+  __m128i a07 = _mm_cvtsi64_si128((long long)s[7]);
+  __m128i a08 = _mm_cvtsi64_si128((long long)s[8]);
+  __m128i a09 = _mm_cvtsi64_si128((long long)s[9]);
+  __m128i a10 = _mm_cvtsi64_si128((long long)s[10]);
+  __m128i a11 = _mm_cvtsi64_si128((long long)s[11]);
+  __m128i a12 = _mm_cvtsi64_si128((long long)s[12]);
+  __m128i a13 = _mm_cvtsi64_si128((long long)s[13]);
+  __m128i a14 = _mm_cvtsi64_si128((long long)s[14]);
+  __m128i a15 = _mm_cvtsi64_si128((long long)s[15]);
+  __m128i a16 = _mm_cvtsi64_si128((long long)s[16]);
+  __m128i a17 = _mm_cvtsi64_si128((long long)s[17]);
+  __m128i a18 = _mm_cvtsi64_si128((long long)s[18]);
+  __m128i a19 = _mm_cvtsi64_si128((long long)s[19]);
+  __m128i a20 = _mm_cvtsi64_si128((long long)s[20]);
+  __m128i a21 = _mm_cvtsi64_si128((long long)s[21]);
+  __m128i a22 = _mm_cvtsi64_si128((long long)s[22]);
+  __m128i a23 = _mm_cvtsi64_si128((long long)s[23]);
+  __m128i a24 = _mm_cvtsi64_si128((long long)s[24]);
   for (int r = 0; r < 24; r++) {
-    // theta
-    __m512i c = _mm512_ternarylogic_epi64(a0, a1, a2, 0x96);
-    c = _mm512_ternarylogic_epi64(c, a3, a4, 0x96);
-    const __m512i cm = _mm512_permutexvar_epi64(prev, c);
-    const __m512i cp = _mm512_rol_epi64(_mm512_permutexvar_epi64(next, c), 1);
-    a0 = _mm512_ternarylogic_epi64(a0, cm, cp, 0x96);
-    a1 = _mm512_ternarylogic_epi64(a1, cm, cp, 0x96);
-    a2 = _mm512_ternarylogic_epi64(a2, cm, cp, 0x96);
-    a3 = _mm512_ternarylogic_epi64(a3, cm, cp, 0x96);
-    a4 = _mm512_ternarylogic_epi64(a4, cm, cp, 0x96);
-    // rho
-    a0 = _mm512_rolv_epi64(a0, rho0);
-    a1 = _mm512_rolv_epi64(a1, rho1);
-    a2 = _mm512_rolv_epi64(a2, rho2);
-    a3 = _mm512_rolv_epi64(a3, rho3);
-    a4 = _mm512_rolv_epi64(a4, rho4);
-    // pi
-    const __m512i p01 = _mm512_permutex2var_epi64(a0, w01, a1);
-    const __m512i p23 = _mm512_permutex2var_epi64(a2, w23, a3);
-    __m512i b0 = _mm512_permutex2var_epi64(p01, o0, p23);
-    __m512i b1 = _mm512_permutex2var_epi64(p01, o1, p23);
-    __m512i b2 = _mm512_permutex2var_epi64(p01, o2, p23);
-    __m512i b3 = _mm512_permutex2var_epi64(p01, o3, p23);
-    __m512i b4 = _mm512_permutex2var_epi64(_mm512_permutex2var_epi64(a0, x01, a1), o4,
-                                           _mm512_permutex2var_epi64(a2, x23, a3));
-    b0 = _mm512_mask_permutexvar_epi64(b0, lane4, l4_0, a4);
-    b1 = _mm512_mask_permutexvar_epi64(b1, lane4, l4_1, a4);
-    b2 = _mm512_mask_permutexvar_epi64(b2, lane4, l4_2, a4);
-    b3 = _mm512_mask_permutexvar_epi64(b3, lane4, l4_3, a4);
-    b4 = _mm512_mask_permutexvar_epi64(b4, lane4, l4_4, a4);
-    // chi
-    a0 = _mm512_ternarylogic_epi64(b0, _mm512_permutexvar_epi64(next, b0), _mm512_permutexvar_epi64(next2, b0), 0xD2);
-    a1 = _mm512_ternarylogic_epi64(b1, _mm512_permutexvar_epi64(next, b1), _mm512_permutexvar_epi64(next2, b1), 0xD2);
-    a2 = _mm512_ternarylogic_epi64(b2, _mm512_permutexvar_epi64(next, b2), _mm512_permutexvar_epi64(next2, b2), 0xD2);
-    a3 = _mm512_ternarylogic_epi64(b3, _mm512_permutexvar_epi64(next, b3), _mm512_permutexvar_epi64(next2, b3), 0xD2);
-    a4 = _mm512_ternarylogic_epi64(b4, _mm512_permutexvar_epi64(next, b4), _mm512_permutexvar_epi64(next2, b4), 0xD2);
-    // iota
-    a0 = _mm512_mask_xor_epi64(a0, 1, a0, _mm512_set1_epi64((long long)RC[r]));
+    const __m128i c0 = _mm_ternarylogic_epi64(_mm_ternarylogic_epi64(a00, a05, a10, 0x96), a15, a20, 0x96);
+    const __m128i c1 = _mm_ternarylogic_epi64(_mm_ternarylogic_epi64(a01, a06, a11, 0x96), a16, a21, 0x96);
+    const __m128i c2 = _mm_ternarylogic_epi64(_mm_ternarylogic_epi64(a02, a07, a12, 0x96), a17, a22, 0x96);
+    const __m128i c3 = _mm_ternarylogic_epi64(_mm_ternarylogic_epi64(a03, a08, a13, 0x96), a18, a23, 0x96);
+    const __m128i c4 = _mm_ternarylogic_epi64(_mm_ternarylogic_epi64(a04, a09, a14, 0x96), a19, a24, 0x96);
+    const __m128i r0 = _mm_rol_epi64(c0, 1);
+    const __m128i r1 = _mm_rol_epi64(c1, 1);
+    const __m128i r2 = _mm_rol_epi64(c2, 1);
+    const __m128i r3 = _mm_rol_epi64(c3, 1);
+    const __m128i r4 = _mm_rol_epi64(c4, 1);
+    const __m128i b00 = _mm_ternarylogic_epi64(a00, c4, r1, 0x96);
+    const __m128i b10 = _mm_rol_epi64(_mm_ternarylogic_epi64(a01, c0, r2, 0x96), 1);
+    const __m128i b20 = _mm_rol_epi64(_mm_ternarylogic_epi64(a02, c1, r3, 0x96), 62);
+    const __m128i b05 = _mm_rol_epi64(_mm_ternarylogic_epi64(a03, c2, r4, 0x96), 28);
+    const __m128i b15 = _mm_rol_epi64(_mm_ternarylogic_epi64(a04, c3, r0, 0x96), 27);
+    const __m128i b16 = _mm_rol_epi64(_mm_ternarylogic_epi64(a05, c4, r1, 0x96), 36);
+    const __m128i b01 = _mm_rol_epi64(_mm_ternarylogic_epi64(a06, c0, r2, 0x96), 44);
+    const __m128i b11 = _mm_rol_epi64(_mm_ternarylogic_epi64(a07, c1, r3, 0x96), 6);
+    const __m128i b21 = _mm_rol_epi64(_mm_ternarylogic_epi64(a08, c2, r4, 0x96), 55);
+    const __m128i b06 = _mm_rol_epi64(_mm_ternarylogic_epi64(a09, c3, r0, 0x96), 20);
+    const __m128i b07 = _mm_rol_epi64(_mm_ternarylogic_epi64(a10, c4, r1, 0x96), 3);
+    const __m128i b17 = _mm_rol_epi64(_mm_ternarylogic_epi64(a11, c0, r2, 0x96), 10);
+    const __m128i b02 = _mm_rol_epi64(_mm_ternarylogic_epi64(a12, c1, r3, 0x96), 43);
+    const __m128i b12 = _mm_rol_epi64(_mm_ternarylogic_epi64(a13, c2, r4, 0x96), 25);
+    const __m128i b22 = _mm_rol_epi64(_mm_ternarylogic_epi64(a14, c3, r0, 0x96), 39);
+    const __m128i b23 = _mm_rol_epi64(_mm_ternarylogic_epi64(a15, c4, r1, 0x96), 41);
+    const __m128i b08 = _mm_rol_epi64(_mm_ternarylogic_epi64(a16, c0, r2, 0x96), 45);
+    const __m128i b18 = _mm_rol_epi64(_mm_ternarylogic_epi64(a17, c1, r3, 0x96), 15);
+    const __m128i b03 = _mm_rol_epi64(_mm_ternarylogic_epi64(a18, c2, r4, 0x96), 21);
+    const __m128i b13 = _mm_rol_epi64(_mm_ternarylogic_epi64(a19, c3, r0, 0x96), 8);
+    const __m128i b14 = _mm_rol_epi64(_mm_ternarylogic_epi64(a20, c4, r1, 0x96), 18);
+    const __m128i b24 = _mm_rol_epi64(_mm_ternarylogic_epi64(a21, c0, r2, 0x96), 2);
+    const __m128i b09 = _mm_rol_epi64(_mm_ternarylogic_epi64(a22, c1, r3, 0x96), 61);
+    const __m128i b19 = _mm_rol_epi64(_mm_ternarylogic_epi64(a23, c2, r4, 0x96), 56);
+    const __m128i b04 = _mm_rol_epi64(_mm_ternarylogic_epi64(a24, c3, r0, 0x96), 14);
+    a00 = _mm_ternarylogic_epi64(b00, b01, b02, 0xD2);
+    a01 = _mm_ternarylogic_epi64(b01, b02, b03, 0xD2);
+    a02 = _mm_ternarylogic_epi64(b02, b03, b04, 0xD2);
+    a03 = _mm_ternarylogic_epi64(b03, b04, b00, 0xD2);
+    a04 = _mm_ternarylogic_epi64(b04, b00, b01, 0xD2);
+    a05 = _mm_ternarylogic_epi64(b05, b06, b07, 0xD2);
+    a06 = _mm_ternarylogic_epi64(b06, b07, b08, 0xD2);
+    a07 = _mm_ternarylogic_epi64(b07, b08, b09, 0xD2);
+    a08 = _mm_ternarylogic_epi64(b08, b09, b05, 0xD2);
+    a09 = _mm_ternarylogic_epi64(b09, b05, b06, 0xD2);
+    a10 = _mm_ternarylogic_epi64(b10, b11, b12, 0xD2);
+    a11 = _mm_ternarylogic_epi64(b11, b12, b13, 0xD2);
+    a12 = _mm_ternarylogic_epi64(b12, b13, b14, 0xD2);
+    a13 = _mm_ternarylogic_epi64(b13, b14, b10, 0xD2);
+    a14 = _mm_ternarylogic_epi64(b14, b10, b11, 0xD2);
+    a15 = _mm_ternarylogic_epi64(b15, b16, b17, 0xD2);
+    a16 = _mm_ternarylogic_epi64(b16, b17, b18, 0xD2);
+    a17 = _mm_ternarylogic_epi64(b17, b18, b19, 0xD2);
+    a18 = _mm_ternarylogic_epi64(b18, b19, b15, 0xD2);
+    a19 = _mm_ternarylogic_epi64(b19, b15, b16, 0xD2);
+    a20 = _mm_ternarylogic_epi64(b20, b21, b22, 0xD2);
+    a21 = _mm_ternarylogic_epi64(b21, b22, b23, 0xD2);
+    a22 = _mm_ternarylogic_epi64(b22, b23, b24, 0xD2);
+    a23 = _mm_ternarylogic_epi64(b23, b24, b20, 0xD2);
+    a24 = _mm_ternarylogic_epi64(b24, b20, b21, 0xD2);
+    a00 = _mm_xor_si128(a00, _mm_cvtsi64_si128((long long)RC[r]));
   }
-  _mm512_mask_storeu_epi64(s + 0, m5, a0);
-  _mm512_mask_storeu_epi64(s + 5, m5, a1);
-  _mm512_mask_storeu_epi64(s + 10, m5, a2);
-  _mm512_mask_storeu_epi64(s + 15, m5, a3);
-  _mm512_mask_storeu_epi64(s + 20, m5, a4);
+  s[0] = (uint64_t)_mm_cvtsi128_si64(a00);
+  s[1] = (uint64_t)_mm_cvtsi128_si64(a01);
+  s[2] = (uint64_t)_mm_cvtsi128_si64(a02);
+  s[3] = (uint64_t)_mm_cvtsi128_si64(a03);
+  s[4] = (uint64_t)_mm_cvtsi128_si64(a04);
+  s[5] = (uint64_t)_mm_cvtsi128_si64(a05);
+  s[6] = (uint64_t)_mm_cvtsi128_si64(a06);
+  s[7] = (uint64_t)_mm_cvtsi128_si64(a07);
+  s[8] = (uint64_t)_mm_cvtsi128_si64(a08);
+  s[9] = (uint64_t)_mm_cvtsi128_si64(a09);
+  s[10] = (uint64_t)_mm_cvtsi128_si64(a10);
+  s[11] = (uint64_t)_mm_cvtsi128_si64(a11);
+  s[12] = (uint64_t)_mm_cvtsi128_si64(a12);
+  s[13] = (uint64_t)_mm_cvtsi128_si64(a13);
+  s[14] = (uint64_t)_mm_cvtsi128_si64(a14);
+  s[15] = (uint64_t)_mm_cvtsi128_si64(a15);
+  s[16] = (uint64_t)_mm_cvtsi128_si64(a16);
+  s[17] = (uint64_t)_mm_cvtsi128_si64(a17);
+  s[18] = (uint64_t)_mm_cvtsi128_si64(a18);
+  s[19] = (uint64_t)_mm_cvtsi128_si64(a19);
+  s[20] = (uint64_t)_mm_cvtsi128_si64(a20);
+  s[21] = (uint64_t)_mm_cvtsi128_si64(a21);
+  s[22] = (uint64_t)_mm_cvtsi128_si64(a22);
+  s[23] = (uint64_t)_mm_cvtsi128_si64(a23);
+  s[24] = (uint64_t)_mm_cvtsi128_si64(a24);
 }
 
 namespace {
@@ -191,10 +233,10 @@ double time_perm(PermFn f) {  // best of 5 bursts of 64 permutations, ns per per
   }
   return st[0] == 42 ? best + 1 : best;  // (keeps the permutations live)
 }
-// The single-state AVX-512 permutation is a 5-plane layout whose pi step costs 14 lane permutes
-// per round; on the hosts measured so far (MI355X box EPYC: 249 vs 188 ns; Xeon VM: par) the
-// scalar one wins, so the choice is made by timing both once per process (LCPC_KECCAK=scalar /
-// avx512 forces one).
+// The two permutations run within a few percent of each other on the MI355X box's EPYC
+// (190 vs 188-198 ns, tools/microbench/transcript_bench) and the vector one is ~15% faster on
+// the Xeon build host, so the choice is made by timing both once per process (LCPC_KECCAK=
+// scalar / avx512 forces one).
 PermFn pick_permutation() {
   const char *force = std::getenv("LCPC_KECCAK");
   __builtin_cpu_init();
@@ -312,6 +354,18 @@ void Transcript::append_messages(const uint8_t *label, size_t ln, const uint8_t 
 //   boundary before it (s <= h2):           pad = p + 1, old_begin' = 0, pos_begin = h2 - s + 1.
 void Strobe128::append_records(const uint8_t *label, size_t ln, const uint8_t *msgs, size_t ml,
                                size_t n) {
+  // the prover's records (6-byte labels, 8 / 16 / 32-byte field reprs) with constant sizes, so
+  // every copy below is a couple of register moves
+  if (ln == 6 && ml == 16) return append_records_t<6, 16>(label, ln, msgs, ml, n);
+  if (ln == 6 && ml == 8) return append_records_t<6, 8>(label, ln, msgs, ml, n);
+  if (ln == 6 && ml == 32) return append_records_t<6, 32>(label, ln, msgs, ml, n);
+  append_records_t<0, 0>(label, ln, msgs, ml, n);
+}
+
+template <size_t LN, size_t ML>  // 0, 0: sizes from the arguments
+void Strobe128::append_records_t(const uint8_t *label, size_t ln_, const uint8_t *msgs, size_t ml_,
+                                 size_t n) {
+  const size_t ln = LN ? LN : ln_, ml = LN ? ML : ml_;
   const size_t h2 = 6 + ln, rec = h2 + 2 + ml;
   alignas(64) uint8_t buf[STROBE_R + 2 * 64 + 8 + 32];
   uint8_t t[8 + 64];  // the record's bytes before the message
@@ -336,38 +390,41 @@ void Strobe128::append_records(const uint8_t *label, size_t ln, const uint8_t *m
   for (size_t i = 0; i < n; i++) {
     const uint8_t *m = msgs + i * ml;
     const size_t s = STROBE_R - p;  // bytes left before the boundary
-    t[0] = pb;
+    // (the template is copied whole and its two position bytes patched in place: byte stores
+    // into t followed by a wide load of t would stall on store forwarding)
+    std::memcpy(buf + p, t, h2 + 2);
+    std::memcpy(buf + p + h2 + 2, m, ml);
+    buf[p] = pb;
     if (s > rec) {
-      t[h2] = (uint8_t)(p + 1);
-      std::memcpy(buf + p, t, h2 + 2);
-      std::memcpy(buf + p + h2 + 2, m, ml);
+      buf[p + h2] = (uint8_t)(p + 1);
       pb = (uint8_t)(p + h2 + 1);
       p += rec;
       continue;
     }
     uint8_t pad;
     if (s > h2) {
-      t[h2] = (uint8_t)(p + 1);
+      buf[p + h2] = (uint8_t)(p + 1);
       pad = (uint8_t)(p + h2 + 1);
       pb = 0;
     } else {
-      t[h2] = 0;
+      buf[p + h2] = 0;
       pad = (uint8_t)(p + 1);
       pb = (uint8_t)(h2 - s + 1);
     }
-    std::memcpy(buf + p, t, h2 + 2);
-    std::memcpy(buf + p + h2 + 2, m, ml);
-    const size_t over = rec - s;
-    uint8_t carry[136];
-    std::memcpy(carry, buf + STROBE_R, over);
-    xor_block(STROBE_R);
-    uint8_t *b = bytes();
-    b[STROBE_R] ^= pad;
-    b[STROBE_R + 1] ^= 0x04 ^ 0x80;
+    // the whole block: words 0..19 and the low 6 bytes of word 20 (bytes 166.. are the
+    // record's overflow into the next block)
+    for (int w = 0; w < 20; w++) {
+      uint64_t v;
+      std::memcpy(&v, buf + 8 * w, 8);
+      st_[w] ^= v;
+    }
+    uint64_t v20;
+    std::memcpy(&v20, buf + 160, 8);
+    st_[20] ^= (v20 & 0x0000ffffffffffffULL) ^ ((uint64_t)pad << 48) ^ ((uint64_t)(0x04 ^ 0x80) << 56);
     keccak_f1600(st_);
-    std::memcpy(buf, carry, over);
+    std::memcpy(buf, buf + STROBE_R, 136);  // the overflow (at most 136 bytes) to the front
     lo = 0;
-    p = over;
+    p = rec - s;
   }
   if (p > lo) xor_block(p);
   pos_ = (uint8_t)p;

@@ -28,6 +28,8 @@ class Strobe128 {
   void prf(uint8_t *d, size_t n, bool more);
   // n merlin append_message(label, msg_i) records (ln, ml <= 64), absorbed block by block
   void append_records(const uint8_t *label, size_t ln, const uint8_t *msgs, size_t ml, size_t n);
+  template <size_t LN, size_t ML>
+  void append_records_t(const uint8_t *label, size_t ln, const uint8_t *msgs, size_t ml, size_t n);
 
  private:
   void run_f();

@@ -169,6 +169,14 @@ class Transcript:
         mp, k2 = _bytes_ptr(message)
         N.load().lcpc_transcript_append_message(self._h, lp, len(label), mp, len(message))
 
+    def append_messages(self, label: bytes, messages: bytes, msg_len: int):
+        """append_message(label, m) for each msg_len-byte m of `messages` (one call)."""
+        if msg_len <= 0 or len(messages) % msg_len:
+            raise ValueError("messages must be whole msg_len-byte records")
+        lp, k1 = _bytes_ptr(label)
+        mp, k2 = _bytes_ptr(messages)
+        N.load().lcpc_transcript_append_messages(self._h, lp, len(label), mp, msg_len, len(messages) // msg_len)
+
     def challenge_bytes(self, label: bytes, n: int) -> bytes:
         lp, k1 = _bytes_ptr(label)
         out = (C.c_uint8 * max(n, 1))()

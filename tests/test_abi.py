@@ -144,6 +144,31 @@ def test_transcript_matches_oracle(api, oracle):
     assert a.challenge_bytes(b"end", 48) == b.challenge_bytes(b"end", 48)
 
 
+@pytest.mark.parametrize("label,msg_len", [(b"$l//PR", 16), (b"$l//PE", 8), (b"$l//PR", 32), (b"lbl", 5),
+                                           (b"x" * 40, 64), (b"", 1), (b"$l//PR", 0)])
+def test_transcript_append_messages_matches_oracle(api, oracle, label, msg_len):
+    """The block-buffered record path (one record after another at every offset of the 166-byte
+    rate, records split across it) against the oracle's message-by-message absorption."""
+    rng = np.random.default_rng(msg_len + len(label))
+    for pre in (0, 1, 7, 100, 131, 165):
+        a, b = api.Transcript(b"test transcript"), oracle.Transcript(b"test transcript")
+        head = rng.integers(0, 256, pre, dtype=np.uint8).tobytes()
+        a.append_message(b"pre", head)
+        b.append_message(b"pre", head)
+        n = 300
+        msgs = rng.integers(0, 256, n * msg_len, dtype=np.uint8).tobytes()
+        if msg_len:
+            a.append_messages(label, msgs, msg_len)
+        else:
+            for _ in range(n):
+                a.append_message(label, b"")
+        for i in range(n):
+            b.append_message(label, msgs[i * msg_len:(i + 1) * msg_len])
+        a.append_message(b"post", head[:3])
+        b.append_message(b"post", head[:3])
+        assert a.challenge_bytes(b"$l//CO", 40) == b.challenge_bytes(b"$l//CO", 40)
+
+
 def test_compute_fails_loudly_without_device(api):
     if api.device_count() > 0:
         pytest.skip("a HIP device is visible; the GPU tests cover this path")
