@@ -502,14 +502,13 @@ lcpc_status finish_commit(lcpc_sharded_commit *c) {
 }
 
 // ---- prove
-lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank, lcpc_transcript *tr,
-                       bool own_tr) {
+// buffers, pinned staging and this rank's slice of the outer tensor (no transcript needed: the
+// pipelined driver does this on a launch worker while the commit is still running)
+lcpc_status prove_alloc(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank) {
   c->root_rank = root_rank;
   c->ndt = c->e->n_degree_tests;
   c->nco = c->e->n_col_opens;
   c->rounds = std::max<size_t>(c->ndt, 1);
-  c->tr = tr;
-  c->own_tr = own_tr;
   const size_t wb = c->wb, np = c->np;
   lcpc_status st;
   HIP_TRY(salloc(c, c->bt, c->n_rows * wb));
@@ -543,6 +542,13 @@ lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_r
     c->p_eval.resize(np * (wb / 8));
   }
   return LCPC_OK;
+}
+
+lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank, lcpc_transcript *tr,
+                       bool own_tr) {
+  c->tr = tr;
+  c->own_tr = own_tr;
+  return prove_alloc(c, outer, root_rank);
 }
 
 // root rank, host: the first challenge (degree-test tensor 0, or the column choice if there
@@ -1064,7 +1070,8 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
               if (!tr) return fail_all(fail(LCPC_ERR_INVALID_ARG, "make_transcript returned NULL"));
             }
             prof::HostScope hs("tick_prove_init");
-            if ((st = prove_init(c, outer, (int)(k % G), tr, true))) return fail_all(st);
+            c->tr = tr;  // (the buffers: prove_alloc, with the subtree stage's launches)
+            c->own_tr = true;
             if (me == c->root_rank && (st = challenge_first(c))) return fail_all(st);
           } else if (c->me == c->root_rank) {
             prof::HostScope hs("tick_wait_challenge");
@@ -1086,9 +1093,12 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     // the compute each exchange feeds, on the polynomials' own streams (launch workers)
     for (auto [k, s] : items) {
       lcpc_sharded_commit *c = cs[k].get();
-      pending[k] = launch.submit(wrap([&pool, c, s = s, S_IDX, S_COLS]() -> lcpc_status {
+      pending[k] = launch.submit(wrap([&pool, c, s = s, k = k, S_IDX, S_COLS, outer, G]() -> lcpc_status {
         if (s == S_CV) return stage_post_cv(c);
-        if (s == S_SUB) return stage_post_subtrees(c);
+        if (s == S_SUB) {
+          const lcpc_status s2 = stage_post_subtrees(c);
+          return s2 ? s2 : prove_alloc(c, outer, (int)(k % G));
+        }
         if (s == S_IDX) return stage_gather_cols(c);
         if (s == S_COLS) return stage_paths(c);
         const size_t r = (s - S_R0) / 2;
