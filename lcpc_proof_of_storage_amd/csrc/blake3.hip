@@ -220,6 +220,76 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
   }
 }
 
+// The same chunks for an element that does not tile a 64-byte block (Ft191: 24 bytes, so
+// elements straddle blocks and chunks).  A block of stream words [gw, gw + 16) starts at word
+// `off` of element e0 = floor((gw - 8) / N); the 4 elements e0 .. e0 + 3 cover it (off + 16 <=
+// N - 1 + 16 <= 4N), elements outside [0, n_rows) -- the 32-byte zero prefix, the tail -- read
+// as zero words.  `off` is the same for every lane of a wave (lanes = columns of one chunk), so
+// the word selection is a uniform switch, not a dynamic register index.
+template <class F, bool CANON>
+__global__ __launch_bounds__(256) void k_leaf_chunks_words(const uint32_t *__restrict__ m, size_t n_rows,
+                                                           size_t n_cols, size_t row_stride, size_t col_stride,
+                                                           uint32_t *__restrict__ cvs, uint8_t *__restrict__ leaves,
+                                                           int n_chunks, size_t row0, int chunk0, int chunk_end) {
+  constexpr int N = F::N;
+  static_assert(4 * N >= N - 1 + 16, "four elements cover a block");
+  const size_t col = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int chunk = chunk0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (col >= n_cols || chunk >= chunk_end) return;
+  const size_t total_words = 8 + n_rows * N;
+  const size_t w0 = (size_t)chunk * 256;
+  const size_t cw = total_words - w0 < 256 ? total_words - w0 : 256;
+  const int nb = (int)((cw + 15) / 16);
+  uint32_t cv[8];
+  iv(cv);
+  const uint32_t *colp = m + col * col_stride * N;
+  for (int b = 0; b < nb; b++) {
+    const long long sw0 = (long long)(w0 + 16 * (size_t)b) - 8;  // stream word of the block's word 0
+    const long long e0 = sw0 >= 0 ? sw0 / N : -((-sw0 + N - 1) / N);
+    const int off = (int)(sw0 - e0 * N);
+    uint32_t w[4 * N];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const long long e = e0 + k;
+      uint32_t r[N];
+      if (e < 0 || (size_t)e >= n_rows) {
+#pragma unroll
+        for (int i = 0; i < N; i++) r[i] = 0;
+      } else {
+        const Fe<F> x = fe_load<F>(colp, ((size_t)e - row0) * row_stride);
+        if constexpr (CANON)
+          fe_canon_repr_words<F>(x, r);
+        else
+          fe_repr_words<F>(x, r);
+      }
+#pragma unroll
+      for (int i = 0; i < N; i++) w[k * N + i] = r[i];
+    }
+    uint32_t msg[16];
+    switch (off) {
+#define LCPC_SEL(o)                                        \
+  case o:                                                  \
+    if constexpr (o + 16 <= 4 * N) {                       \
+      _Pragma("unroll") for (int i = 0; i < 16; i++) msg[i] = w[o + i]; \
+    }                                                      \
+    break;
+      LCPC_SEL(0) LCPC_SEL(1) LCPC_SEL(2) LCPC_SEL(3) LCPC_SEL(4) LCPC_SEL(5) LCPC_SEL(6) LCPC_SEL(7)
+#undef LCPC_SEL
+      default: break;
+    }
+    const size_t left = cw - 16 * (size_t)b;
+    const uint32_t blen = left >= 16 ? 64u : (uint32_t)(4 * left);
+    uint32_t flags = b == 0 ? CHUNK_START : 0u;
+    if (b == nb - 1) flags |= CHUNK_END | (n_chunks == 1 ? ROOT : 0u);
+    compress(cv, msg, (uint64_t)chunk, blen, flags);
+  }
+  if (n_chunks == 1 && leaves) {
+    store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
+  } else {
+    store8(cvs + ((size_t)(chunk - chunk0) * n_cols + col) * 8, cv);
+  }
+}
+
 // Fold n_chunks chaining values of each column into its BLAKE3 root (in place in cvs).
 __global__ __launch_bounds__(256) void k_leaf_merge(uint32_t *__restrict__ cvs, size_t n_cols,
                                                     int n_chunks, uint8_t *__restrict__ leaves) {
@@ -367,7 +437,14 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
                            col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
       return hipGetLastError();
     } else {
-      return hipErrorInvalidValue;
+      prof::Scope ps("leaf_chunks", s);
+      if (canon)
+        hipLaunchKernelGGL((k_leaf_chunks_words<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
+                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
+      else
+        hipLaunchKernelGGL((k_leaf_chunks_words<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
+                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
+      return hipGetLastError();
     }
   });
   if (e != hipSuccess || n_chunks == 1) return e;
@@ -400,7 +477,14 @@ hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows
                            (int)chunk_hi);
       return hipGetLastError();
     } else {
-      return hipErrorInvalidValue;
+      prof::Scope ps("leaf_chunks", s);
+      if (canon)
+        hipLaunchKernelGGL((k_leaf_chunks_words<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
+                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi);
+      else
+        hipLaunchKernelGGL((k_leaf_chunks_words<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
+                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi);
+      return hipGetLastError();
     }
   });
 }

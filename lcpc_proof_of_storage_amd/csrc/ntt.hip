@@ -10,6 +10,7 @@ namespace lcpc {
   hipError_t ntt_tw_table_##n(uint32_t *, int, bool, hipStream_t);
 DECL(ft63)
 DECL(ft127)
+DECL(ft191)
 DECL(ft255)
 DECL(ft253)
 #undef DECL
@@ -18,9 +19,9 @@ int field_words(int fid) {
   return dispatch_field(fid, []<class F>() { return F::N; });
 }
 
-bool field_gpu_supported(int fid) { return fid == 0 || fid == 1 || fid == 3 || fid == 4; }
+bool field_gpu_supported(int fid) { return fid >= 0 && fid <= 4; }
 
-int ntt_max_log_n(int fid) { return fid == 3 || fid == 4 ? 22 : 24; }
+int ntt_max_log_n(int fid) { return fid >= 2 ? 22 : 24; }
 
 hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream_t s) {
   if (!field_gpu_supported(fid) || log_n < 0 || log_n > ntt_max_log_n(fid))
@@ -37,6 +38,7 @@ hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream
   switch (fid) {
     case 0: e = ntt_tw_table_ft63(p.d_tw, log_n, inverse, s); break;
     case 1: e = ntt_tw_table_ft127(p.d_tw, log_n, inverse, s); break;
+    case 2: e = ntt_tw_table_ft191(p.d_tw, log_n, inverse, s); break;
     case 3: e = ntt_tw_table_ft255(p.d_tw, log_n, inverse, s); break;
     default: e = ntt_tw_table_ft253(p.d_tw, log_n, inverse, s); break;
   }
@@ -60,6 +62,7 @@ hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, si
   switch (p.fid) {
     case 0: return ntt_rows_ft63(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
     case 1: return ntt_rows_ft127(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
+    case 2: return ntt_rows_ft191(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
     case 3: return ntt_rows_ft255(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
     case 4: return ntt_rows_ft253(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
     default: return hipErrorInvalidValue;

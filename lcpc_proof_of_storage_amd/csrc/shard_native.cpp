@@ -364,6 +364,8 @@ using ShardPtr = std::unique_ptr<lcpc_sharded_commit, ShardDeleter>;
 lcpc_status check_shardable(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows) {
   if (!e || !comm) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   if (e->kind != KIND_RS) return fail(LCPC_ERR_UNSUPPORTED, "row shards: Ligero / R-S encodings only");
+  if (1024 % field_bytes(e->fid))  // Ft191: an element would straddle two ranks' chunks
+    return fail(LCPC_ERR_UNSUPPORTED, "row shards: the element size must divide a 1 KiB BLAKE3 chunk");
   const int G = comm->nranks;
   if (G < 1 || (G & (G - 1)) || e->n_cols % (size_t)G)
     return fail(LCPC_ERR_UNSUPPORTED, "row shards need a power-of-two rank count dividing n_cols");
@@ -1020,6 +1022,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   for (size_t t = 0; t < n_ticks; t++) {
     prof::HostScope hs_tick("tick_total");
     // last tick's final stages: the proofs go to the pool; finished polynomials free their buffers
+    prof::HostScope hs_fin("tick_finalize");
     for (size_t k : to_finalize) {
       if ((st = settle(k))) return fail_all(st);
       submit_final(k);
@@ -1030,6 +1033,8 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
       cs[finals.front().first].reset();  // every exchange of it is complete (the last landed on the host)
       finals.pop_front();
     }
+    hs_fin.~HostScope();
+    new (&hs_fin) prof::HostScope("tick_schedule");
     std::vector<Xop> ops;
     std::vector<hipEvent_t> done;
     std::vector<std::pair<size_t, size_t>> items;  // (poly, stage)
@@ -1066,6 +1071,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
             if (roots) std::memcpy(roots + 32 * k, c->root, 32);
             lcpc_transcript *tr = nullptr;
             if (me == (int)(k % G)) {
+              prof::HostScope hs2("tick_make_transcript");
               tr = make_transcript(user, k, c->root);
               if (!tr) return fail_all(fail(LCPC_ERR_INVALID_ARG, "make_transcript returned NULL"));
             }
@@ -1091,6 +1097,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
       if ((st = run_group(comm, ops, done))) return fail_all(st);
     }
     // the compute each exchange feeds, on the polynomials' own streams (launch workers)
+    prof::HostScope hs_sub("tick_submit");
     for (auto [k, s] : items) {
       lcpc_sharded_commit *c = cs[k].get();
       pending[k] = launch.submit(wrap([&pool, c, s = s, k = k, S_IDX, S_COLS, outer, G]() -> lcpc_status {

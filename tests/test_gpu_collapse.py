@@ -12,13 +12,13 @@ pytestmark = pytest.mark.gpu
 SHAPES = [(37, 100), (1, 64), (4, 1000), (600, 70), (512, 4096)]
 
 
-@pytest.mark.parametrize("fid", [1, 0, 3])
+@pytest.mark.parametrize("fid", [1, 0, 2, 3])
 @pytest.mark.parametrize("n_rows,n_per_row", SHAPES)
 @pytest.mark.parametrize("n_t", [1, 2, 3, 4])
 def test_collapse_tensors_match_oracle(gpu, oracle, fid, n_rows, n_per_row, n_t):
     from lcpc_proof_of_storage_amd.shard import GpuBackend
-    if fid == 3 and n_rows * n_per_row > 100000:
-        pytest.skip("Ft255: the small shapes suffice")
+    if fid in (2, 3) and n_rows * n_per_row > 100000:
+        pytest.skip("Ft191 / Ft255: the small shapes suffice")
     nl = oracle.limbs(fid)
     n_cols = 1 << (n_per_row.bit_length())
     enc = gpu.LigeroEncoding.new_from_dims(fid, n_per_row, n_cols)

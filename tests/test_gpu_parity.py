@@ -10,7 +10,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-FIELDS = [0, 1, 3, 4]  # Ft63, Ft127, Ft255, Ft253_192 (Ft191 has no GPU kernels)
+FIELDS = [0, 1, 2, 3, 4]  # Ft63, Ft127, Ft191, Ft255, Ft253_192
 
 
 def rand_elems(oracle, fid, n, seed):
@@ -73,6 +73,8 @@ def _commit_both(gpu, oracle, fid, n_per_row, n_cols, length, seed, nco=16, ndt=
     (0, 700, 1024, 700),           # one row
     (3, 512, 1024, 4096),
     (4, 300, 512, 2000),           # big-endian repr field
+    (2, 300, 512, 2000),           # Ft191: 24-byte elements straddle BLAKE3 blocks and chunks
+    (2, 2048, 4096, 100 * 2048 + 9),  # Ft191, 100 rows: a 2424-byte leaf message (3 chunks)
     (1, 8192, 16384, 128 * 8192),  # cfg2 shape: 128 x 8192 -> 16384
 ])
 def test_commit_matches_oracle(gpu, oracle, fid, n_per_row, n_cols, length):
@@ -111,6 +113,7 @@ def test_commit_empty_and_oversized_inputs(gpu, oracle):
     (1, 8192, 16384, 100 * 8192 + 77), # two-pass, ragged last row
     (0, 8192, 16384, 5000),            # two-pass, a single partial row (no full rows)
     (3, 2048, 8192, 3 * 2048 + 1),     # two-pass Ft255, rate 1/4
+    (2, 8192, 16384, 50 * 8192 + 5),   # two-pass Ft191
 ])
 def test_commit_device_matches_oracle(gpu, oracle, hipmem, fid, n_per_row, n_cols, length):
     """lcpc_commit_new_device: coefficients already in HBM (bench path); the commitment's own
@@ -146,6 +149,7 @@ def test_commit_device_matches_oracle(gpu, oracle, hipmem, fid, n_per_row, n_col
     (0, 100, 256, 3000, 128, 3),
     (3, 256, 512, 1000, 40, 1),
     (4, 64, 128, 1000, 20, 2),
+    (2, 512, 1024, 60 * 512 + 3, 64, 2),  # Ft191
 ])
 def test_prove_verify_matches_oracle(gpu, oracle, fid, n_per_row, n_cols, length, nco, ndt):
     coeffs, g_enc, o_enc, g, o = _commit_both(gpu, oracle, fid, n_per_row, n_cols, length, 5, nco, ndt)

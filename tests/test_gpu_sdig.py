@@ -19,7 +19,7 @@ def rand_elems(oracle, fid, n, seed):
     return oracle.ChaCha(seed_u64=seed).field_random(fid, n)
 
 
-@pytest.mark.parametrize("fid", [0, 1, 3, 4])
+@pytest.mark.parametrize("fid", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("n_per_row,code,seed", [(21, 3, 0), (100, 3, 7), (1000, 3, 1), (4096, 3, 0),
                                                  (500, 1, 2), (500, 2, 3), (500, 4, 4), (500, 5, 5),
                                                  (500, 6, 6)])
