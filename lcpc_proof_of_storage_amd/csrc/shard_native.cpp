@@ -355,6 +355,12 @@ struct ShardDeleter {
     Device *d = c->dev;
     c->s = nullptr;
     if (s) (void)hipStreamSynchronize(s);
+    // the stream has drained: no buffer needs its own drain on release (one hipStreamSynchronize
+    // per buffer cost ~0.4 ms per polynomial)
+    for (DBuf *b : {&c->coeffs, &c->comm_rows, &c->hashes, &c->cv, &c->cv_send, &c->cv_recv, &c->sub, &c->subs,
+                    &c->bt, &c->tens, &c->part_d, &c->allpart, &c->sum, &c->canon, &c->didx, &c->mycols,
+                    &c->allcols, &c->dpaths, &c->scratch})
+      b->settle();
     delete c;
     if (s) d->release_stream(s, false);
   }
@@ -988,9 +994,9 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     std::string msg = g_err;
     for (auto &f : pending)
       if (f.valid()) f.wait();
+    for (auto &f : finals) f.second.wait();  // (their tasks reset cs[k])
     for (auto &c : cs)
       if (c && c->next.valid()) c->next.wait();
-    for (auto &f : finals) f.second.wait();
     {
       std::lock_guard<std::mutex> l2(err_mu);
       if (!err_msg.empty()) msg = err_msg;
@@ -1000,11 +1006,13 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   auto submit_final = [&](size_t k) {
     lcpc_sharded_commit *c = cs[k].get();
     lcpc_proof **dst = proofs ? proofs + k : nullptr;
-    finals.emplace_back(k, pool.submit(wrap([c, dst]() -> lcpc_status {
+    // the proof and the polynomial's teardown on the pool: nothing else touches cs[k] any more
+    finals.emplace_back(k, pool.submit(wrap([c, dst, &cs, k]() -> lcpc_status {
                           lcpc_proof *p = nullptr;
                           const lcpc_status s2 = host_proof(c, &p);
                           if (dst) *dst = p;
                           else delete p;
+                          cs[k].reset();
                           return s2;
                         })));
   };
@@ -1022,7 +1030,6 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   for (size_t t = 0; t < n_ticks; t++) {
     prof::HostScope hs_tick("tick_total");
     // last tick's final stages: the proofs go to the pool; finished polynomials free their buffers
-    prof::HostScope hs_fin("tick_finalize");
     for (size_t k : to_finalize) {
       if ((st = settle(k))) return fail_all(st);
       submit_final(k);
@@ -1030,11 +1037,8 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     to_finalize.clear();
     while (!finals.empty() && finals.front().second.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
       if ((st = finals.front().second.get())) return fail_all(st);
-      cs[finals.front().first].reset();  // every exchange of it is complete (the last landed on the host)
       finals.pop_front();
     }
-    hs_fin.~HostScope();
-    new (&hs_fin) prof::HostScope("tick_schedule");
     std::vector<Xop> ops;
     std::vector<hipEvent_t> done;
     std::vector<std::pair<size_t, size_t>> items;  // (poly, stage)
@@ -1128,7 +1132,6 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   while (!finals.empty()) {
     const lcpc_status s2 = finals.front().second.get();
     if (s2 && !first) first = s2;
-    cs[finals.front().first].reset();
     finals.pop_front();
   }
   if (first) {

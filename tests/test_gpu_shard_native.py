@@ -1,5 +1,5 @@
 """GPU: the native row-sharded protocol (csrc/shard_native.cpp through lcpc_comm / lcpc_sharded_*)
-against the single-GPU commit / prove and the oracle, bit for bit.
+against the single-GPU commit / prove and the CPU oracle (every commit + prove case), bit for bit.
 
 * one rank: RCCL with a 1-rank communicator (the RCCL code path: group calls, own-piece copies)
   and the no-exchange comm;
@@ -50,6 +50,21 @@ def _same_proof(a, b):
             and np.array_equal(a["cols"], b["cols"]) and a["paths"] == b["paths"])
 
 
+def _oracle_same(fid, enc, coeffs, outer, root, fields):
+    """the CPU oracle's commit + proof of the same polynomial (the reference's algorithm) against
+    a sharded proof's fields"""
+    sys.path.insert(0, HERE)
+    import oracle_ffi as O
+    nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
+    o_enc = O.Encoding.ligero(fid, enc.n_per_row, enc.n_cols, nco, ndt)
+    oc = O.Commit(o_enc, coeffs.reshape(-1))
+    op = oc.prove(o_enc, outer.reshape(-1), O.standard_transcript(nco, oc.root()))
+    pr = np.concatenate([x.reshape(-1) for x in fields["p_random"]]) if ndt else np.zeros(0, np.uint64)
+    return (oc.root() == root and np.array_equal(fields["p_eval"].reshape(-1), op.p_eval)
+            and np.array_equal(pr, op.p_random) and np.array_equal(fields["cols"].reshape(-1), op.cols)
+            and b"".join(fields["paths"]) == op.paths.tobytes())
+
+
 def _run_rank(L, hipmem, comm, fid, n, seed=9, root_rank=0):
     """commit + prove through the native sharded entry points; returns what rank-0 checks."""
     from lcpc_proof_of_storage_amd import shard
@@ -70,6 +85,7 @@ def _run_rank(L, hipmem, comm, fid, n, seed=9, root_rank=0):
         if comm.rank == root_rank:
             pf = single.prove(outer, enc, _transcript(L, single.get_root(), nco))
             res["proof"] = _same_proof(_proof_fields(spf), _proof_fields(pf))
+            res["oracle"] = _oracle_same(fid, enc, coeffs, outer, sc.get_root(), _proof_fields(spf))
             # and the sharded proof verifies
             inner = L.field_random(fid, enc.n_per_row, seed + 2)
             ev = spf.verify(single.get_root(), outer, inner, enc, _transcript(L, single.get_root(), nco))
