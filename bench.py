@@ -88,11 +88,13 @@ def parse():
     ap.add_argument("--roofline-steps", type=int, default=3,
                     help="serial steps after the timed region whose encode launches give the roofline")
     ap.add_argument("--commit-slots", type=int, default=-1,
-                    help="replicas (ligero / sdig): commits admitted to the GPU at once, first come first "
-                         "served (0: no limit; default 4, 2 for --code sdig, from a sweep on the box).  "
+                    help="replicas (ligero / sdig / pos): commits admitted to the GPU at once, first come first "
+                         "served (0: no limit; default 4, 2 for --code sdig, none for pos, from sweeps on the box).  "
                          "Commits then finish in order and each proof's serial host "
                          "transcript starts while later commits run, instead of every commit of a wave "
                          "finishing together at its end")
+    ap.add_argument("--workers", type=int, default=0,
+                    help="replicas: host worker threads (steps in flight) exactly; 0: --pipeline's rule")
     ap.add_argument("--timeline", default=None,
                     help="replicas (ligero / sdig): write every timed step's gate / commit / prove "
                          "times (s, from the start of the timed region) to this JSON file")
@@ -109,7 +111,7 @@ def parse():
     if args.log_len is None:
         args.log_len = 20 if args.code == "encode" else 24
     if args.commit_slots < 0:
-        args.commit_slots = 2 if args.code == "sdig" else 4
+        args.commit_slots = {"sdig": 2, "pos": 0}.get(args.code, 4)
     if args.pipeline <= 0:
         args.pipeline = 4 if args.code == "pos" else 16
     return args
@@ -389,12 +391,20 @@ def pos_workload(args, L, torch, rank, local_rank):
     from lcpc_proof_of_storage_amd import _native
     lib = _native.load()
 
+    gate = threading.Semaphore(args.commit_slots) if args.commit_slots > 0 else None
+
     def step(slot):
         d_el = slots[slot]
-        rc = lib.lcpc_pos_bytes_to_field_device(d_bytes.data_ptr(), n_bytes, d_el.data_ptr(), None)
-        if rc:
-            raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
-        c = L.LcCommit.commit_device(d_el.data_ptr(), n_el, enc)
+        if gate is not None:
+            gate.acquire()
+        try:
+            rc = lib.lcpc_pos_bytes_to_field_device(d_bytes.data_ptr(), n_bytes, d_el.data_ptr(), None)
+            if rc:
+                raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
+            c = L.LcCommit.commit_device(d_el.data_ptr(), n_el, enc)
+        finally:
+            if gate is not None:
+                gate.release()
         P.verifiable_polynomial_evaluation(c, left)
         c.open_columns(cols)
         return c.get_root()
@@ -800,13 +810,10 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
         args, L, torch, rank, device_idx)
     torch.cuda.synchronize()
     prof = not args.no_prof
-    # in-flight depth: every step in flight at once for short runs, else a divisor of steps, so
-    # the timed region never ends on a partial wave
-    P = max(1, args.pipeline)
-    if args.steps <= 2 * P:
-        P = max(1, args.steps)
-    else:
-        P = max(d for d in range(1, P + 1) if args.steps % d == 0)
+    # in-flight depth: --pipeline workers pull steps from one counter; with the commit gate there
+    # are no waves to align (a K = 20 sweep on the box: 16 workers 11.7-11.8 G/s, 20 workers
+    # 10.5-11.2, 10 workers 10.6-11.8, gpurun_out/r02v)
+    P = args.workers if args.workers > 0 else max(1, min(args.pipeline, args.steps))
     n_workers = P
     warm_left = [max(0, args.warmup)]  # exactly --warmup untimed steps, over whichever workers
     warmup_done = warm_left[0]
