@@ -160,6 +160,20 @@ def replica_seed(rank):
     return SEED + rank
 
 
+def host_cpu_use(c0, c1, elapsed):
+    """Host CPU time this process spent in the timed region, in cores (user + system)."""
+    quota = None
+    try:  # cgroup v2 CPU quota, "max 100000" when unlimited
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return {"cores_busy": ((c1.user - c0.user) + (c1.system - c0.system)) / max(elapsed, 1e-9),
+            "user_s": c1.user - c0.user, "system_s": c1.system - c0.system,
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": quota,
+            "host_wait": os.environ.get("LCPC_HOST_WAIT", "default")}
+
+
 def job_throughput(n_per_step, steps, world, elapsed):
     """Whole-job rate: the units all ranks processed / the max-over-ranks time."""
     return n_per_step * steps * world / elapsed
@@ -864,6 +878,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     L.prof_reset()
     barrier()
     t0 = time.perf_counter()
+    c0 = os.times()
     start.set()
     for w in workers:
         w.join()
@@ -873,6 +888,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     assert all(r == root for r in roots), "nondeterministic root across steps"
     barrier()
     elapsed = time.perf_counter() - t0
+    c1 = os.times()
     if args.timeline and getattr(wl, "timeline", None) is not None:
         tl = [(s_, a - t0, b - t0, c - t0, d - t0) for s_, a, b, c, d in wl.timeline if a >= t0]
         json.dump({"elapsed": elapsed, "steps": sorted(tl, key=lambda r: r[2])}, open(args.timeline, "w"))
@@ -904,6 +920,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     }
     if lat:
         out["latency"] = lat
+    out["host_cpu"] = host_cpu_use(c0, c1, elapsed)
     if stats:
         out["kernels_timed_region"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]}
                                        for k, v in stats.items()}

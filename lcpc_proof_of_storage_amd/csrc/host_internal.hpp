@@ -7,7 +7,9 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <new>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -215,6 +217,17 @@ inline Device *get_device(int id, lcpc_status *st) {
       slot->init_err = std::string("HIP init failed: ") + hipGetErrorString(e);
     } else {
       slot->ok = true;
+      // how host threads wait for the GPU (LCPC_HOST_WAIT=spin|yield|blocking; unset = the
+      // runtime's default).  A spinning wait burns a core of the process's CPU share.
+      if (const char *w = std::getenv("LCPC_HOST_WAIT")) {
+        const std::string m(w);
+        const unsigned f = m == "spin"       ? hipDeviceScheduleSpin
+                           : m == "yield"    ? hipDeviceScheduleYield
+                           : m == "blocking" ? hipDeviceScheduleBlockingSync
+                                             : hipDeviceScheduleAuto;
+        e = hipSetDeviceFlags(f);
+        if (e != hipSuccess) fprintf(stderr, "liblcpc_mi: hipSetDeviceFlags(%s): %s\n", w, hipGetErrorString(e));
+      }
     }
   }
   if (!slot->ok) {
@@ -360,11 +373,81 @@ struct lcpc_commit {
   uint8_t root[32];
 };
 
+// Page-locked host memory for proofs: prove's device -> host copies land in the proof itself
+// (no staging slot and no host memcpy: ~23 MB per Brakedown proof at cfg4), and verify uploads
+// from it by DMA.  Blocks of >= 64 KiB come from a process-wide reuse pool (pinning is slow);
+// smaller ones, and any when the HIP runtime cannot pin (a host-only process), are heap memory.  Elements are default-initialised (resize does not zero).
+struct PinnedHeap {
+  std::mutex mu;
+  std::multimap<size_t, void *> free_;
+  std::map<void *, size_t> size_;
+  static constexpr size_t MIN = (size_t)64 << 10;
+  void *get(size_t bytes) {
+    const size_t want = (bytes + MIN - 1) & ~(MIN - 1);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = free_.lower_bound(want);
+      if (it != free_.end() && it->first <= 2 * want) {
+        void *p = it->second;
+        free_.erase(it);
+        return p;
+      }
+    }
+    void *p = nullptr;
+    if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    size_[p] = want;
+    return p;
+  }
+  // false if p is not one of ours (heap memory)
+  bool put(void *p) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = size_.find(p);
+    if (it == size_.end()) return false;
+    free_.emplace(it->second, p);
+    return true;
+  }
+};
+inline PinnedHeap g_pinned_heap;
+
+template <class T>
+struct PinnedAlloc {
+  using value_type = T;
+  PinnedAlloc() = default;
+  template <class U>
+  PinnedAlloc(const PinnedAlloc<U> &) {}
+  T *allocate(size_t n) {
+    const size_t bytes = n * sizeof(T);
+    void *p = bytes >= PinnedHeap::MIN ? g_pinned_heap.get(bytes) : nullptr;
+    if (!p) p = std::malloc(bytes ? bytes : 1);  // small, or no HIP runtime (host-only use)
+    if (!p) throw std::bad_alloc();
+    return static_cast<T *>(p);
+  }
+  void deallocate(T *p, size_t) {
+    if (!g_pinned_heap.put(p)) std::free(p);
+  }
+  template <class U>
+  void construct(U *p) noexcept {
+    ::new ((void *)p) U;  // default-initialise: the buffers are filled by DMA or memcpy
+  }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    ::new ((void *)p) U(std::forward<A>(a)...);
+  }
+  template <class U>
+  bool operator==(const PinnedAlloc<U> &) const { return true; }
+  template <class U>
+  bool operator!=(const PinnedAlloc<U> &) const { return false; }
+};
+template <class T>
+using pinned_vector = std::vector<T, PinnedAlloc<T>>;
+
 struct lcpc_proof {
   int fid = 1;
   size_t n_cols = 0, n_per_row = 0, n_rows = 0, ndt = 0, nco = 0, path_len = 0;
-  std::vector<uint64_t> p_eval, p_random, cols, col_idx;
-  std::vector<uint8_t> paths;
+  pinned_vector<uint64_t> p_eval, p_random, cols;
+  std::vector<uint64_t> col_idx;
+  pinned_vector<uint8_t> paths;
 };
 
 struct lcpc_transcript {

@@ -365,6 +365,14 @@ lcpc_status lcpc_reserve(const lcpc_encoding *e, size_t len, size_t count) {
     if (s) dev->release_stream(s, false);
   for (hipStream_t s : hi)
     if (s) dev->release_stream(s, true);
+  // the page-locked blocks of `count` proofs (p_random, p_eval, columns, paths)
+  const size_t ndt = e->n_degree_tests;
+  std::vector<void *> pins;
+  for (size_t k = 0; k < count; k++)
+    for (size_t b : {ndt * np * wb, np * wb, nco * nr * wb, nco * pl * 32})
+      if (b >= PinnedHeap::MIN)
+        if (void *p = g_pinned_heap.get(b)) pins.push_back(p);
+  for (void *p : pins) g_pinned_heap.put(p);
   return st;
 }
 
@@ -373,9 +381,10 @@ lcpc_status lcpc_prepare_thread(const lcpc_encoding *e, size_t n_rows) {
   // the sizes lcpc_prove asks of each thread-local slot
   const size_t wb = (size_t)field_bytes(e->fid), np = e->n_per_row, nco = e->n_col_opens;
   const size_t ndt = e->n_degree_tests, pl = log2_np2(e->n_cols);
-  const size_t want[PIN_N] = {2 * np * wb, std::max<size_t>(1, ndt) * np * wb, np * wb,
-                              std::max<size_t>(1, nco * n_rows * wb), nco * pl * 32 + nco * 8, n_rows * wb,
-                              n_rows * wb};
+  (void)ndt;
+  (void)pl;
+  // (p_random, p_eval and the columns land in the proof's own page-locked vectors)
+  const size_t want[PIN_N] = {2 * np * wb, 1, 1, 1, nco * 8, n_rows * wb, n_rows * wb};
   for (int i = 0; i < PIN_N; i++)
     if (!t_pin[i].get(std::max<size_t>(1, want[i]))) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
   return LCPC_OK;
@@ -618,12 +627,14 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   p->nco = nco;
   p->path_len = log2_np2(c->n_cols);
 
-  // pinned staging for everything that crosses PCIe
-  uint8_t *h_prand = (uint8_t *)t_pin[PIN_PRANDOM].get(std::max<size_t>(1, ndt) * np * wb);
-  uint8_t *h_peval = (uint8_t *)t_pin[PIN_PEVAL].get(np * wb);
+  // the proof's own vectors are page-locked (pinned_vector): results land there by DMA
+  p->p_random.resize(ndt * np * limbs);
+  p->p_eval.resize(np * limbs);
+  uint8_t *h_prand = (uint8_t *)p->p_random.data();
+  uint8_t *h_peval = (uint8_t *)p->p_eval.data();
   uint8_t *h_tens = (uint8_t *)t_pin[PIN_TENSOR].get(nr * wb);
   uint8_t *h_outer = (uint8_t *)t_pin[PIN_OUTER].get(nr * wb);
-  if (!h_prand || !h_peval || !h_tens || !h_outer) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  if (!h_tens || !h_outer) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
   std::memcpy(h_outer, outer, nr * wb);
 
   // tensors on device: [t_i | outer] -- the evaluation tensor rides along with the first
@@ -677,10 +688,12 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
 
   // columns (:1101-1115)
   challenge_columns(tr->t, c->n_cols, nco, p->col_idx);
-  uint8_t *h_cols = (uint8_t *)t_pin[PIN_COLS].get(std::max<size_t>(1, nco * nr * wb));
-  uint8_t *h_paths = (uint8_t *)t_pin[PIN_PATHS].get(std::max<size_t>(1, nco * p->path_len * 32 + nco * 8));
-  if (!h_cols || !h_paths) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
-  uint8_t *h_idx = h_paths + nco * p->path_len * 32;
+  p->cols.resize(nco * nr * limbs);
+  p->paths.resize(nco * p->path_len * 32);
+  uint8_t *h_cols = (uint8_t *)p->cols.data();
+  uint8_t *h_paths = p->paths.data();
+  uint8_t *h_idx = (uint8_t *)t_pin[PIN_PATHS].get(std::max<size_t>(1, nco * 8));
+  if (!h_idx) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
   std::memcpy(h_idx, p->col_idx.data(), nco * 8);
   DBuf didx, dcols, dpaths;
   HIP_TRY(didx.alloc(dev, nco * 8));
@@ -697,10 +710,6 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
       HIP_TRY(hipMemcpyAsync(h_paths, dpaths.p, nco * p->path_len * 32, hipMemcpyDeviceToHost, s));
   }
   HIP_TRY(hipStreamSynchronize(s));
-  p->p_random.assign((const uint64_t *)h_prand, (const uint64_t *)(h_prand + ndt * np * wb));
-  p->p_eval.assign((const uint64_t *)h_peval, (const uint64_t *)(h_peval + np * wb));
-  p->cols.assign((const uint64_t *)h_cols, (const uint64_t *)(h_cols + nco * nr * wb));
-  p->paths.assign(h_paths, h_paths + nco * p->path_len * 32);
   *out = p.release();
   return LCPC_OK;
 }

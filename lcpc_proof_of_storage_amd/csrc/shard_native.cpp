@@ -756,8 +756,8 @@ lcpc_status host_proof(lcpc_sharded_commit *c, lcpc_proof **out) {
   p->ndt = c->ndt;
   p->nco = nco;
   p->path_len = log2_np2(c->nc);
-  p->p_eval = c->p_eval;
-  p->p_random = c->p_random;
+  p->p_eval.assign(c->p_eval.begin(), c->p_eval.end());
+  p->p_random.assign(c->p_random.begin(), c->p_random.end());
   p->col_idx = c->col_idx;
   p->cols.resize(nco * n_rows * (wb / 8));
   uint8_t *dst = (uint8_t *)p->cols.data();
