@@ -117,10 +117,16 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
     // element-major codeword [n_cols][n_rows]: the message part is the coefficient matrix
     // transposed, the SDIG levels fill the rest, and each leaf is a contiguous column
     c->col_major = true;
-    HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb,
-                           src_is_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
-    if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
-    HIP_TRY(transpose_elems(fid, (const uint32_t *)cf, n_rows, np, np, np, (uint32_t *)cm, n_rows, s));
+    if (src_is_host) {
+      HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb, hipMemcpyHostToDevice, s));
+      if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
+      HIP_TRY(transpose_elems(fid, (const uint32_t *)cf, n_rows, np, np, np, (uint32_t *)cm, n_rows, s));
+    } else {
+      // one pass over the caller's coefficients writes both the transposed message part and
+      // the commitment's zero-padded row-major copy (no separate device-to-device copy)
+      HIP_TRY(transpose_elems(fid, (const uint32_t *)d_src, n_rows, np, np, np, (uint32_t *)cm, n_rows, s,
+                              TR_PLAIN, nullptr, len, (uint32_t *)cf, np));
+    }
     DBuf tmp;
     HIP_TRY(tmp.alloc(dev, e->sdig.tmp_elems * n_rows * wb));
     HIP_TRY(sdig_encode_cm(e->sdig, (uint32_t *)cm, n_rows, tmp.as<uint32_t>(), s));

@@ -193,18 +193,23 @@ __global__ __launch_bounds__(256) void k_reed_solomon(const uint32_t *__restrict
 // 32 x 32 element tiles through LDS (padded row: no repeated bank pattern down a column).
 // MODE: TR_PLAIN copies elements; TR_FROM_MONT writes canonical values (the PoS on-disk repr);
 // TR_TO_MONT reads canonical values, flags any that is not < p in *bad (from_repr's check).
+// Source elements at flat offset r * ss + c >= n_flat also read as zero.  With `copy`, the
+// (zero-padded) source is also written row-major to copy[r * cs + c] as it is read.
 template <class F, int MODE>
 __global__ __launch_bounds__(256) void k_transpose(const uint32_t *__restrict__ src, size_t rows,
                                                    size_t cols, size_t ss, size_t nv,
                                                    uint32_t *__restrict__ dst, size_t ds,
-                                                   uint32_t *__restrict__ bad) {
+                                                   uint32_t *__restrict__ bad, size_t n_flat,
+                                                   uint32_t *__restrict__ copy, size_t cs) {
   __shared__ Fe<F> tile[32][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const size_t c0 = (size_t)blockIdx.x * 32, r0 = (size_t)blockIdx.y * 32;
   bool ok = true;
   for (int i = ty; i < 32; i += 8) {
     const size_t r = r0 + i, c = c0 + tx;
-    Fe<F> x = (r < rows && c < cols && c < nv) ? fe_load<F>(src, r * ss + c) : fe_zero<F>();
+    Fe<F> x = (r < rows && c < cols && c < nv && r * ss + c < n_flat) ? fe_load<F>(src, r * ss + c)
+                                                                      : fe_zero<F>();
+    if (copy && r < rows && c < cols) fe_store<F>(copy, r * cs + c, x);  // lanes = adjacent columns
     if constexpr (MODE == TR_TO_MONT) {
       ok &= fe_is_canonical<F>(x);
       x = fe_to_mont<F>(x);
@@ -466,21 +471,23 @@ hipError_t sdig_encode_cm(const SdigPlan &plan, uint32_t *cw, size_t R, uint32_t
 
 hipError_t transpose_elems(int fid, const uint32_t *src, size_t rows, size_t cols,
                            size_t src_stride, size_t n_valid, uint32_t *dst, size_t dst_stride,
-                           hipStream_t s, int mode, uint32_t *bad) {
+                           hipStream_t s, int mode, uint32_t *bad, size_t n_flat, uint32_t *copy,
+                           size_t copy_stride) {
   if (!rows || !cols) return hipSuccess;
   if (mode == TR_TO_MONT && !bad) return hipErrorInvalidValue;
+  if (copy && mode != TR_PLAIN) return hipErrorInvalidValue;
   return dispatch_field(fid, [&]<class F>() {
     prof::Scope ps("transpose", s);
     dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));
     if (mode == TR_FROM_MONT)
       hipLaunchKernelGGL((k_transpose<F, TR_FROM_MONT>), grid, dim3(256), 0, s, src, rows, cols,
-                         src_stride, n_valid, dst, dst_stride, bad);
+                         src_stride, n_valid, dst, dst_stride, bad, n_flat, copy, copy_stride);
     else if (mode == TR_TO_MONT)
       hipLaunchKernelGGL((k_transpose<F, TR_TO_MONT>), grid, dim3(256), 0, s, src, rows, cols,
-                         src_stride, n_valid, dst, dst_stride, bad);
+                         src_stride, n_valid, dst, dst_stride, bad, n_flat, copy, copy_stride);
     else
       hipLaunchKernelGGL((k_transpose<F, TR_PLAIN>), grid, dim3(256), 0, s, src, rows, cols,
-                         src_stride, n_valid, dst, dst_stride, bad);
+                         src_stride, n_valid, dst, dst_stride, bad, n_flat, copy, copy_stride);
     return hipGetLastError();
   });
 }

@@ -79,12 +79,14 @@ hipError_t sdig_encode_cm(const SdigPlan &plan, uint32_t *cw, size_t R, uint32_t
                           hipStream_t s);
 
 // dst[c][r] = src[r][c] (element units, row strides src_stride / dst_stride) for r < rows,
-// c < cols; source columns c >= n_valid read as zero.  mode TR_FROM_MONT stores canonical
-// values; TR_TO_MONT reads canonical values into Montgomery form and sets *bad = 1 if any is
-// not < p.
+// c < cols; source columns c >= n_valid, and flat source offsets r * src_stride + c >= n_flat,
+// read as zero.  mode TR_FROM_MONT stores canonical values; TR_TO_MONT reads canonical values
+// into Montgomery form and sets *bad = 1 if any is not < p.  `copy` (TR_PLAIN only) also
+// receives the zero-padded source row-major: copy[r * copy_stride + c], r < rows, c < cols.
 enum { TR_PLAIN = 0, TR_FROM_MONT = 1, TR_TO_MONT = 2 };
 hipError_t transpose_elems(int fid, const uint32_t *src, size_t rows, size_t cols,
                            size_t src_stride, size_t n_valid, uint32_t *dst, size_t dst_stride,
-                           hipStream_t s, int mode = TR_PLAIN, uint32_t *bad = nullptr);
+                           hipStream_t s, int mode = TR_PLAIN, uint32_t *bad = nullptr,
+                           size_t n_flat = SIZE_MAX, uint32_t *copy = nullptr, size_t copy_stride = 0);
 
 }  // namespace lcpc

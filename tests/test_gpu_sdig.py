@@ -88,14 +88,16 @@ def test_sdig_commit_matches_oracle(gpu, oracle, fid, length, seed):
     assert g.get_root() == o.root()
 
 
-def test_sdig_commit_device_input(gpu, oracle, hipmem):
-    fid, length, seed = 1, 10000, 4
+@pytest.mark.parametrize("fid,length,seed", [(1, 10000, 4), (0, 1 << 14, 5), (3, 4097, 6)])
+def test_sdig_commit_device_input(gpu, oracle, hipmem, fid, length, seed):
+    # device input: the transpose writes the message part and the padded coefficient copy
     coeffs, g_enc, o_enc, g, o = _commit_both(gpu, oracle, fid, length, seed)
     d = hipmem.to_device(coeffs)
     try:
         gd = gpu.LcCommit.commit_device(d, length, g_enc)
         assert gd.get_root() == o.root()
         assert np.array_equal(gd.coeffs.reshape(-1), o.coeffs)
+        assert np.array_equal(gd.comm.reshape(-1), o.comm)
         del gd
     finally:
         hipmem.free(d)
