@@ -381,6 +381,7 @@ struct PinnedHeap {
   std::mutex mu;
   std::multimap<size_t, void *> free_;
   std::map<void *, size_t> size_;
+  std::atomic<bool> no_pin{false};
   static constexpr size_t MIN = (size_t)64 << 10;
   void *get(size_t bytes) {
     const size_t want = (bytes + MIN - 1) & ~(MIN - 1);
@@ -393,8 +394,12 @@ struct PinnedHeap {
         return p;
       }
     }
+    if (no_pin.load(std::memory_order_relaxed)) return nullptr;
     void *p = nullptr;
-    if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess) {
+      no_pin.store(true, std::memory_order_relaxed);  // e.g. no HIP runtime: heap memory from now on
+      return nullptr;
+    }
     std::lock_guard<std::mutex> lk(mu);
     size_[p] = want;
     return p;
@@ -408,7 +413,8 @@ struct PinnedHeap {
     return true;
   }
 };
-inline PinnedHeap g_pinned_heap;
+// never destroyed: proofs freed during interpreter teardown still return their blocks safely
+inline PinnedHeap &g_pinned_heap = *new PinnedHeap;
 
 template <class T>
 struct PinnedAlloc {
