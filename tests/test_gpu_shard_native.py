@@ -203,17 +203,17 @@ def _worker(rank, world, port, job, args, q):
         dist.destroy_process_group()
 
 
-def _spawn(job, args, timeout=280):
+def _spawn(job, args, timeout=280, world=2):
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, job, args, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, job, args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=timeout) for _ in range(2))
+    res = dict(q.get(timeout=timeout) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
     return res
@@ -233,6 +233,25 @@ def test_native_sharded_world2_one_gpu(gpu, case, root_rank):
 def test_native_pipeline_world2_one_gpu(gpu):
     res = _spawn("many", (1, 1 << 14, 6, 2))
     for r in (0, 1):
+        assert "error" not in res[r] and all(res[r].values()), (r, res[r])
+
+
+# ---------------------------------------------------------------- four ranks on the one GPU
+# (the rank count of a 4-GPU node; 2^22 splits its 5 BLAKE3 chunks 1/1/1/2, 2^16's single chunk
+# leaves three ranks without rows, 2^20's three chunks leave one)
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("root_rank", [0, 3])
+@pytest.mark.parametrize("fid,n", [(1, 1 << 22), (1, 1 << 16), (0, 3 * 4096 + 17)])
+def test_native_sharded_world4_one_gpu(gpu, fid, n, root_rank):
+    res = _spawn("rank", (fid, n, 9, root_rank), world=4)
+    for r in range(4):
+        assert "error" not in res[r] and all(res[r].values()), (r, res[r])
+
+
+@pytest.mark.timeout(300)
+def test_native_pipeline_world4_one_gpu(gpu):
+    res = _spawn("many", (1, 1 << 20, 6, 2), world=4)
+    for r in range(4):
         assert "error" not in res[r] and all(res[r].values()), (r, res[r])
 
 
