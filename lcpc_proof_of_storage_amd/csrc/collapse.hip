@@ -206,7 +206,30 @@ hipError_t collapse_mfma_t(const uint32_t *coeffs, size_t n_rows, size_t n_per_r
   return hipGetLastError();
 }
 
+// dst[i] = src[i] in 16- or 8-byte words (either side may be page-locked host memory: the
+// prover's results go to host memory by these stores, not by a copy-engine transfer)
+template <class W>
+__global__ void k_copy_words(W *__restrict__ dst, const W *__restrict__ src, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
 }  // namespace
+
+hipError_t copy_words(void *dst, const void *src, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  if (((uintptr_t)dst | (uintptr_t)src | bytes) & 7) return hipErrorInvalidValue;
+  if (!(((uintptr_t)dst | (uintptr_t)src | bytes) & 15)) {
+    const size_t n = bytes / 16;
+    hipLaunchKernelGGL((k_copy_words<uint4>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (uint4 *)dst,
+                       (const uint4 *)src, n);
+  } else {
+    const size_t n = bytes / 8;
+    hipLaunchKernelGGL((k_copy_words<uint2>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (uint2 *)dst,
+                       (const uint2 *)src, n);
+  }
+  return hipGetLastError();
+}
 
 hipError_t collapse_fold_rows(int fid, const uint32_t *vecs, size_t n_vecs, size_t len, uint32_t *out,
                               hipStream_t s) {

@@ -162,9 +162,11 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
     HIP_TRY(leaf_hashes(fid, c->comm.as<uint32_t>(), n_rows, nc, nc, c->hashes.as<uint8_t>(), scratch.p, s,
                         c->canon));
   HIP_TRY(merkle_tree(c->hashes.as<uint8_t>(), np2, s));
-  HIP_TRY(hipMemcpyAsync(c->root, c->hashes.as<uint8_t>() + (c->n_hashes - 1) * 32, 32,
-                         hipMemcpyDeviceToHost, s));
+  uint8_t *h_root = (uint8_t *)t_pin[PIN_OUTER].get(32);
+  if (!h_root) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  HIP_TRY(d2h(h_root, c->hashes.as<uint8_t>() + (c->n_hashes - 1) * 32, 32, s));
   HIP_TRY(hipStreamSynchronize(s));
+  std::memcpy(c->root, h_root, 32);
   c->coeffs.settle();
   c->comm.settle();
   c->hashes.settle();
@@ -649,21 +651,24 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   HIP_TRY(dtens.alloc(dev, 2 * nr * wb));
   HIP_TRY(dres.alloc(dev, 2 * np * wb));
   HIP_TRY(scratch.alloc(dev, collapse_scratch_bytes(fid, nr, np, 2)));
-  HIP_TRY(hipMemcpyAsync(dtens.as<uint8_t>() + nr * wb, h_outer, nr * wb, hipMemcpyHostToDevice, s));
+  HIP_TRY(h2d(dtens.as<uint8_t>() + nr * wb, h_outer, nr * wb, s));
   std::vector<uint64_t> tensor;
   const uint8_t *repr = nullptr;
   bool eval_done = false;
   for (size_t i = 0; i < ndt; i++) {
-    challenge_tensor(tr->t, fid, nr, tensor);
-    std::memcpy(h_tens, tensor.data(), nr * wb);
-    HIP_TRY(hipMemcpyAsync(dtens.p, h_tens, nr * wb, hipMemcpyHostToDevice, s));
-    const int nt = eval_done ? 1 : 2;
-    HIP_TRY(collapse_rows(fid, c->coeffs.as<uint32_t>(), nr, np, dtens.as<uint32_t>(), nt,
-                          dres.as<uint32_t>(), scratch.p, s));
-    HIP_TRY(hipMemcpyAsync(h_prand + i * np * wb, dres.p, np * wb, hipMemcpyDeviceToHost, s));
-    if (!eval_done) {
-      HIP_TRY(hipMemcpyAsync(h_peval, dres.as<uint8_t>() + np * wb, np * wb, hipMemcpyDeviceToHost, s));
-      eval_done = true;
+    {
+      prof::HostScope hs("host_prove_round_issue");
+      challenge_tensor(tr->t, fid, nr, tensor);
+      std::memcpy(h_tens, tensor.data(), nr * wb);
+      HIP_TRY(h2d(dtens.p, h_tens, nr * wb, s));
+      const int nt = eval_done ? 1 : 2;
+      HIP_TRY(collapse_rows(fid, c->coeffs.as<uint32_t>(), nr, np, dtens.as<uint32_t>(), nt,
+                            dres.as<uint32_t>(), scratch.p, s));
+      HIP_TRY(d2h(h_prand + i * np * wb, dres.p, np * wb, s));
+      if (!eval_done) {
+        HIP_TRY(d2h(h_peval, dres.as<uint8_t>() + np * wb, np * wb, s));
+        eval_done = true;
+      }
     }
     {
       prof::HostScope hs("host_prove_gpu_wait");
@@ -679,7 +684,7 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   if (!eval_done) {
     HIP_TRY(collapse_rows(fid, c->coeffs.as<uint32_t>(), nr, np, dtens.as<uint32_t>() + nr * limbs * 2, 1,
                           dres.as<uint32_t>(), scratch.p, s));
-    HIP_TRY(hipMemcpyAsync(h_peval, dres.p, np * wb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(d2h(h_peval, dres.p, np * wb, s));
     d_eval = dres.as<uint32_t>();
   }
   {
@@ -703,7 +708,7 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   std::memcpy(h_idx, p->col_idx.data(), nco * 8);
   DBuf didx, dcols, dpaths;
   HIP_TRY(didx.alloc(dev, nco * 8));
-  if (nco) HIP_TRY(hipMemcpyAsync(didx.p, h_idx, nco * 8, hipMemcpyHostToDevice, s));
+  if (nco) HIP_TRY(h2d(didx.p, h_idx, nco * 8, s));
   HIP_TRY(dcols.alloc(dev, nco * nr * wb));
   HIP_TRY(dpaths.alloc(dev, nco * p->path_len * 32));
   HIP_TRY(gather_columns(fid, c->comm.as<uint32_t>(), nr, c->n_cols, didx.as<uint64_t>(), nco,
@@ -711,11 +716,14 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), nco, p->path_len,
                        dpaths.as<uint8_t>(), s));
   if (nco) {
-    HIP_TRY(hipMemcpyAsync(h_cols, dcols.p, nco * nr * wb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(d2h(h_cols, dcols.p, nco * nr * wb, s));
     if (p->path_len)
-      HIP_TRY(hipMemcpyAsync(h_paths, dpaths.p, nco * p->path_len * 32, hipMemcpyDeviceToHost, s));
+      HIP_TRY(d2h(h_paths, dpaths.p, nco * p->path_len * 32, s));
   }
-  HIP_TRY(hipStreamSynchronize(s));
+  {
+    prof::HostScope hs("host_prove_cols_wait");
+    HIP_TRY(hipStreamSynchronize(s));
+  }
   *out = p.release();
   return LCPC_OK;
 }

@@ -2,6 +2,7 @@
 #include "prof.hpp"
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -53,8 +54,17 @@ void resolve() {  // caller holds mu
 
 bool enabled() { return on; }
 
+// LCPC_PROF_HOST_ONLY=1: record the host phases only (no event pair per launch)
+static bool host_only() {
+  static const bool v = [] {
+    const char *e = getenv("LCPC_PROF_HOST_ONLY");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 Scope::Scope(const char *name, hipStream_t s) : name_(name), s_(s) {
-  if (!on) return;
+  if (!on || host_only()) return;
   {
     std::lock_guard<std::mutex> lk(mu);
     a_ = get_event();

@@ -177,9 +177,9 @@ lcpc_status run_group(lcpc_comm *c, std::vector<Xop> &ops, const std::vector<hip
     for (size_t i = 0; i < ops.size(); i++) {
       const Xop &op = ops[i];
       if (op.kind == Xop::ALL_GATHER && op.bytes)
-        HIP_TRY(hipMemcpyAsync(op.recv, op.send, op.bytes, hipMemcpyDeviceToDevice, op.s));
+        HIP_TRY(d2d(op.recv, op.send, op.bytes, op.s));
       if (op.kind == Xop::ALL_TO_ALL && op.rb[0])
-        HIP_TRY(hipMemcpyAsync(op.recv, op.send, op.rb[0], hipMemcpyDeviceToDevice, op.s));
+        HIP_TRY(d2d(op.recv, op.send, op.rb[0], op.s));
       if (i < done.size()) HIP_TRY(hipEventRecord(done[i], op.s));
     }
     return LCPC_OK;
@@ -190,11 +190,11 @@ lcpc_status run_group(lcpc_comm *c, std::vector<Xop> &ops, const std::vector<hip
     // own pieces: device copies on the comm stream
     for (auto &op : ops) {
       if (op.kind == Xop::ALL_GATHER && op.bytes)
-        HIP_TRY(hipMemcpyAsync(op.recv + (size_t)me * op.bytes, op.send, op.bytes, hipMemcpyDeviceToDevice, cs));
+        HIP_TRY(d2d(op.recv + (size_t)me * op.bytes, op.send, op.bytes, cs));
       if (op.kind == Xop::ALL_TO_ALL && op.rb[me]) {
         size_t so = 0, ro = 0;
         for (int k = 0; k < me; k++) so += op.sb[k], ro += op.rb[k];
-        HIP_TRY(hipMemcpyAsync(op.recv + ro, op.send + so, op.rb[me], hipMemcpyDeviceToDevice, cs));
+        HIP_TRY(d2d(op.recv + ro, op.send + so, op.rb[me], cs));
       }
     }
     if (G > 1) {
@@ -490,7 +490,7 @@ lcpc_status stage_post_subtrees(lcpc_sharded_commit *c) {
   if (G > 1) HIP_TRY(merkle_tree_io(h + (2 * nc - 2 * G) * 32, G, h + (2 * nc - G) * 32, c->s));
   lcpc_status st = c->h_root.get(c->dev, 32);
   if (st) return st;
-  HIP_TRY(hipMemcpyAsync(c->h_root.p, h + (2 * nc - 2) * 32, 32, hipMemcpyDeviceToHost, c->s));
+  HIP_TRY(d2h(c->h_root.p, h + (2 * nc - 2) * 32, 32, c->s));
   HIP_TRY(hipEventRecord(c->ev_host, c->s));
   return LCPC_OK;
 }
@@ -531,8 +531,7 @@ lcpc_status prove_alloc(lcpc_sharded_commit *c, const uint64_t *outer, int root_
   if (c->nr) {  // (h_outer lives until the proof is released, so the copy needs no drain here)
     if ((st = c->h_outer.get(c->dev, c->nr * wb))) return st;
     std::memcpy(c->h_outer.p, (const uint8_t *)outer + c->part[c->me].r_lo * wb, c->nr * wb);
-    HIP_TRY(hipMemcpyAsync(c->tens.as<uint8_t>() + c->nr * wb, c->h_outer.p, c->nr * wb, hipMemcpyHostToDevice,
-                           c->s));
+    HIP_TRY(h2d(c->tens.as<uint8_t>() + c->nr * wb, c->h_outer.p, c->nr * wb, c->s));
   }
   if (c->me == root_rank) {
     HIP_TRY(salloc(c, c->allpart, (size_t)c->G * 2 * np * wb));
@@ -588,7 +587,7 @@ hipStream_t upload_stream(const lcpc_sharded_commit *c) { return c->G == 1 ? c->
 // root: the challenge vector onto the comm stream before the exchange group is issued
 lcpc_status stage_tensor_upload(lcpc_sharded_commit *c, size_t r) {
   if (c->me != c->root_rank || r >= c->ndt) return LCPC_OK;
-  HIP_TRY(hipMemcpyAsync(c->bt.p, c->h_t.p, c->n_rows * c->wb, hipMemcpyHostToDevice, upload_stream(c)));
+  HIP_TRY(h2d(c->bt.p, c->h_t.p, c->n_rows * c->wb, upload_stream(c)));
   return LCPC_OK;
 }
 
@@ -603,8 +602,7 @@ lcpc_status stage_collapse(lcpc_sharded_commit *c, size_t r) {
   } else {
     const uint32_t *tens = c->tens.as<uint32_t>();
     if (!eval_only) {
-      HIP_TRY(hipMemcpyAsync(c->tens.p, c->bt.as<uint8_t>() + c->part[c->me].r_lo * wb, nr * wb,
-                             hipMemcpyDeviceToDevice, c->s));
+      HIP_TRY(d2d(c->tens.p, c->bt.as<uint8_t>() + c->part[c->me].r_lo * wb, nr * wb, c->s));
     } else {
       tens = (const uint32_t *)(c->tens.as<uint8_t>() + nr * wb);
     }
@@ -638,8 +636,8 @@ lcpc_status stage_fold(lcpc_sharded_commit *c, size_t r) {
   const size_t len = (size_t)round_tensors(c, r) * np;
   HIP_TRY(collapse_fold_rows(c->fid, c->allpart.as<uint32_t>(), c->G, len, c->sum.as<uint32_t>(), c->s));
   HIP_TRY(convert(c->fid, c->sum.as<uint32_t>(), c->canon.as<uint32_t>(), len, false, c->s));
-  HIP_TRY(hipMemcpyAsync(c->h_sum.p, c->sum.p, len * wb, hipMemcpyDeviceToHost, c->s));
-  HIP_TRY(hipMemcpyAsync(c->h_repr.p, c->canon.p, len * wb, hipMemcpyDeviceToHost, c->s));
+  HIP_TRY(d2h(c->h_sum.p, c->sum.p, len * wb, c->s));
+  HIP_TRY(d2h(c->h_repr.p, c->canon.p, len * wb, c->s));
   HIP_TRY(hipEventRecord(c->ev_host, c->s));
   return LCPC_OK;
 }
@@ -694,7 +692,7 @@ Xop op_idx_bcast(lcpc_sharded_commit *c) {
 
 lcpc_status stage_idx_upload(lcpc_sharded_commit *c) {
   if (c->me != c->root_rank || !c->nco) return LCPC_OK;
-  HIP_TRY(hipMemcpyAsync(c->didx.p, c->h_idx.p, c->nco * 8, hipMemcpyHostToDevice, upload_stream(c)));
+  HIP_TRY(h2d(c->didx.p, c->h_idx.p, c->nco * 8, upload_stream(c)));
   return LCPC_OK;
 }
 
@@ -733,8 +731,8 @@ lcpc_status stage_paths(lcpc_sharded_commit *c) {
   if (c->nco) {
     HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), 2 * c->nc - 1, c->didx.as<uint64_t>(), c->nco, pl,
                          c->dpaths.as<uint8_t>(), c->s));
-    HIP_TRY(hipMemcpyAsync(c->h_cols.p, c->allcols.p, c->nco * c->n_rows * c->wb, hipMemcpyDeviceToHost, c->s));
-    if (pl) HIP_TRY(hipMemcpyAsync(c->h_paths.p, c->dpaths.p, c->nco * pl * 32, hipMemcpyDeviceToHost, c->s));
+    HIP_TRY(d2h(c->h_cols.p, c->allcols.p, c->nco * c->n_rows * c->wb, c->s));
+    if (pl) HIP_TRY(d2h(c->h_paths.p, c->dpaths.p, c->nco * pl * 32, c->s));
   }
   HIP_TRY(hipEventRecord(c->ev_host, c->s));
   return LCPC_OK;
@@ -887,7 +885,7 @@ size_t lcpc_sharded_commit_n_hashes(const lcpc_sharded_commit *c) { return c ? 2
 lcpc_status lcpc_sharded_commit_copy_hashes(const lcpc_sharded_commit *c, uint8_t *out) {
   if (!c || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   HIP_TRY(hipSetDevice(c->dev->id));
-  HIP_TRY(hipMemcpyAsync(out, c->hashes.p, (2 * c->nc - 1) * 32, hipMemcpyDeviceToHost, c->s));
+  HIP_TRY(d2h(out, c->hashes.p, (2 * c->nc - 1) * 32, c->s));
   HIP_TRY(hipStreamSynchronize(c->s));
   return LCPC_OK;
 }
