@@ -160,6 +160,15 @@ def replica_seed(rank):
     return SEED + rank
 
 
+def cgroup_throttle():
+    """cgroup v2 cpu.stat throttling counters (nr_throttled, throttled_usec), or None."""
+    try:
+        kv = dict(line.split() for line in open("/sys/fs/cgroup/cpu.stat"))
+        return {k: int(kv[k]) for k in ("nr_periods", "nr_throttled", "throttled_usec") if k in kv}
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpu_use(c0, c1, elapsed):
     """Host CPU time this process spent in the timed region, in cores (user + system)."""
     quota = None
@@ -878,7 +887,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     L.prof_reset()
     barrier()
     t0 = time.perf_counter()
-    c0 = os.times()
+    c0, th0 = os.times(), cgroup_throttle()
     start.set()
     for w in workers:
         w.join()
@@ -888,7 +897,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     assert all(r == root for r in roots), "nondeterministic root across steps"
     barrier()
     elapsed = time.perf_counter() - t0
-    c1 = os.times()
+    c1, th1 = os.times(), cgroup_throttle()
     if args.timeline and getattr(wl, "timeline", None) is not None:
         tl = [(s_, a - t0, b - t0, c - t0, d - t0) for s_, a, b, c, d in wl.timeline if a >= t0]
         json.dump({"elapsed": elapsed, "steps": sorted(tl, key=lambda r: r[2])}, open(args.timeline, "w"))
@@ -921,6 +930,8 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     if lat:
         out["latency"] = lat
     out["host_cpu"] = host_cpu_use(c0, c1, elapsed)
+    if th0 and th1:
+        out["host_cpu"]["cgroup_throttled"] = {k: th1[k] - th0[k] for k in th0 if k in th1}
     if stats:
         out["kernels_timed_region"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]}
                                        for k, v in stats.items()}
