@@ -181,7 +181,7 @@ struct Device {
     }
     prof::HostScope hs("rt_hipHostMalloc_pool");
     void *p = nullptr;
-    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(mu);
     pinned_sizes[p] = want;
     return p;
@@ -319,7 +319,7 @@ struct PinnedSlot {
       p = nullptr;
       cap = 0;
       size_t want = n < 4096 ? 4096 : n + n / 4;
-      if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+      if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess) return nullptr;
       cap = want;
     }
     return p;
@@ -502,6 +502,8 @@ inline lcpc_status encode_rows_any(const lcpc_encoding *e, const uint32_t *src, 
 }
 
 // Device address of page-locked (hipHostMalloc'd) host memory, or nullptr for pageable memory.
+// Every page-locked block of this library is allocated hipHostMallocPortable, so it is mapped
+// for every device a thread may switch to.
 inline void *host_dev_ptr(const void *h) {
   if (!h) return nullptr;
   void *d = nullptr;
