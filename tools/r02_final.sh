@@ -12,7 +12,7 @@ $T 560 python -u -m pytest tests -m "gpu and slow" -x -v --timeout 900 --timeout
 $T 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 bash tools/prof_workload.sh ${1:-r02fin}/ligero 20 --warmup 5
 bash tools/prof_workload.sh ${1:-r02fin}/sdig 32 --code sdig --warmup 8
-$T 300 python bench.py --code pos --steps 16 --warmup 4 > $OUT/bench_pos.json 2> $OUT/bench_pos.err
+$T 300 python bench.py --code pos --steps 64 --warmup 4 > $OUT/bench_pos.json 2> $OUT/bench_pos.err
 $T 300 python bench.py --code encode --steps 512 --warmup 32 > $OUT/bench_encode.json 2> $OUT/bench_encode.err
 $T 200 python bench.py --steps 256 --warmup 16 --cpu-baseline off --verify-reps 0 > $OUT/bench_ligero_k256.json 2>> $OUT/bench.err
 $T 200 python bench.py --mode sharded --steps 256 --warmup 8 --lag 4 --cpu-baseline off --verify-reps 0 > $OUT/bench_sharded_k256.json 2>> $OUT/bench.err
