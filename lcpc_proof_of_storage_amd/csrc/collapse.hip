@@ -21,6 +21,7 @@
 #include "kernels.hpp"
 #include "prof.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace lcpc {
@@ -208,10 +209,20 @@ hipError_t collapse_mfma_t(const uint32_t *coeffs, size_t n_rows, size_t n_per_r
 
 // dst[i] = src[i] in 16- or 8-byte words (either side may be page-locked host memory: the
 // prover's results go to host memory by these stores, not by a copy-engine transfer)
+// A few workgroups with a grid-stride loop: a transfer to / from host memory is bound by the
+// link, and a full-size grid would only hold wave slots that the concurrent encodes could use.
 template <class W>
-__global__ void k_copy_words(W *__restrict__ dst, const W *__restrict__ src, size_t n) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dst[i] = src[i];
+__global__ __launch_bounds__(256) void k_copy_words(W *__restrict__ dst, const W *__restrict__ src, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+size_t copy_max_blocks() {  // LCPC_COPY_BLOCKS (A/B knob), default 64
+  static const size_t v = [] {
+    const char *e = getenv("LCPC_COPY_BLOCKS");
+    const long n = e ? atol(e) : 0;
+    return n > 0 ? (size_t)n : (size_t)64;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -221,12 +232,12 @@ hipError_t copy_words(void *dst, const void *src, size_t bytes, hipStream_t s) {
   if (((uintptr_t)dst | (uintptr_t)src | bytes) & 7) return hipErrorInvalidValue;
   if (!(((uintptr_t)dst | (uintptr_t)src | bytes) & 15)) {
     const size_t n = bytes / 16;
-    hipLaunchKernelGGL((k_copy_words<uint4>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (uint4 *)dst,
-                       (const uint4 *)src, n);
+    hipLaunchKernelGGL((k_copy_words<uint4>), dim3((unsigned)std::min((n + 255) / 256, copy_max_blocks())), dim3(256),
+                       0, s, (uint4 *)dst, (const uint4 *)src, n);
   } else {
     const size_t n = bytes / 8;
-    hipLaunchKernelGGL((k_copy_words<uint2>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (uint2 *)dst,
-                       (const uint2 *)src, n);
+    hipLaunchKernelGGL((k_copy_words<uint2>), dim3((unsigned)std::min((n + 255) / 256, copy_max_blocks())), dim3(256),
+                       0, s, (uint2 *)dst, (const uint2 *)src, n);
   }
   return hipGetLastError();
 }
