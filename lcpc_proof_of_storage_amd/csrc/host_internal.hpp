@@ -325,7 +325,7 @@ struct PinnedSlot {
     return p;
   }
 };
-enum { PIN_REPR = 0, PIN_PRANDOM, PIN_PEVAL, PIN_COLS, PIN_PATHS, PIN_TENSOR, PIN_OUTER, PIN_N };
+enum { PIN_REPR = 0, PIN_PRANDOM, PIN_PEVAL, PIN_COLS, PIN_PATHS, PIN_TENSOR, PIN_OUTER, PIN_STAGE, PIN_STAGE2, PIN_N };
 inline thread_local PinnedSlot t_pin[PIN_N];
 
 inline size_t next_pow2(size_t v) {
@@ -527,6 +527,45 @@ inline hipError_t h2d(void *d, const void *h, size_t bytes, hipStream_t s) {
   if (!bytes) return hipSuccess;
   if (void *hd = host_dev_ptr(h); hd && !(((uintptr_t)hd | (uintptr_t)d | bytes) & 7)) return copy_words(d, hd, bytes, s);
   return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
+}
+
+// Device -> any host memory.  Mapped page-locked memory: the copy kernel, asynchronous.
+// Pageable memory: pieces of at most 4 MiB go through this thread's two page-locked staging
+// slots by the copy kernel, double-buffered (the next piece's kernel runs while the host copies
+// the previous one out); returns once the data is in place.
+struct StageEvents {
+  hipEvent_t e[2] = {nullptr, nullptr};
+  ~StageEvents() {
+    for (hipEvent_t x : e)
+      if (x) (void)hipEventDestroy(x);
+  }
+};
+inline thread_local StageEvents t_stage_ev;
+inline hipError_t d2h_staged(void *h, const void *d, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  if (host_dev_ptr(h) || (((uintptr_t)d | bytes) & 7)) return d2h(h, d, bytes, s);
+  constexpr size_t PIECE = (size_t)4 << 20;
+  const size_t first = std::min(bytes, PIECE);
+  uint8_t *stg[2] = {(uint8_t *)t_pin[PIN_STAGE].get(first), (uint8_t *)t_pin[PIN_STAGE2].get(first)};
+  void *sd[2] = {host_dev_ptr(stg[0]), host_dev_ptr(stg[1])};
+  for (int k = 0; k < 2; k++)
+    if (!t_stage_ev.e[k] && hipEventCreateWithFlags(&t_stage_ev.e[k], hipEventDisableTiming) != hipSuccess)
+      t_stage_ev.e[k] = nullptr;
+  if (!sd[0] || !sd[1] || !t_stage_ev.e[0] || !t_stage_ev.e[1])
+    return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
+  const size_t n_pieces = (bytes + PIECE - 1) / PIECE;
+  auto issue = [&](size_t k) -> hipError_t {
+    const size_t off = k * PIECE, n = std::min(PIECE, bytes - off);
+    hipError_t e = copy_words(sd[k & 1], (const uint8_t *)d + off, n, s);
+    return e == hipSuccess ? hipEventRecord(t_stage_ev.e[k & 1], s) : e;
+  };
+  hipError_t e = issue(0);
+  for (size_t k = 0; e == hipSuccess && k < n_pieces; k++) {
+    if (k + 1 < n_pieces) e = issue(k + 1);  // its slot was copied out in the previous iteration
+    if (e == hipSuccess) e = hipEventSynchronize(t_stage_ev.e[k & 1]);
+    if (e == hipSuccess) std::memcpy((uint8_t *)h + k * PIECE, stg[k & 1], std::min(PIECE, bytes - k * PIECE));
+  }
+  return e;
 }
 
 inline hipError_t d2d(void *dst, const void *src, size_t bytes, hipStream_t s) {

@@ -392,7 +392,7 @@ lcpc_status lcpc_prepare_thread(const lcpc_encoding *e, size_t n_rows) {
   (void)ndt;
   (void)pl;
   // (p_random, p_eval and the columns land in the proof's own page-locked vectors)
-  const size_t want[PIN_N] = {2 * np * wb, 1, 1, 1, nco * 8, n_rows * wb, n_rows * wb};
+  const size_t want[PIN_N] = {2 * np * wb, 1, 1, 1, nco * 8, n_rows * wb, n_rows * wb, 1, 1};
   for (int i = 0; i < PIN_N; i++)
     if (!t_pin[i].get(std::max<size_t>(1, want[i]))) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
   return LCPC_OK;
@@ -1271,7 +1271,7 @@ lcpc_status lcpc_pos_eval_encoded(const lcpc_commit *c, const uint64_t *left, si
                         dout.as<uint32_t>(), scratch.p, lease.s));
   // over a canonical matrix the Montgomery products come out as canonical values
   if (c->canon) HIP_TRY(convert(c->fid, dout.as<uint32_t>(), dout.as<uint32_t>(), c->n_cols, true, lease.s));
-  HIP_TRY(hipMemcpyAsync(out, dout.p, c->n_cols * wb, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(d2h_staged(out, dout.p, c->n_cols * wb, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
@@ -1340,9 +1340,9 @@ lcpc_status lcpc_open_columns(const lcpc_commit *c, const uint64_t *idx, size_t 
                          dcol.as<uint32_t>(), lease.s, c->col_major, c->canon));
   HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), c->n_hashes, didx.as<uint64_t>(), n, path_len,
                        dpath.as<uint8_t>(), lease.s));
-  if (cols_out) HIP_TRY(hipMemcpyAsync(cols_out, dcol.p, n * c->n_rows * wb, hipMemcpyDeviceToHost, lease.s));
+  if (cols_out) HIP_TRY(d2h_staged(cols_out, dcol.p, n * c->n_rows * wb, lease.s));
   if (paths_out && path_len)
-    HIP_TRY(hipMemcpyAsync(paths_out, dpath.p, n * path_len * 32, hipMemcpyDeviceToHost, lease.s));
+    HIP_TRY(d2h_staged(paths_out, dpath.p, n * path_len * 32, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
