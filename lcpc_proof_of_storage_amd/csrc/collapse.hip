@@ -227,16 +227,18 @@ size_t copy_max_blocks() {  // LCPC_COPY_BLOCKS (A/B knob), default 64
 
 }  // namespace
 
-hipError_t copy_words(void *dst, const void *src, size_t bytes, hipStream_t s) {
+hipError_t copy_words(void *dst, const void *src, size_t bytes, hipStream_t s, bool over_link) {
   if (!bytes) return hipSuccess;
+  // device-to-device copies are HBM-bound: a full grid; copies over the host link: a few groups
+  const size_t cap = over_link ? copy_max_blocks() : (size_t)1 << 20;
   if (((uintptr_t)dst | (uintptr_t)src | bytes) & 7) return hipErrorInvalidValue;
   if (!(((uintptr_t)dst | (uintptr_t)src | bytes) & 15)) {
     const size_t n = bytes / 16;
-    hipLaunchKernelGGL((k_copy_words<uint4>), dim3((unsigned)std::min((n + 255) / 256, copy_max_blocks())), dim3(256),
+    hipLaunchKernelGGL((k_copy_words<uint4>), dim3((unsigned)std::min((n + 255) / 256, cap)), dim3(256),
                        0, s, (uint4 *)dst, (const uint4 *)src, n);
   } else {
     const size_t n = bytes / 8;
-    hipLaunchKernelGGL((k_copy_words<uint2>), dim3((unsigned)std::min((n + 255) / 256, copy_max_blocks())), dim3(256),
+    hipLaunchKernelGGL((k_copy_words<uint2>), dim3((unsigned)std::min((n + 255) / 256, cap)), dim3(256),
                        0, s, (uint2 *)dst, (const uint2 *)src, n);
   }
   return hipGetLastError();

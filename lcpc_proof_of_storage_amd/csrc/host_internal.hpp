@@ -570,7 +570,7 @@ inline hipError_t d2h_staged(void *h, const void *d, size_t bytes, hipStream_t s
 
 inline hipError_t d2d(void *dst, const void *src, size_t bytes, hipStream_t s) {
   if (!bytes) return hipSuccess;
-  if (!(((uintptr_t)dst | (uintptr_t)src | bytes) & 7)) return copy_words(dst, src, bytes, s);
+  if (!(((uintptr_t)dst | (uintptr_t)src | bytes) & 7)) return copy_words(dst, src, bytes, s, false);
   return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
 }
 

@@ -104,8 +104,8 @@ hipError_t dot(int fid, const uint32_t *a, const uint32_t *b, size_t n, uint32_t
 hipError_t convert(int fid, const uint32_t *in, uint32_t *out, size_t n, bool to_mont,
                    hipStream_t s, uint32_t *bad = nullptr);
 // bytes (a multiple of 8, 8-byte aligned pointers) copied by a kernel on stream s; either side
-// may be device-mapped page-locked host memory
-hipError_t copy_words(void *dst, const void *src, size_t bytes, hipStream_t s);
+// may be device-mapped page-locked host memory (over_link: then a capped grid)
+hipError_t copy_words(void *dst, const void *src, size_t bytes, hipStream_t s, bool over_link = true);
 // chunk-local self-test entry: out = a * b elementwise (Montgomery)
 hipError_t mul_elementwise(int fid, const uint32_t *a, const uint32_t *b, uint32_t *out,
                            size_t n, hipStream_t s);
