@@ -577,7 +577,7 @@ inline hipError_t d2d(void *dst, const void *src, size_t bytes, hipStream_t s) {
 // upload host -> device (pool buffer)
 inline lcpc_status upload(Device *dev, DBuf &b, const void *h, size_t bytes) {
   HIP_TRY(b.alloc(dev, bytes));
-  if (bytes) HIP_TRY(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, t_stream));
+  if (bytes) HIP_TRY(h2d(b.p, h, bytes, t_stream));  // page-locked sources (a proof's vectors): copy kernel
   return LCPC_OK;
 }
 
