@@ -117,6 +117,61 @@ __device__ __forceinline__ Fe<F> fe_sub_lazy(const Fe<F>& a, const Fe<F>& b) {
   return t;  // mod 2^(32N): a - b + p whether or not a - b borrowed
 }
 
+// ---- lazy residues in [0, 2p) (p < R/2, so 2p < R): the NTT passes keep every intermediate
+// value in [0, 2p) and reduce once, at the final store (ntt_v2.hpp)
+template <class F>
+struct TwoP {
+  static constexpr uint32_t limb(int i) {
+    uint64_t c = 0, s = 0;
+    for (int k = 0; k <= i; k++) {
+      s = 2ull * F::P[k] + c;
+      c = s >> 32;
+    }
+    return (uint32_t)s;
+  }
+};
+// a + b for a, b < 2p: the sum (with its carry out) minus 2p when it is >= 2p, in [0, 2p)
+template <class F>
+__device__ __forceinline__ Fe<F> fe_add_2p(const Fe<F>& a, const Fe<F>& b) {
+  static_assert(F::P[F::N - 1] < 0x80000000u, "needs p < R / 2");
+  Fe<F> t, u, r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) t.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) u.v[i] = __builtin_subc(t.v[i], TwoP<F>::limb(i), br, &br);
+  const bool take_u = c | (br ^ 1u);
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = take_u ? u.v[i] : t.v[i];
+  return r;
+}
+// a - b for a, b < 2p, plus 2p when it borrowed: in [0, 2p)
+template <class F>
+__device__ __forceinline__ Fe<F> fe_sub_2p(const Fe<F>& a, const Fe<F>& b) {
+  Fe<F> t, u, r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) t.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) u.v[i] = __builtin_addc(t.v[i], TwoP<F>::limb(i), c, &c);
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = br ? u.v[i] : t.v[i];
+  return r;
+}
+// x < 2p -> x mod p
+template <class F>
+__device__ __forceinline__ Fe<F> fe_reduce_2p(const Fe<F>& x) {
+  Fe<F> u, r;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) u.v[i] = __builtin_subc(x.v[i], F::P[i], br, &br);
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = br ? x.v[i] : u.v[i];
+  return r;
+}
+
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   return (uint64_t)a * (uint64_t)b + c;
 }
@@ -222,7 +277,7 @@ __device__ __forceinline__ void fips_col_step(uint32_t lo, uint32_t hi, uint32_t
 // a carry iff it was nonzero.  Each carry is folded into r2 one product later, so the SGPR a
 // mad writes is not read by the very next instruction.  tools/microbench/femul_variants.hip:
 // Ft127 366 -> 465 G mul/s on MI355X, bit-identical to the CIOS form.
-template <class F>
+template <class F, bool LAZY = false>
 __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
   constexpr int N = F::N;
   uint32_t m[N], out[N];
@@ -263,6 +318,11 @@ __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
   }
   // out + acc * 2^(32N) < 2p: one conditional subtraction
   Fe<F> u, r;
+  if constexpr (LAZY) {  // a < 2p, b < p: the value is < p (1 + 2p/R) < 2p < R, so acc == 0
+#pragma unroll
+    for (int i = 0; i < N; i++) r.v[i] = out[i];
+    return r;
+  }
   uint32_t br = 0;
 #pragma unroll
   for (int i = 0; i < N; i++) u.v[i] = __builtin_subc(out[i], F::P[i], br, &br);
@@ -270,6 +330,14 @@ __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
 #pragma unroll
   for (int i = 0; i < N; i++) r.v[i] = take_u ? u.v[i] : out[i];
   return r;
+}
+
+// a * b R^-1 in [0, 2p) for a < 2p, b < p (no final subtraction)
+template <class F>
+__device__ __forceinline__ Fe<F> fe_mul_lazy(const Fe<F>& a, const Fe<F>& b) {
+  static_assert(F::NP == 0xffffffffu && F::P[0] == 1u, "p = 1 mod 2^32");
+  static_assert(F::P[F::N - 1] < 0x80000000u, "needs p < R / 2");
+  return fe_mul_fips<F, true>(a, b);
 }
 
 // Largest K with K * p < R = 2^(32N) (a safe bound from the top word): a sum of K products,

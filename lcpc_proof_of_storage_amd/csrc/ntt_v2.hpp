@@ -16,8 +16,22 @@
 #include "kernels.hpp"
 #include "prof.hpp"
 
+// LCPC_NTT_LAZY (default 1): butterflies keep residues in [0, 2p) (no final subtraction in the
+// twiddle products), and pass B's final store reduces to [0, p).
+#ifndef LCPC_NTT_LAZY
+#define LCPC_NTT_LAZY 1
+#endif
+
 namespace lcpc {
 namespace ntt_v2 {
+
+#if LCPC_NTT_LAZY
+template <class F>
+__device__ __forceinline__ Fe<F> NTT_MUL(const Fe<F> &a, const Fe<F> &b) { return fe_mul_lazy<F>(a, b); }
+#else
+template <class F>
+__device__ __forceinline__ Fe<F> NTT_MUL(const Fe<F> &a, const Fe<F> &b) { return fe_mul<F>(a, b); }
+#endif
 
 __device__ __forceinline__ int brev(int x, int bits) {
   return bits ? (int)(__builtin_bitreverse32((uint32_t)x) >> (32 - bits)) : 0;
@@ -42,11 +56,22 @@ __device__ __forceinline__ void dif_regs(Fe<F> *x, int b_lo, const Fe<F> *tw) {
       const bool triv = (LOG_GL == 0 && jm == 0);
       if (HALFZ && qq == 0) {
         const Fe<F> a = x[j];
+#if LCPC_NTT_LAZY
+        x[j + h] = triv ? a : fe_mul_lazy<F>(a, tw[(b_lo + jm * GL) << s]);
+#else
         x[j + h] = triv ? a : fe_mul<F>(a, tw[(b_lo + jm * GL) << s]);
+#endif
       } else {
         const Fe<F> a = x[j], c = x[j + h];
+#if LCPC_NTT_LAZY
+        // residues in [0, 2p) throughout; the final store reduces (k_pass_b)
+        x[j] = fe_add_2p<F>(a, c);
+        const Fe<F> d = fe_sub_2p<F>(a, c);
+        x[j + h] = triv ? d : fe_mul_lazy<F>(d, tw[(b_lo + jm * GL) << s]);
+#else
         x[j] = fe_add<F>(a, c);
         x[j + h] = triv ? fe_sub<F>(a, c) : fe_mul<F>(fe_sub_lazy<F>(a, c), tw[(b_lo + jm * GL) << s]);
+#endif
       }
     }
   }
@@ -150,9 +175,9 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
         const size_t e = c * (size_t)brev(t, LOG_S);
         Fe<F> y = x[j];
         if (CANON)
-          y = fe_mul<F>(y, fe_load<F>(twc, e));
+          y = NTT_MUL<F>(y, fe_load<F>(twc, e));
         else if (e)
-          y = fe_mul<F>(y, fe_load<F>(twn, e));
+          y = NTT_MUL<F>(y, fe_load<F>(twn, e));
         fe_store<F>(out, c + ((size_t)t << log_m), y);
       }
       return;
@@ -182,9 +207,9 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
         const size_t e = c * (size_t)brev(t, LOG_S);
         Fe<F> y = x[j];
         if (CANON)
-          y = fe_mul<F>(y, fe_load<F>(twc, e));
+          y = NTT_MUL<F>(y, fe_load<F>(twc, e));
         else if (e)
-          y = fe_mul<F>(y, fe_load<F>(twn, e));
+          y = NTT_MUL<F>(y, fe_load<F>(twn, e));
         fe_store<F>(out, c + ((size_t)t << log_m), y);
       }
     }
@@ -225,7 +250,11 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_b(uint32_t *__restrict__ da
   mid_rounds<F, LOG_S, LOG_CW, LOG_T, R, rr_of<LOG_S, R, 0>(), LOG_S>(tile, tw, tid);
   for (int idx = tid; idx < S * CW; idx += T) {
     const int v = idx >> LOG_S, t = idx & (S - 1);
+#if LCPC_NTT_LAZY
+    fe_store<F>(io, idx, fe_reduce_2p<F>(tile[t * LD + v]));
+#else
     fe_store<F>(io, idx, tile[t * LD + v]);
+#endif
   }
 }
 
