@@ -535,9 +535,28 @@ inline hipError_t h2d(void *d, const void *h, size_t bytes, hipStream_t s) {
 // the previous one out); returns once the data is in place.
 struct StageEvents {
   hipEvent_t e[2] = {nullptr, nullptr};
-  ~StageEvents() {
-    for (hipEvent_t x : e)
+  int dev = -1;  // events belong to the device current when they were created
+  ~StageEvents() { reset(); }
+  void reset() {
+    for (hipEvent_t &x : e) {
       if (x) (void)hipEventDestroy(x);
+      x = nullptr;
+    }
+  }
+  bool ready() {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return false;
+    if (cur != dev) {
+      reset();
+      dev = cur;
+    }
+    for (hipEvent_t &x : e) {
+      if (!x && hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
+        x = nullptr;
+        return false;
+      }
+    }
+    return true;
   }
 };
 inline thread_local StageEvents t_stage_ev;
@@ -548,11 +567,7 @@ inline hipError_t d2h_staged(void *h, const void *d, size_t bytes, hipStream_t s
   const size_t first = std::min(bytes, PIECE);
   uint8_t *stg[2] = {(uint8_t *)t_pin[PIN_STAGE].get(first), (uint8_t *)t_pin[PIN_STAGE2].get(first)};
   void *sd[2] = {host_dev_ptr(stg[0]), host_dev_ptr(stg[1])};
-  for (int k = 0; k < 2; k++)
-    if (!t_stage_ev.e[k] && hipEventCreateWithFlags(&t_stage_ev.e[k], hipEventDisableTiming) != hipSuccess)
-      t_stage_ev.e[k] = nullptr;
-  if (!sd[0] || !sd[1] || !t_stage_ev.e[0] || !t_stage_ev.e[1])
-    return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
+  if (!sd[0] || !sd[1] || !t_stage_ev.ready()) return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
   const size_t n_pieces = (bytes + PIECE - 1) / PIECE;
   auto issue = [&](size_t k) -> hipError_t {
     const size_t off = k * PIECE, n = std::min(PIECE, bytes - off);
