@@ -46,6 +46,40 @@ def test_encode_full_rows(gpu, oracle, fid, log_n):
         assert np.array_equal(got[r], oracle.fft_io(fid, rows[r]))
 
 
+def _words(v: int, nl: int):
+    return [(v >> (64 * i)) & ((1 << 64) - 1) for i in range(nl)]
+
+
+@pytest.mark.parametrize("fid", FIELDS)
+@pytest.mark.parametrize("log_n", [13, 16])
+@pytest.mark.parametrize("pattern", ["max", "alternating", "max_zero_half", "max_halfz"])
+def test_encode_extreme_values(gpu, oracle, fid, log_n, pattern):
+    """Rows of the largest residue p - 1 (raw Montgomery words), alternating 0 / p - 1, and a
+    full-length row whose second half is p - 1: every butterfly sum and difference of the
+    passes' [0, 2p) residues then sits at its carry / borrow boundary."""
+    n = 1 << log_n
+    nl = oracle.limbs(fid)
+    pm1 = oracle.modulus(fid) - 1
+    w = np.array(_words(pm1, nl), np.uint64)
+    if pattern == "max":
+        row = np.tile(w, n)
+    elif pattern == "alternating":
+        row = np.zeros(n * nl, np.uint64)
+        row.reshape(n, nl)[1::2] = w
+    else:
+        row = np.zeros(n * nl, np.uint64)
+        half = slice(n // 2, None) if pattern == "max_zero_half" else slice(0, n // 2)
+        row.reshape(n, nl)[half] = w
+    if pattern == "max_halfz":  # rate-1/2 row: the upper half is known zero (pass A's first stage)
+        enc = gpu.RsEncoding.new(fid, n // 2, n, 4, 1)
+        got = row.copy()
+        enc.encode(got)
+    else:
+        enc = gpu.RsEncoding.new(fid, 1, n, 4, 1)
+        got = enc.encode_rows(row.reshape(1, -1).copy()).reshape(-1)
+    assert np.array_equal(got, oracle.fft_io(fid, row))
+
+
 def test_encode_errors(gpu):
     enc = gpu.RsEncoding.new(1, 8, 16, 4, 1)
     bad = np.zeros(12 * 2, np.uint64)
