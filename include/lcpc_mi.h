@@ -496,6 +496,26 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
                                            void *user, size_t lag, lcpc_proof **proofs,
                                            uint8_t *roots);
 
+/* Host-only (no device): the point-to-point transfers rank `rank` issues, in order, in every
+ * exchange group of lcpc_sharded_commit_prove_many(n_polys, lag) -- the exact list run_group
+ * hands RCCL as ncclSend / ncclRecv between ncclGroupStart / ncclGroupEnd.  Lets a single host
+ * check that every rank's groups match (each send p -> q of n bytes meets a receive on q from p of
+ * n bytes at the same position of the pair's sequence: no deadlock, right byte counts) for any
+ * rank count without a GPU.  These exchanges replace nothing in the reference (its rows never
+ * leave one host, lcpc-2d/src/lib.rs:677-682, 736-815); stage numbers: 0 chaining values,
+ * 1 subtrees, 2 + 2r / 3 + 2r round r's tensor broadcast / partial gather, 2 + 2 rounds column
+ * indices, 3 + 2 rounds opened columns (rounds = max(n_degree_tests, 1)).  *n_out = the record
+ * count; LCPC_ERR_INVALID_ARG if it exceeds cap (out may be NULL with cap 0 to size). */
+typedef struct lcpc_p2p_record {
+  uint32_t tick, pos, poly, stage;
+  int32_t is_send, peer;
+  uint64_t bytes;
+} lcpc_p2p_record;
+lcpc_status lcpc_sharded_p2p_schedule(lcpc_field f, size_t n_rows, size_t n_per_row, size_t n_cols,
+                                      size_t n_degree_tests, size_t n_col_opens, int nranks, int rank,
+                                      size_t n_polys, size_t lag, lcpc_p2p_record *out, size_t cap,
+                                      size_t *n_out);
+
 /* ------------------------------------------------------------------ kernel timing
  * HIP-event timing of every kernel launch on the handle streams (off by default). */
 void lcpc_prof_enable(int enable);

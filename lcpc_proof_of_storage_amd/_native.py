@@ -33,6 +33,12 @@ BROADCAST_FN = C.CFUNCTYPE(C.c_int, vp, vp, sz, C.c_int)
 MAKE_TRANSCRIPT_FN = C.CFUNCTYPE(vp, vp, sz, u8p)
 
 
+class P2pRecord(C.Structure):
+    """lcpc_p2p_record (include/lcpc_mi.h)"""
+    _fields_ = [("tick", C.c_uint32), ("pos", C.c_uint32), ("poly", C.c_uint32), ("stage", C.c_uint32),
+                ("is_send", C.c_int32), ("peer", C.c_int32), ("bytes", C.c_uint64)]
+
+
 class CommOps(C.Structure):
     _fields_ = [("user", vp), ("all_gather", ALL_GATHER_FN), ("all_to_all_v", ALL_TO_ALL_V_FN),
                 ("broadcast", BROADCAST_FN)]
@@ -175,6 +181,8 @@ SIGNATURES = {
     "lcpc_sharded_prove": (i32, [vp, u64p, sz, vp, vp, i32, C.POINTER(vp)]),
     "lcpc_sharded_commit_prove_many": (i32, [vp, C.POINTER(vp), sz, sz, u64p, vp, MAKE_TRANSCRIPT_FN, vp, sz,
                                              C.POINTER(vp), u8p]),
+    "lcpc_sharded_p2p_schedule": (i32, [i32, sz, sz, sz, sz, sz, i32, i32, sz, sz, C.POINTER(P2pRecord), sz,
+                                        szp]),
     "lcpc_prof_enable": (None, [i32]),
     "lcpc_prof_reset": (None, []),
     "lcpc_prof_get": (i32, [C.c_char_p, C.POINTER(C.c_double), u64p]),

@@ -144,7 +144,11 @@ struct Device {
       }
     }
     prof::HostScope hs("rt_hipMalloc");
-    hipError_t e = hipMalloc(p, bytes);
+    // a pool thread's current device is whatever it last set (GPU 0 for a fresh thread): the
+    // block must come from THIS device, so make it current before allocating
+    hipError_t e = hipSetDevice(id);
+    if (e != hipSuccess) return e;
+    e = hipMalloc(p, bytes);
     if (e == hipErrorOutOfMemory) {
       (void)hipGetLastError();
       trim();
@@ -181,6 +185,7 @@ struct Device {
     }
     prof::HostScope hs("rt_hipHostMalloc_pool");
     void *p = nullptr;
+    (void)hipSetDevice(id);
     if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(mu);
     pinned_sizes[p] = want;
@@ -193,6 +198,7 @@ struct Device {
     if (it != pinned_sizes.end()) pinned_free.emplace(it->second, p);
   }
   void trim() {
+    (void)hipSetDevice(id);
     (void)hipDeviceSynchronize();
     std::lock_guard<std::mutex> lk(mu);
     for (auto &kv : free_blocks) {
@@ -386,7 +392,11 @@ struct PinnedHeap {
   std::multimap<size_t, void *> free_;
   std::map<void *, size_t> size_;
   std::atomic<bool> no_pin{false};
+  size_t cached = 0;  // bytes on the free list
   static constexpr size_t MIN = (size_t)64 << 10;
+  // the free list keeps at most this much page-locked memory; blocks returned beyond it are
+  // unpinned (varied proof sizes would otherwise grow the pool without bound)
+  static constexpr size_t CAP = (size_t)4 << 30;
   void *get(size_t bytes) {
     const size_t want = (bytes + MIN - 1) & ~(MIN - 1);
     {
@@ -394,6 +404,7 @@ struct PinnedHeap {
       auto it = free_.lower_bound(want);
       if (it != free_.end() && it->first <= 2 * want) {
         void *p = it->second;
+        cached -= it->first;
         free_.erase(it);
         return p;
       }
@@ -402,7 +413,11 @@ struct PinnedHeap {
     prof::HostScope hs("rt_hipHostMalloc_proof");
     void *p = nullptr;
     if (hipHostMalloc(&p, want, hipHostMallocPortable) != hipSuccess) {
-      no_pin.store(true, std::memory_order_relaxed);  // e.g. no HIP runtime: heap memory from now on
+      (void)hipGetLastError();
+      // latch heap memory only when there is no HIP runtime at all (a host-only process); a
+      // transient failure (e.g. the page-locked limit) falls back for this block alone
+      int n = 0;
+      if (hipGetDeviceCount(&n) != hipSuccess || n == 0) no_pin.store(true, std::memory_order_relaxed);
       return nullptr;
     }
     std::lock_guard<std::mutex> lk(mu);
@@ -414,6 +429,12 @@ struct PinnedHeap {
     std::lock_guard<std::mutex> lk(mu);
     auto it = size_.find(p);
     if (it == size_.end()) return false;
+    if (cached + it->second > CAP) {
+      size_.erase(it);
+      (void)hipHostFree(p);
+      return true;
+    }
+    cached += it->second;
     free_.emplace(it->second, p);
     return true;
   }

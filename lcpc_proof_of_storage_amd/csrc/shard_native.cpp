@@ -89,8 +89,14 @@ Rccl &rccl() {
 // (the root rank's transcript work for several polynomials in flight)
 class TaskPool {
  public:
-  explicit TaskPool(size_t n) {
-    for (size_t i = 0; i < n; i++) th_.emplace_back([this] { run(); });
+  // dev >= 0: every worker makes that device current before its first task (a fresh thread's
+  // current device is GPU 0, and the stages allocate from the device pool and launch there)
+  explicit TaskPool(size_t n, int dev = -1) {
+    for (size_t i = 0; i < n; i++)
+      th_.emplace_back([this, dev] {
+        if (dev >= 0) (void)hipSetDevice(dev);
+        run();
+      });
   }
   ~TaskPool() {
     {
@@ -167,6 +173,59 @@ struct Xop {
   hipStream_t s = nullptr;  // the producing polynomial's compute stream
 };
 
+// One point-to-point transfer of an exchange group on rank `me` (G > 1).  RCCL matches the
+// sends p -> q and the receives on q from p of one group in issue order, so a group is
+// deadlock-free and moves the right bytes iff, for every ordered pair (p, q), p's sends to q and
+// q's receives from p form the same sequence of sizes.  This list is the single source of the
+// RCCL calls (run_group) and of the host-only schedule check (lcpc_sharded_p2p_schedule).
+struct P2p {
+  bool send;
+  int peer;
+  size_t op;  // index of the exchange in the group
+  const uint8_t *sbuf;
+  uint8_t *rbuf;
+  size_t bytes;
+};
+
+std::vector<P2p> p2p_plan(int G, int me, const std::vector<Xop> &ops) {
+  std::vector<P2p> v;
+  for (size_t i = 0; i < ops.size(); i++) {
+    const Xop &op = ops[i];
+    switch (op.kind) {
+      case Xop::ALL_GATHER:
+        if (!op.bytes) break;
+        for (int p = 0; p < G; p++) {
+          if (p == me) continue;
+          v.push_back({true, p, i, op.send, nullptr, op.bytes});
+          v.push_back({false, p, i, nullptr, op.recv + (size_t)p * op.bytes, op.bytes});
+        }
+        break;
+      case Xop::ALL_TO_ALL: {
+        size_t so = 0, ro = 0;
+        for (int p = 0; p < G; p++) {
+          if (p != me) {
+            if (op.sb[p]) v.push_back({true, p, i, op.send + so, nullptr, op.sb[p]});
+            if (op.rb[p]) v.push_back({false, p, i, nullptr, op.recv + ro, op.rb[p]});
+          }
+          so += op.sb[p];
+          ro += op.rb[p];
+        }
+        break;
+      }
+      case Xop::BROADCAST:
+        if (!op.bytes) break;
+        if (me == op.root) {
+          for (int p = 0; p < G; p++)
+            if (p != me) v.push_back({true, p, i, op.recv, nullptr, op.bytes});
+        } else {
+          v.push_back({false, op.root, i, nullptr, op.recv, op.bytes});
+        }
+        break;
+    }
+  }
+  return v;
+}
+
 // Issues one group of exchanges on the comm stream; `done` events are recorded after it.
 lcpc_status run_group(lcpc_comm *c, std::vector<Xop> &ops, const std::vector<hipEvent_t> &done) {
   const int G = c->nranks, me = c->rank;
@@ -197,42 +256,23 @@ lcpc_status run_group(lcpc_comm *c, std::vector<Xop> &ops, const std::vector<hip
         HIP_TRY(d2d(op.recv + ro, op.send + so, op.rb[me], cs));
       }
     }
-    if (G > 1) {
-      Rccl &R = rccl();
-      NCCL_TRY(R.GroupStart());
-      for (auto &op : ops) {
-        switch (op.kind) {
-          case Xop::ALL_GATHER:
-            if (!op.bytes) break;
-            for (int p = 0; p < G; p++) {
-              if (p == me) continue;
-              NCCL_TRY(R.Send(op.send, op.bytes, ncclUint8, p, c->nc, cs));
-              NCCL_TRY(R.Recv(op.recv + (size_t)p * op.bytes, op.bytes, ncclUint8, p, c->nc, cs));
-            }
-            break;
-          case Xop::ALL_TO_ALL: {
-            size_t so = 0, ro = 0;
-            for (int p = 0; p < G; p++) {
-              if (p != me) {
-                if (op.sb[p]) NCCL_TRY(R.Send(op.send + so, op.sb[p], ncclUint8, p, c->nc, cs));
-                if (op.rb[p]) NCCL_TRY(R.Recv(op.recv + ro, op.rb[p], ncclUint8, p, c->nc, cs));
-              }
-              so += op.sb[p];
-              ro += op.rb[p];
-            }
-            break;
-          }
-          case Xop::BROADCAST:
-            if (!op.bytes) break;
-            if (me == op.root) {
-              for (int p = 0; p < G; p++)
-                if (p != me) NCCL_TRY(R.Send(op.recv, op.bytes, ncclUint8, p, c->nc, cs));
-            } else {
-              NCCL_TRY(R.Recv(op.recv, op.bytes, ncclUint8, op.root, c->nc, cs));
-            }
-            break;
+    Rccl &R = rccl();
+    NCCL_TRY(R.GroupStart());
+    {
+      // an error between GroupStart and GroupEnd still closes the group (an open group on this
+      // thread would swallow the next sharded call's exchanges)
+      struct GroupGuard {
+        Rccl &R;
+        bool open = true;
+        ~GroupGuard() {
+          if (open) (void)R.GroupEnd();
         }
+      } guard{R};
+      for (const P2p &x : p2p_plan(G, me, ops)) {
+        if (x.send) NCCL_TRY(R.Send(x.sbuf, x.bytes, ncclUint8, x.peer, c->nc, cs));
+        else NCCL_TRY(R.Recv(x.rbuf, x.bytes, ncclUint8, x.peer, c->nc, cs));
       }
+      guard.open = false;
       NCCL_TRY(R.GroupEnd());
     }
   } else {
@@ -367,17 +407,47 @@ struct ShardDeleter {
 };
 using ShardPtr = std::unique_ptr<lcpc_sharded_commit, ShardDeleter>;
 
-lcpc_status check_shardable(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows) {
-  if (!e || !comm) return fail(LCPC_ERR_INVALID_ARG, "null argument");
-  if (e->kind != KIND_RS) return fail(LCPC_ERR_UNSUPPORTED, "row shards: Ligero / R-S encodings only");
-  if (1024 % field_bytes(e->fid))  // Ft191: an element would straddle two ranks' chunks
+// the shape conditions of a row-sharded commitment (no device needed)
+lcpc_status check_geom(int fid, int kind, size_t n_cols, int G, size_t n_rows) {
+  if (kind != KIND_RS) return fail(LCPC_ERR_UNSUPPORTED, "row shards: Ligero / R-S encodings only");
+  if (1024 % field_bytes(fid))  // Ft191: an element would straddle two ranks' chunks
     return fail(LCPC_ERR_UNSUPPORTED, "row shards: the element size must divide a 1 KiB BLAKE3 chunk");
-  const int G = comm->nranks;
-  if (G < 1 || (G & (G - 1)) || e->n_cols % (size_t)G)
+  if (G < 1 || (G & (G - 1)) || n_cols % (size_t)G)
     return fail(LCPC_ERR_UNSUPPORTED, "row shards need a power-of-two rank count dividing n_cols");
   if (n_rows == 0) return fail(LCPC_ERR_INVALID_ARG, "n_rows");
+  return LCPC_OK;
+}
+
+lcpc_status check_shardable(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows) {
+  if (!e || !comm) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  lcpc_status st = check_geom(e->fid, e->kind, e->n_cols, comm->nranks, n_rows);
+  if (st) return st;
   if (comm->dev != e->dev) return fail(LCPC_ERR_INVALID_ARG, "comm and encoding on different devices");
   return LCPC_OK;
+}
+
+// the partition and sizes every exchange descriptor reads (host only)
+void shard_geom(lcpc_sharded_commit *c, int fid, size_t np, size_t nc, size_t n_rows, int G, int me) {
+  c->fid = fid;
+  c->wb = field_bytes(fid);
+  c->G = G;
+  c->me = me;
+  c->n_rows = n_rows;
+  c->np = np;
+  c->nc = nc;
+  c->B = nc / G;
+  c->n_chunks = leaf_n_chunks(fid, n_rows);
+  c->part = partition(fid, n_rows, G);
+  c->nr = c->part[me].r_hi - c->part[me].r_lo;
+}
+
+// the prove-side sizes (n_degree_tests / n_col_opens of the encoding passed to prove,
+// lcpc-2d/src/lib.rs:1053,1101)
+void prove_geom(lcpc_sharded_commit *c, size_t ndt, size_t nco, int root_rank) {
+  c->root_rank = root_rank;
+  c->ndt = ndt;
+  c->nco = nco;
+  c->rounds = std::max<size_t>(ndt, 1);
 }
 
 lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, ShardPtr &out) {
@@ -385,17 +455,7 @@ lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, S
   c->e = e;
   c->comm = comm;
   c->dev = e->dev;
-  c->fid = e->fid;
-  c->wb = field_bytes(e->fid);
-  c->G = comm->nranks;
-  c->me = comm->rank;
-  c->n_rows = n_rows;
-  c->np = e->n_per_row;
-  c->nc = e->n_cols;
-  c->B = c->nc / c->G;
-  c->n_chunks = leaf_n_chunks(c->fid, n_rows);
-  c->part = partition(c->fid, n_rows, c->G);
-  c->nr = c->part[c->me].r_hi - c->part[c->me].r_lo;
+  shard_geom(c.get(), e->fid, e->n_per_row, e->n_cols, n_rows, comm->nranks, comm->rank);
   HIP_TRY(hipSetDevice(c->dev->id));
   c->s = c->dev->acquire_stream(false);
   if (!c->s) return fail(LCPC_ERR_DEVICE, "no HIP stream");
@@ -512,11 +572,8 @@ lcpc_status finish_commit(lcpc_sharded_commit *c) {
 // ---- prove
 // buffers, pinned staging and this rank's slice of the outer tensor (no transcript needed: the
 // pipelined driver does this on a launch worker while the commit is still running)
-lcpc_status prove_alloc(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank) {
-  c->root_rank = root_rank;
-  c->ndt = c->e->n_degree_tests;
-  c->nco = c->e->n_col_opens;
-  c->rounds = std::max<size_t>(c->ndt, 1);
+lcpc_status prove_alloc(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank, const lcpc_encoding *pe) {
+  prove_geom(c, pe->n_degree_tests, pe->n_col_opens, root_rank);
   const size_t wb = c->wb, np = c->np;
   lcpc_status st;
   HIP_TRY(salloc(c, c->bt, c->n_rows * wb));
@@ -551,11 +608,11 @@ lcpc_status prove_alloc(lcpc_sharded_commit *c, const uint64_t *outer, int root_
   return LCPC_OK;
 }
 
-lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank, lcpc_transcript *tr,
-                       bool own_tr) {
+lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank, const lcpc_encoding *pe,
+                       lcpc_transcript *tr, bool own_tr) {
   c->tr = tr;
   c->own_tr = own_tr;
-  return prove_alloc(c, outer, root_rank);
+  return prove_alloc(c, outer, root_rank, pe);
 }
 
 // root rank, host: the first challenge (degree-test tensor 0, or the column choice if there
@@ -779,8 +836,141 @@ void prove_release(lcpc_sharded_commit *c) {
   c->own_tr = false;
 }
 
-lcpc_status one_group(lcpc_sharded_commit *c, Xop op) {
+// ---- the pipelined schedule (lcpc_sharded_commit_prove_many)
+// Stages of polynomial k: 0 = chaining-value all-to-all, 1 = subtree all-gather, then for each
+// round r a tensor broadcast and a partial-sum gather, then the column-index broadcast and the
+// column gather.  Stage s of polynomial k goes out in tick k + off[s]; off[] leaves `lag` ticks
+// wherever the root rank absorbs one row combination before the next exchange needs its
+// challenge.  Every rank computes the same schedule, so the exchange groups match.
+enum { S_CV = 0, S_SUB = 1, S_R0 = 2 };
+struct Sched {
+  size_t ndt = 0, rounds = 1, n_stages = 0, s_idx = 0, s_cols = 0, n_ticks = 0, lag = 1;
+  std::vector<size_t> off;
+  // the polynomial whose stage s goes out in tick t, or SIZE_MAX
+  size_t poly(size_t t, size_t s, size_t n_polys) const {
+    return (t < off[s] || t - off[s] >= n_polys) ? SIZE_MAX : t - off[s];
+  }
+};
+
+Sched make_sched(size_t ndt, int G, size_t lag, size_t n_polys) {
+  Sched sc;
+  // ~1.3 ms of absorption per round over ~1.1 ms / G per tick (cfg3)
+  sc.lag = lag ? lag : 1 + (size_t)G;
+  sc.ndt = ndt;
+  sc.rounds = std::max<size_t>(ndt, 1);
+  sc.n_stages = 2 + 2 * sc.rounds + 2;
+  sc.off.assign(sc.n_stages, 0);
+  sc.off[S_CV] = 0;
+  sc.off[S_SUB] = 1;
+  sc.off[S_R0] = 3;  // the root rank needs the root on the host and the first challenge
+  sc.off[S_R0 + 1] = sc.off[S_R0] + 1;
+  for (size_t r = 1; r < sc.rounds; r++) {
+    sc.off[S_R0 + 2 * r] = sc.off[S_R0 + 2 * r - 1] + sc.lag;
+    sc.off[S_R0 + 2 * r + 1] = sc.off[S_R0 + 2 * r] + 1;
+  }
+  sc.s_idx = S_R0 + 2 * sc.rounds;
+  sc.s_cols = sc.s_idx + 1;
+  sc.off[sc.s_idx] = sc.off[sc.s_idx - 1] + (ndt ? 2 : 1) * sc.lag;
+  sc.off[sc.s_cols] = sc.off[sc.s_idx] + 1;
+  sc.n_ticks = n_polys + sc.off[sc.s_cols];
+  return sc;
+}
+
+// the exchange of stage s (pure: descriptors only; the stage's host work happens before)
+Xop stage_op(lcpc_sharded_commit *c, const Sched &sc, size_t s) {
+  if (s == S_CV) return op_cv_exchange(c);
+  if (s == S_SUB) return op_subtree_exchange(c);
+  if (s == sc.s_idx) return op_idx_bcast(c);
+  if (s == sc.s_cols) return op_cols_gather(c);
+  const size_t r = (s - S_R0) / 2;
+  return (s - S_R0) % 2 == 0 ? op_tensor_bcast(c, r) : op_partial_gather(c, r);
+}
+
+const char *stage_name(const Sched &sc, size_t s) {
+  if (s == S_CV) return "chaining-value all-to-all";
+  if (s == S_SUB) return "subtree all-gather";
+  if (s == sc.s_idx) return "column-index broadcast";
+  if (s == sc.s_cols) return "opened-column gather";
+  return (s - S_R0) % 2 == 0 ? "challenge-tensor broadcast" : "partial-combination gather";
+}
+
+// ---- watchdog
+// A sharded call whose exchanges never complete (a peer that issued a different group, a dead
+// rank) would block forever in a stream or event wait.  The watchdog thread watches a progress
+// mark the calling thread moves at every tick and wait; when it has not moved for
+// LCPC_SHARD_WATCHDOG_S seconds (default 120; 0 disables) it prints the tick, the stage and the
+// peers on stderr and ends the process with status 75 (no re-exec, no further GPU call).
+class Watchdog {
+ public:
+  Watchdog(int G, int me) : G_(G), me_(me) {
+    const char *v = getenv("LCPC_SHARD_WATCHDOG_S");
+    limit_ = v ? atof(v) : 120.0;
+    if (limit_ > 0) th_ = std::thread([this] { run(); });
+  }
+  ~Watchdog() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  // what the calling thread is about to wait for
+  void mark(size_t tick, size_t n_ticks, const char *what, const std::string &group = std::string()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    tick_ = tick;
+    n_ticks_ = n_ticks;
+    what_ = what;
+    if (!group.empty()) group_ = group;
+    last_ = std::chrono::steady_clock::now();
+  }
+
+ private:
+  void run() {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (!stop_) {
+      cv_.wait_for(lk, std::chrono::milliseconds(500));
+      if (stop_) return;
+      const double idle = std::chrono::duration<double>(std::chrono::steady_clock::now() - last_).count();
+      if (idle > limit_) {
+        fprintf(stderr,
+                "liblcpc_mi watchdog: rank %d of %d made no progress for %.0f s at tick %zu of %zu, waiting on %s;"
+                " the tick's exchange group (poly:stage -> peers): %s\n",
+                me_, G_, idle, tick_, n_ticks_, what_, group_.c_str());
+        fflush(stderr);
+        std::_Exit(75);
+      }
+    }
+  }
+  int G_, me_;
+  double limit_ = 120;
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+  size_t tick_ = 0, n_ticks_ = 0;
+  const char *what_ = "start";
+  std::string group_ = "-";
+  std::chrono::steady_clock::time_point last_ = std::chrono::steady_clock::now();
+};
+
+std::string describe_group(const std::vector<std::pair<size_t, size_t>> &items, const std::vector<Xop> &ops,
+                           const Sched &sc, int G, int me) {
+  std::string g;
+  for (size_t i = 0; i < items.size(); i++) {
+    std::string peers;
+    for (const P2p &x : p2p_plan(G, me, {ops[i]}))
+      peers += (x.send ? " >" : " <") + std::to_string(x.peer);
+    g += "[" + std::to_string(items[i].first) + ":" + stage_name(sc, items[i].second) + (peers.empty() ? " -" : peers) +
+         "] ";
+  }
+  return g.empty() ? "-" : g;
+}
+
+lcpc_status one_group(lcpc_sharded_commit *c, Xop op, Watchdog *wd = nullptr, size_t step = 0,
+                      const char *what = "") {
   std::vector<Xop> ops{std::move(op)};
+  if (wd) wd->mark(step, 0, what);
   return run_group(c->comm, ops, {c->ev_done});
 }
 
@@ -862,11 +1052,13 @@ lcpc_status lcpc_sharded_commit_new_device(const lcpc_encoding *e, const void *d
   std::lock_guard<std::mutex> lk(comm->mu);
   ShardPtr c;
   if ((st = shard_init(e, comm, n_rows, c))) return st;
+  Watchdog wd(comm->nranks, comm->rank);
   if ((st = stage_pre_commit(c.get(), d_rows))) return st;
-  if ((st = one_group(c.get(), op_cv_exchange(c.get())))) return st;
+  if ((st = one_group(c.get(), op_cv_exchange(c.get()), &wd, 0, "chaining-value all-to-all"))) return st;
   if ((st = stage_post_cv(c.get()))) return st;
-  if ((st = one_group(c.get(), op_subtree_exchange(c.get())))) return st;
+  if ((st = one_group(c.get(), op_subtree_exchange(c.get()), &wd, 1, "subtree all-gather"))) return st;
   if ((st = stage_post_subtrees(c.get()))) return st;
+  wd.mark(2, 0, "the commitment root");
   if ((st = finish_commit(c.get()))) return st;
   *out = c.release();
   return LCPC_OK;
@@ -907,30 +1099,29 @@ lcpc_status lcpc_sharded_prove(lcpc_sharded_commit *c, const uint64_t *outer, si
     lcpc_sharded_commit *c;
     ~Cleanup() { prove_release(c); }
   } cleanup{c};
-  if ((st = prove_init(c, outer, root, c->me == root ? tr : nullptr, false))) return st;
+  if ((st = prove_init(c, outer, root, e, c->me == root ? tr : nullptr, false))) return st;
+  Watchdog wd(c->G, c->me);
   if (c->me == root && (st = challenge_first(c))) return st;
   for (size_t r = 0; r < c->rounds; r++) {
     if ((st = stage_tensor_upload(c, r))) return st;
-    if ((st = one_group(c, op_tensor_bcast(c, r)))) return st;
+    if ((st = one_group(c, op_tensor_bcast(c, r), &wd, 2 * r, "challenge-tensor broadcast"))) return st;
     if ((st = stage_collapse(c, r))) return st;
-    if ((st = one_group(c, op_partial_gather(c, r)))) return st;
+    if ((st = one_group(c, op_partial_gather(c, r), &wd, 2 * r + 1, "partial-combination gather"))) return st;
     if ((st = stage_fold(c, r))) return st;
+    wd.mark(2 * r + 1, 0, "the folded row combination");
     if (c->me == root && (st = host_absorb(c, r))) return st;
   }
   if ((st = stage_idx_upload(c))) return st;
-  if ((st = one_group(c, op_idx_bcast(c)))) return st;
+  if ((st = one_group(c, op_idx_bcast(c), &wd, 2 * c->rounds, "column-index broadcast"))) return st;
   if ((st = stage_gather_cols(c))) return st;
-  if ((st = one_group(c, op_cols_gather(c)))) return st;
+  if ((st = one_group(c, op_cols_gather(c), &wd, 2 * c->rounds + 1, "opened-column gather"))) return st;
   if ((st = stage_paths(c))) return st;
+  wd.mark(2 * c->rounds + 2, 0, "the opened columns and paths");
   return host_proof(c, out);
 }
 
 // ---------------------------------------------------------------- the pipelined driver
-// Stages of polynomial k: 0 = chaining-value all-to-all, 1 = subtree all-gather, then for each
-// round r a tensor broadcast and a partial-sum gather, then the column-index broadcast and the
-// column gather.  Stage s of polynomial k goes out in tick k + off[s]; off[] leaves `lag` ticks
-// wherever the root rank absorbs one row combination before the next exchange needs its
-// challenge.  Every rank computes the same schedule, so the exchange groups match.
+// (the schedule: make_sched above)
 lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *const *d_rows, size_t n_polys,
                                            size_t n_rows, const uint64_t *outer, lcpc_comm *comm,
                                            lcpc_make_transcript_fn make_transcript, void *user, size_t lag,
@@ -944,24 +1135,9 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   std::lock_guard<std::mutex> lk(comm->mu);
   HIP_TRY(hipSetDevice(e->dev->id));
   const int G = comm->nranks, me = comm->rank;
-  if (lag == 0) lag = 1 + (size_t)G;  // ~1.3 ms of absorption per round over ~1.1 ms / G per tick (cfg3)
-  const size_t ndt = e->n_degree_tests, rounds = std::max<size_t>(ndt, 1);
-  // stage offsets
-  enum { S_CV = 0, S_SUB = 1, S_R0 = 2 };
-  const size_t n_stages = 2 + 2 * rounds + 2;
-  std::vector<size_t> off(n_stages);
-  off[S_CV] = 0;
-  off[S_SUB] = 1;
-  off[S_R0] = 3;  // the root rank needs the root on the host and the first challenge
-  off[S_R0 + 1] = off[S_R0] + 1;
-  for (size_t r = 1; r < rounds; r++) {
-    off[S_R0 + 2 * r] = off[S_R0 + 2 * r - 1] + lag;
-    off[S_R0 + 2 * r + 1] = off[S_R0 + 2 * r] + 1;
-  }
-  const size_t S_IDX = S_R0 + 2 * rounds, S_COLS = S_IDX + 1;
-  off[S_IDX] = off[S_IDX - 1] + (ndt ? 2 : 1) * lag;
-  off[S_COLS] = off[S_IDX] + 1;
-  const size_t n_ticks = n_polys + off[S_COLS];
+  const Sched sc = make_sched(e->n_degree_tests, G, lag, n_polys);
+  const size_t n_stages = sc.n_stages, S_IDX = sc.s_idx, S_COLS = sc.s_cols, n_ticks = sc.n_ticks;
+  Watchdog wd(G, me);
 
   // Host threads: the main thread issues the exchange groups in schedule order; each
   // polynomial's compute launches after an exchange (and its first encode) run on `launch`
@@ -969,8 +1145,8 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   // exchange: the main thread settles it first), so the main thread's tick is the group plus the
   // waits; the root rank's transcript absorptions and the final proofs run on `pool`.
   const size_t hw = std::max(2u, std::thread::hardware_concurrency());
-  TaskPool pool(std::min<size_t>(16, hw));
-  TaskPool launch(std::min<size_t>(4, hw));
+  TaskPool pool(std::min<size_t>(16, hw), e->dev->id);
+  TaskPool launch(std::min<size_t>(4, hw), e->dev->id);
   std::vector<ShardPtr> cs(n_polys);
   std::vector<std::future<lcpc_status>> pending(n_polys);  // the polynomial's outstanding launch task
   std::deque<std::pair<size_t, std::future<lcpc_status>>> finals;  // (poly, host_proof)
@@ -1027,6 +1203,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   for (size_t k = 0; k < std::min(AHEAD, n_polys); k++) start(k);
   for (size_t t = 0; t < n_ticks; t++) {
     prof::HostScope hs_tick("tick_total");
+    wd.mark(t, n_ticks, "the previous tick's launches");
     // last tick's final stages: the proofs go to the pool; finished polynomials free their buffers
     for (size_t k : to_finalize) {
       if ((st = settle(k))) return fail_all(st);
@@ -1041,33 +1218,30 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     std::vector<hipEvent_t> done;
     std::vector<std::pair<size_t, size_t>> items;  // (poly, stage)
     for (size_t s = 0; s < n_stages; s++) {
-      if (t < off[s] || t - off[s] >= n_polys) continue;
-      const size_t k = t - off[s];
+      const size_t k = sc.poly(t, s, n_polys);
+      if (k == SIZE_MAX) continue;
       {
         prof::HostScope hs("tick_wait_launch");
+        wd.mark(t, n_ticks, "a polynomial's compute launches");
         if ((st = settle(k))) return fail_all(st);
       }
       lcpc_sharded_commit *c = cs[k].get();
-      if (s == S_CV) {
-        ops.push_back(op_cv_exchange(c));
-      } else if (s == S_SUB) {
-        ops.push_back(op_subtree_exchange(c));
-      } else if (s == S_IDX) {
+      // the stage's host work before its exchange
+      if (s == S_IDX) {
         if (c->me == c->root_rank) {
           prof::HostScope hs("tick_wait_challenge");
+          wd.mark(t, n_ticks, "the root rank's transcript (column challenge)");
           if ((st = c->next.get())) return fail_all(st);
         }
         if ((st = stage_idx_upload(c))) return fail_all(st);
-        ops.push_back(op_idx_bcast(c));
-      } else if (s == S_COLS) {
-        ops.push_back(op_cols_gather(c));
-      } else {
+      } else if (s >= S_R0 && s < S_IDX && (s - S_R0) % 2 == 0) {
         const size_t r = (s - S_R0) / 2;
-        if ((s - S_R0) % 2 == 0) {
+        {
           if (r == 0) {
             // the commit is complete (root on the host) and the transcript exists
             {
               prof::HostScope hs("tick_wait_root");
+              wd.mark(t, n_ticks, "the commitment root (subtree exchange)");
               if ((st = finish_commit(c))) return fail_all(st);
             }
             if (roots) std::memcpy(roots + 32 * k, c->root, 32);
@@ -1083,30 +1257,30 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
             if (me == c->root_rank && (st = challenge_first(c))) return fail_all(st);
           } else if (c->me == c->root_rank) {
             prof::HostScope hs("tick_wait_challenge");
+            wd.mark(t, n_ticks, "the root rank's transcript (challenge tensor)");
             if ((st = c->next.get())) return fail_all(st);
           }
           if ((st = stage_tensor_upload(c, r))) return fail_all(st);
-          ops.push_back(op_tensor_bcast(c, r));
-        } else {
-          ops.push_back(op_partial_gather(c, r));
         }
       }
+      ops.push_back(stage_op(c, sc, s));
       done.push_back(c->ev_done);
       items.emplace_back(k, s);
     }
     if (!ops.empty()) {
       prof::HostScope hs("tick_run_group");
+      wd.mark(t, n_ticks, "issuing the exchange group", G > 1 ? describe_group(items, ops, sc, G, me) : std::string());
       if ((st = run_group(comm, ops, done))) return fail_all(st);
     }
     // the compute each exchange feeds, on the polynomials' own streams (launch workers)
     prof::HostScope hs_sub("tick_submit");
     for (auto [k, s] : items) {
       lcpc_sharded_commit *c = cs[k].get();
-      pending[k] = launch.submit(wrap([&pool, c, s = s, k = k, S_IDX, S_COLS, outer, G]() -> lcpc_status {
+      pending[k] = launch.submit(wrap([&pool, c, s = s, k = k, S_IDX, S_COLS, outer, G, e]() -> lcpc_status {
         if (s == S_CV) return stage_post_cv(c);
         if (s == S_SUB) {
           const lcpc_status s2 = stage_post_subtrees(c);
-          return s2 ? s2 : prove_alloc(c, outer, (int)(k % G));
+          return s2 ? s2 : prove_alloc(c, outer, (int)(k % G), e);
         }
         if (s == S_IDX) return stage_gather_cols(c);
         if (s == S_COLS) return stage_paths(c);
@@ -1121,6 +1295,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     }
     if (t + AHEAD < n_polys) start(t + AHEAD);
   }
+  wd.mark(n_ticks, n_ticks, "the last proofs");
   for (size_t k : to_finalize) {
     if ((st = settle(k))) return fail_all(st);
     submit_final(k);
@@ -1138,6 +1313,52 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   }
   HIP_TRY(hipStreamSynchronize(comm->cs));
   return first ? fail(first, msg) : LCPC_OK;
+}
+
+lcpc_status lcpc_sharded_p2p_schedule(lcpc_field f, size_t n_rows, size_t n_per_row, size_t n_cols,
+                                      size_t n_degree_tests, size_t n_col_opens, int nranks, int rank,
+                                      size_t n_polys, size_t lag, lcpc_p2p_record *out, size_t cap,
+                                      size_t *n_out) {
+  if (!valid_field(f) || nranks < 1 || rank < 0 || rank >= nranks || !n_out || (cap && !out))
+    return fail(LCPC_ERR_INVALID_ARG, "arguments");
+  lcpc_status st = check_geom(f, KIND_RS, n_cols, nranks, n_rows);
+  if (st) return st;
+  const Sched sc = make_sched(n_degree_tests, nranks, lag, n_polys);
+  // one descriptor-only shard state per polynomial (no device buffers: offsets from null)
+  std::vector<std::unique_ptr<lcpc_sharded_commit>> cs(n_polys);
+  for (size_t k = 0; k < n_polys; k++) {
+    cs[k] = std::make_unique<lcpc_sharded_commit>();
+    shard_geom(cs[k].get(), f, n_per_row, n_cols, n_rows, nranks, rank);
+    prove_geom(cs[k].get(), n_degree_tests, n_col_opens, (int)(k % nranks));
+  }
+  size_t n = 0;
+  for (size_t t = 0; t < sc.n_ticks; t++) {
+    std::vector<Xop> ops;
+    std::vector<std::pair<size_t, size_t>> items;
+    for (size_t s = 0; s < sc.n_stages; s++) {
+      const size_t k = sc.poly(t, s, n_polys);
+      if (k == SIZE_MAX) continue;
+      ops.push_back(stage_op(cs[k].get(), sc, s));
+      items.emplace_back(k, s);
+    }
+    uint32_t pos = 0;
+    for (const P2p &x : p2p_plan(nranks, rank, ops)) {
+      if (n < cap) {
+        lcpc_p2p_record &r = out[n];
+        r.tick = (uint32_t)t;
+        r.pos = pos;
+        r.poly = (uint32_t)items[x.op].first;
+        r.stage = (uint32_t)items[x.op].second;
+        r.is_send = x.send ? 1 : 0;
+        r.peer = x.peer;
+        r.bytes = x.bytes;
+      }
+      n++;
+      pos++;
+    }
+  }
+  *n_out = n;
+  return n > cap ? fail(LCPC_ERR_INVALID_ARG, "cap") : LCPC_OK;
 }
 
 }  // extern "C"

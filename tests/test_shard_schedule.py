@@ -1,0 +1,132 @@
+"""CPU: the RCCL exchange groups of the pipelined row-sharded driver match across ranks.
+
+lcpc_sharded_p2p_schedule (include/lcpc_mi.h) returns, for one rank, the exact ncclSend /
+ncclRecv list run_group issues in every group of lcpc_sharded_commit_prove_many.  RCCL pairs the
+sends p -> q and the receives on q from p of one group in issue order, so the multi-rank path is
+deadlock-free and moves the right bytes iff, in every tick, p's sends to q and q's receives from
+p are the same sequence of sizes.  Checked here for 2, 4 and 8 ranks at cfg3 (Ft127 2^24:
+512 x 32768 -> 65536, 309 opens, 2 degree tests) and at ragged shapes, without a GPU.  The
+exchanges replace nothing in the reference (its rows never leave one host,
+lcpc-2d/src/lib.rs:677-682, 736-815); the byte counts are checked against that layout.
+"""
+import collections
+import ctypes as C
+
+import pytest
+
+from lcpc_proof_of_storage_amd import _native
+
+FT63, FT127, FT255 = 0, 1, 3
+WB = {FT63: 8, FT127: 16, FT255: 32}
+
+
+def schedule(fid, n_rows, np_, nc, ndt, nco, G, rank, n_polys, lag=0):
+    lib = _native.load()
+    n = C.c_size_t()
+    assert lib.lcpc_sharded_p2p_schedule(fid, n_rows, np_, nc, ndt, nco, G, rank, n_polys, lag, None, 0,
+                                         C.byref(n)) in (0, 30)
+    buf = (_native.P2pRecord * max(n.value, 1))()
+    rc = lib.lcpc_sharded_p2p_schedule(fid, n_rows, np_, nc, ndt, nco, G, rank, n_polys, lag, buf, n.value,
+                                       C.byref(n))
+    assert rc == 0, _native.last_error()
+    return [(r.tick, r.pos, r.poly, r.stage, bool(r.is_send), r.peer, r.bytes) for r in buf[:n.value]]
+
+
+def rows_of(fid, n_rows, G):
+    lib = _native.load()
+    out = []
+    for g in range(G):
+        r0, nr = C.c_size_t(), C.c_size_t()
+        assert lib.lcpc_sharded_rows(fid, n_rows, G, g, C.byref(r0), C.byref(nr)) == 0
+        out.append((r0.value, nr.value))
+    return out
+
+
+def check_matching(fid, n_rows, np_, nc, ndt, nco, G, n_polys, lag=0):
+    sched = [schedule(fid, n_rows, np_, nc, ndt, nco, G, g, n_polys, lag) for g in range(G)]
+    sends = collections.defaultdict(list)  # (tick, p, q) -> [(poly, stage, bytes)]
+    recvs = collections.defaultdict(list)
+    for g, recs in enumerate(sched):
+        last = (-1, -1)
+        for tick, pos, poly, stage, is_send, peer, nbytes in recs:
+            assert (tick, pos) > last, "records out of group order"
+            last = (tick, pos)
+            assert 0 <= peer < G and peer != g and nbytes > 0
+            if is_send:
+                sends[(tick, g, peer)].append((poly, stage, nbytes))
+            else:
+                recvs[(tick, peer, g)].append((poly, stage, nbytes))
+    assert set(sends) == set(recvs), "a tick has sends without matching receives (or the reverse)"
+    for key in sends:
+        assert sends[key] == recvs[key], f"tick {key[0]}: {key[1]}->{key[2]} sends {sends[key]} vs recvs {recvs[key]}"
+    return sched
+
+
+def stage_bytes(sched, stage, poly=0):
+    """bytes rank g sends / receives in (poly, stage)"""
+    out = []
+    for recs in sched:
+        s = sum(r[6] for r in recs if r[2] == poly and r[3] == stage and r[4])
+        v = sum(r[6] for r in recs if r[2] == poly and r[3] == stage and not r[4])
+        out.append((s, v))
+    return out
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_cfg3_groups_match(G):
+    n_rows, np_, nc, ndt, nco = 512, 32768, 65536, 2, 309
+    sched = check_matching(FT127, n_rows, np_, nc, ndt, nco, G, n_polys=20)
+    wb = WB[FT127]
+    rows = rows_of(FT127, n_rows, G)
+    n_chunks = -(-(32 + n_rows * wb) // 1024)
+    B = nc // G
+    # stage 0: rank g sends its chunks' chaining values of block k to rank k (32 B per column)
+    for g, (sb, rb) in enumerate(stage_bytes(sched, 0)):
+        nch_g = (g + 1) * n_chunks // G - g * n_chunks // G
+        assert sb == (G - 1) * nch_g * B * 32
+        assert rb == (n_chunks - nch_g) * B * 32
+    # stage 1: all-gather of the (2B - 1)-digest subtrees
+    for sb, rb in stage_bytes(sched, 1):
+        assert sb == rb == (G - 1) * (2 * B - 1) * 32
+    # poly 0's root is rank 0: tensor broadcasts (n_rows elements), then its partial sums
+    # (2 tensors in round 0, 1 after), then the column indices and column pieces
+    rounds = max(ndt, 1)
+    for r in range(rounds):
+        bc = stage_bytes(sched, 2 + 2 * r)
+        assert bc[0] == ((G - 1) * n_rows * wb, 0) and all(x == (0, n_rows * wb) for x in bc[1:])
+        nt = 2 if r == 0 else 1
+        ga = stage_bytes(sched, 3 + 2 * r)
+        assert ga[0] == (0, (G - 1) * nt * np_ * wb) and all(x == (nt * np_ * wb, 0) for x in ga[1:])
+    idx = stage_bytes(sched, 2 + 2 * rounds)
+    assert idx[0] == ((G - 1) * nco * 8, 0)
+    cols = stage_bytes(sched, 3 + 2 * rounds)
+    assert cols[0][1] == nco * (n_rows - rows[0][1]) * wb
+    assert all(cols[g] == (nco * rows[g][1] * wb, 0) for g in range(1, G))
+
+
+@pytest.mark.parametrize("fid,n_rows,np_,nc,ndt,nco,G", [
+    (FT127, 37, 64, 128, 2, 7, 4),   # ragged rows: some ranks' row shards differ in size
+    (FT127, 3, 16, 32, 1, 5, 4),     # fewer rows than ranks: empty shards
+    (FT63, 100, 128, 256, 3, 11, 8),
+    (FT255, 9, 64, 128, 0, 4, 2),    # no degree tests: round 0 is the evaluation alone
+    (FT127, 512, 32768, 65536, 2, 309, 8),
+])
+@pytest.mark.parametrize("lag", [0, 1, 5])
+def test_ragged_groups_match(fid, n_rows, np_, nc, ndt, nco, G, lag):
+    check_matching(fid, n_rows, np_, nc, ndt, nco, G, n_polys=7, lag=lag)
+
+
+def test_every_rank_has_the_same_group_structure():
+    G = 4
+    sched = [schedule(FT127, 512, 32768, 65536, 2, 309, G, g, 9) for g in range(G)]
+    # each tick's (poly, stage) set with traffic is seen by all ranks (an all-to-all / gather
+    # stage involves every rank)
+    per_rank = [{(r[0], r[2], r[3]) for r in recs} for recs in sched]
+    assert per_rank[0] == per_rank[1] == per_rank[2] == per_rank[3]
+
+
+def test_schedule_rejects_bad_rank_counts():
+    lib = _native.load()
+    n = C.c_size_t()
+    assert lib.lcpc_sharded_p2p_schedule(FT127, 512, 32768, 65536, 2, 309, 3, 0, 4, 0, None, 0, C.byref(n)) != 0
+    assert lib.lcpc_sharded_p2p_schedule(2, 512, 32768, 65536, 2, 309, 2, 0, 4, 0, None, 0, C.byref(n)) != 0  # Ft191
