@@ -104,8 +104,8 @@ def parse():
                          "4 for --code pos (a 1 GiB request's 2.3 GiB codeword per slot: deeper "
                          "pipelines only contend for HBM)")
     args = ap.parse_args()
-    if args.code != "ligero":
-        args.mode = "replicas"  # cfg2 / cfg4 / cfg5 run as independent steps per rank
+    if args.code in ("sdig", "encode"):
+        args.mode = "replicas"  # cfg2 / cfg4 run as independent steps per rank
     if args.mode == "auto":
         args.mode = "sharded" if args.gpus > 1 else "replicas"
     if args.log_len is None:
@@ -673,7 +673,9 @@ def main():
     import lcpc_proof_of_storage_amd as L
 
     L.set_device(device_idx)
-    if args.mode == "sharded":
+    if args.mode == "sharded" and args.code == "pos":
+        out = run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share)
+    elif args.mode == "sharded":
         out = run_sharded(args, L, torch, dist, rank, world, device, backend, share)
     else:
         out = run_replicas(args, L, torch, dist, rank, world, device_idx, backend)
@@ -822,6 +824,114 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
             out["cpu_baseline_1core"] = {"value": n / dt1, "unit": "field-elements/s", "cores": 1, "kind": "port",
                                          "sample": f"{sample1}: one run on 1 thread ({dt1:.2f} s)"}
             out["parity_root_vs_oracle"] = out["parity_root_vs_oracle"] and oroot1 == roots[0]
+    return out
+
+
+# ---------------------------------------------------------------- cfg5 over several GPUs
+def run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share):
+    """cfg5 with ONE file's rows sharded over the ranks: every step is one proof-of-storage
+    request (networking/server.rs:652-737) on the whole file -- each rank packs its rows' bytes
+    (data_field.rs:38-46), the rows are committed together (lcpc_sharded_commit_new_device), and
+    u^T Enc(M) plus the client's 256 columns with paths come back on rank 0
+    (lcpc_sharded_pos_request).  Steps are serial (each is two collectives)."""
+    from lcpc_proof_of_storage_amd import pos as P
+    from lcpc_proof_of_storage_amd import shard
+    n_bytes = args.pos_bytes
+    n_el = -(-n_bytes // 7)
+    np_, nc, snd = P.get_aspect_ratio_default_from_file_len(n_bytes)
+    n_rows = -(-n_el // np_)
+    enc = L.LigeroEncoding.new_from_dims(L.FT63, np_, nc)
+    r0, nr = shard.sharded_rows(L.FT63, n_rows, world, rank)
+    host = np.random.default_rng(1).integers(0, 256, n_bytes, dtype=np.uint8)  # the same file on every rank
+    lo, hi = min(n_bytes, 7 * np_ * r0), min(n_bytes, 7 * np_ * (r0 + nr))
+    mine = np.zeros(-(-(hi - lo) // 8) * 8 + 8, np.uint8)
+    mine[:hi - lo] = host[lo:hi]
+    d_bytes = torch.from_numpy(mine).to(device)
+    d_rows = torch.zeros(max(nr * np_, 1), dtype=torch.int64, device=device)
+    x = L.field_random(L.FT63, 1, 1337)
+    left, _ = P.form_side_vectors_for_polynomial_evaluation_from_point(x, n_rows, nc)
+    cols = P.get_column_indicies_from_random_seed(1337, 256, nc)
+    torch.cuda.synchronize()
+    if world == 1:
+        comm, comm_kind = shard.NativeComm.single(), "none (one rank)"
+    elif backend == "nccl" and not share:
+        comm, comm_kind = shard.NativeComm.rccl(dist), "RCCL (liblcpc_mi lcpc_comm_rccl_new, device send/recv)"
+    else:
+        comm, comm_kind = shard.NativeComm.host(dist), "host-staged gloo collectives (ranks share one GPU)"
+
+    def step():
+        if hi > lo:
+            shard.pos_pack_shard(d_bytes.data_ptr() - lo, n_bytes, np_, r0, nr, d_rows.data_ptr())
+        sc = shard.ShardedCommit(enc, comm, d_rows.data_ptr() if nr else 0, n_rows)
+        res = sc.pos_request(left, cols, root=0)
+        return sc.get_root(), res
+
+    def barrier():
+        sync_barrier(dist, torch.cuda.synchronize)
+
+    for _ in range(max(1, args.warmup)):
+        root, res0 = step()
+    L.prof_enable(False)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r_, _ = step()
+        assert r_ == root, "nondeterministic root across steps"
+    barrier()
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0, "cpu" if backend == "gloo" else device)
+    iso = {}
+    if not args.no_prof:
+        L.prof_reset()
+        L.prof_enable(True)
+        for _ in range(args.roofline_steps):
+            step()
+        L.prof_enable(False)
+        iso = L.prof_stats()
+    value = n_el * args.steps / elapsed
+    out = {
+        "metric": "proof-of-storage server request: committed field-elements/s (pack+commit+eval+256-col open), "
+                  f"{n_bytes / 2**30:g} GiB file, rows sharded over the GPUs",
+        "value": value, "unit": "field-elements/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u64 (WriteableFt63 Montgomery limbs)",
+        "data": f"synthetic: {n_bytes} random bytes (numpy default_rng(1)), each rank's rows resident in its HBM",
+        "config": {"workload": f"PoS request on one {n_bytes}-byte file: {n_el} WriteableFt63 elements, default "
+                               f"dims {n_rows}x{np_}->{nc}, u^T Enc(M) at a point, 256 opened columns",
+                   "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd,
+                   "parallelism": f"rows sharded x{world} (lcpc_sharded_commit_new_device + lcpc_sharded_pos_request)",
+                   "exchanges": comm_kind, "rows_on_rank0": nr},
+        "mb_per_s": n_bytes * args.steps / elapsed / 1e6,
+    }
+    wl = Workload(algo_bytes=nr * np_ * 8 + nr * nc * 8, enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
+                  enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, this rank's "
+                                  f"{nr} rows)",
+                  traffic_key=(n_el, "Ft63", "pos"), mul_count=nr * ntt_muls(nc),
+                  mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass "
+                            "twiddles per row", leaf_compressions=0)
+    out.update(roofline_objects(wl, iso, {}, args, traffic_rows_frac=nr / n_rows))
+    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    if rank == 0:
+        # parity of this run's answers against the oracle on a bounded sample is the replicas
+        # line's job (bench.py --code pos); here the root and the request's digests are reported
+        import hashlib
+        ev, opened = res0
+        out["answer_digests"] = {"root": root.hex(), "eval_sha256": hashlib.sha256(ev.tobytes()).hexdigest(),
+                                 "cols_sha256": hashlib.sha256(b"".join(o.col.tobytes() for o in opened)).hexdigest()}
+    if rank == 0 and want_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ffi as O  # CPU baseline only
+        sample = host[: n_bytes // 16]
+        el = O.pos_bytes_to_field(sample.tobytes())
+        o_enc = O.Encoding.ligero(0, np_, nc)
+        cores, basis = available_cores()
+        O.lib().of_set_threads(cores)
+        t1 = time.perf_counter()
+        oc = O.Commit(o_enc, el)
+        O.collapse(0, oc.comm, O.pos_side_vectors(0, x.reshape(-1), oc.n_rows, nc)[0], oc.n_rows, nc)
+        dt = (time.perf_counter() - t1) * 16
+        out["cpu_baseline"] = {"value": n_el / dt, "unit": "field-elements/s", "cores": cores, "kind": "port",
+                               "sample": f"commit + u^T Enc(M) of the first 1/16 of the file, scaled to the whole "
+                                         f"file ({dt / 16:.2f} s)", "cores_basis": basis}
     return out
 
 

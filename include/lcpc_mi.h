@@ -481,6 +481,18 @@ lcpc_status lcpc_sharded_commit_copy_hashes(const lcpc_sharded_commit *c, uint8_
 lcpc_status lcpc_sharded_prove(lcpc_sharded_commit *c, const uint64_t *outer, size_t outer_len,
                                const lcpc_encoding *e, lcpc_transcript *tr, int root,
                                lcpc_proof **out);
+/* Collective proof-of-storage request on a row-sharded file commitment (networking/server.rs:
+ * 652-737; the file's WriteableFt63 rows split over the ranks as above): on rank `root`,
+ * eval_out (n_cols elements) = verifiable_polynomial_evaluation (proof-of-storage/src/
+ * lcpc_online.rs:454-484), sum_r left[r] comm[r][j] over the ENCODED matrix -- the ranks'
+ * partial sums over their rows gathered and folded mod p -- and cols_out / paths_out the n_open
+ * requested columns (whole columns [k][n_rows], Montgomery, as lcpc_open_columns) with their
+ * Merkle paths.  left (n_rows elements) and idx (n_open) are host inputs on every rank; outputs
+ * are written on `root` only (NULL skips one).  Replaces lcpc_pos_eval_encoded +
+ * lcpc_open_columns (lcpc_online.rs:454-484, 226-247) for one file committed over several GPUs. */
+lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *left, size_t n_rows,
+                                     const uint64_t *idx, size_t n_open, int root,
+                                     uint64_t *eval_out, uint64_t *cols_out, uint8_t *paths_out);
 /* Pipelined commit + prove of n_polys row-sharded polynomials (a proof-of-storage server's
  * objects, the bench's steps): polynomial i reads this rank's rows at d_rows[i] and is proved on
  * rank i % nranks, whose transcript is make_transcript(user, i, root_i) (the library frees it);

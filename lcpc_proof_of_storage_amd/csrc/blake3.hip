@@ -220,6 +220,96 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
   }
 }
 
+// The same chunks for a column-major matrix ([column][row], a column's message words contiguous
+// in memory: the SDIG commitments and the PoS column files).  Read lane-per-column, every load of
+// a wave touches 64 columns n_rows * B bytes apart; here the wave loads each 64-byte block of its
+// 64 columns cooperatively instead -- 4 adjacent lanes read one column's block, so a load
+// instruction covers 16 columns x 64 contiguous bytes -- and hands the blocks over through LDS
+// (double buffered, rows padded to 80 B so the per-column reads are bank-conflict free).  Needs
+// n_rows * N % 4 == 0 (16-B aligned columns); the message word w of a column is memory word w - 8
+// of the column (w >= 8), and a 4-word unit lies wholly inside or outside the message.
+template <class F, bool CANON>
+__global__ __launch_bounds__(256) void k_leaf_chunks_cm(const uint32_t *__restrict__ m, size_t n_rows,
+                                                        size_t n_cols, uint32_t *__restrict__ cvs,
+                                                        uint8_t *__restrict__ leaves, int n_chunks) {
+  constexpr int N = F::N;
+  static_assert(16 % N == 0 && 8 % N == 0, "element must tile a BLAKE3 block");
+  constexpr int EPB = 16 / N;
+  __shared__ uint4 stage[4][2][64][5];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t col0 = (size_t)blockIdx.x * 64, col = col0 + lane;
+  const int chunk = blockIdx.y * 4 + wave;
+  if (chunk >= n_chunks) return;  // whole waves
+  const size_t msg_words = 8 + n_rows * N;  // the column's message, in words
+  const size_t w0 = (size_t)chunk * 256;
+  const size_t cw = msg_words - w0 < 256 ? msg_words - w0 : 256;
+  const int nb = (int)((cw + 15) / 16);
+  const int unit = lane & 3, csub = lane >> 2;
+  // block b's 4 loads of this lane: unit `unit` (words 4 unit .. +3) of column col0 + csub + 16 i
+  auto gload = [&](int b, uint4 r[4]) {
+    const size_t w = w0 + 16 * (size_t)b + 4 * unit;  // message word
+    const bool in = w >= 8 && w < msg_words;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const size_t c = col0 + csub + 16 * i;
+      r[i] = in && c < n_cols ? reinterpret_cast<const uint4 *>(m + c * n_rows * N + (w - 8))[0]
+                              : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lput = [&](int buf, const uint4 r[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) stage[wave][buf][csub + 16 * i][unit] = r[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  uint32_t cv[8];
+  iv(cv);
+  uint4 r[4];
+  gload(0, r);
+  lput(0, r);
+  for (int b = 0; b < nb; b++) {
+    const bool more = b + 1 < nb;
+    if (more) gload(b + 1, r);
+    uint32_t msg[16];
+    {
+      const uint4 *row = stage[wave][b & 1][lane];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint4 q = row[k];
+        msg[4 * k] = q.x; msg[4 * k + 1] = q.y; msg[4 * k + 2] = q.z; msg[4 * k + 3] = q.w;
+      }
+    }
+    // element words -> repr words (Montgomery -> canonical unless CANON); the zero prefix and
+    // words past the message stay zero either way (from_mont(0) = 0, and they load as zero)
+#pragma unroll
+    for (int k = 0; k < EPB; k++) {
+      Fe<F> e;
+#pragma unroll
+      for (int i = 0; i < N; i++) e.v[i] = msg[k * N + i];
+      uint32_t w[N];
+      if constexpr (CANON)
+        fe_canon_repr_words<F>(e, w);
+      else
+        fe_repr_words<F>(e, w);
+#pragma unroll
+      for (int i = 0; i < N; i++) msg[k * N + i] = w[i];
+    }
+    const size_t left = cw - 16 * (size_t)b;
+    const uint32_t blen = left >= 16 ? 64u : (uint32_t)(4 * left);
+    uint32_t flags = b == 0 ? CHUNK_START : 0u;
+    if (b == nb - 1) flags |= CHUNK_END | (n_chunks == 1 ? ROOT : 0u);
+    compress(cv, msg, (uint64_t)chunk, blen, flags);
+    if (more) lput((b + 1) & 1, r);
+  }
+  if (col >= n_cols) return;
+  if (n_chunks == 1 && leaves) {
+    store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
+  } else {
+    store8(cvs + ((size_t)chunk * n_cols + col) * 8, cv);
+  }
+}
+
 // The same chunks for an element that does not tile a 64-byte block (Ft191: 24 bytes, so
 // elements straddle blocks and chunks).  A block of stream words [gw, gw + 16) starts at word
 // `off` of element e0 = floor((gw - 8) / N); the 4 elements e0 .. e0 + 3 cover it (off + 16 <=
@@ -429,6 +519,15 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
   hipError_t e = dispatch_field(fid, [&]<class F>() {
     if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
       prof::Scope ps("leaf_chunks", s);
+      if (row_stride == 1 && col_stride == n_rows && (n_rows * F::N) % 4 == 0) {  // column-major, 16-B aligned
+        if (canon)
+          hipLaunchKernelGGL((k_leaf_chunks_cm<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols,
+                             (uint32_t *)scratch, leaves, n_chunks);
+        else
+          hipLaunchKernelGGL((k_leaf_chunks_cm<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols,
+                             (uint32_t *)scratch, leaves, n_chunks);
+        return hipGetLastError();
+      }
       if (canon)
         hipLaunchKernelGGL((k_leaf_chunks<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
                            col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);

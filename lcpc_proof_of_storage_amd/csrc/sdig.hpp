@@ -55,10 +55,9 @@ struct CsrDev {
   size_t rows = 0, cols = 0, nnz = 0;
   const uint32_t *ptr = nullptr, *idx = nullptr, *val = nullptr;
   // Ft127 matrix-core form (sdig.hip, k_spmm_mfma): every output's nonzeros padded to groups of
-  // 4; gptr[j] = first group of output j, pidx = input index per padded nonzero, hd = the
-  // balanced digits h[k][a][u] of val_k 2^(8a) mod p, 256 B per padded nonzero (zero for pads)
-  const uint32_t *gptr = nullptr, *pidx = nullptr;
-  const uint8_t *hd = nullptr;
+  // 4; gptr[j] = first group of output j, pidx = input index per padded nonzero, gval = its
+  // value (16 B, zero for pads; the kernel derives the digits of val 2^(8a) mod p itself)
+  const uint32_t *gptr = nullptr, *pidx = nullptr, *gval = nullptr;
   size_t groups = 0;
 };
 struct SdigPlan {

@@ -974,6 +974,21 @@ lcpc_status one_group(lcpc_sharded_commit *c, Xop op, Watchdog *wd = nullptr, si
   return run_group(c->comm, ops, {c->ev_done});
 }
 
+// a gather of per-rank byte counts to one rank (an all-to-all with only the root receiving)
+Xop gather_to_root(const lcpc_sharded_commit *c, const uint8_t *send, uint8_t *recv, int root,
+                   const std::vector<size_t> &bytes_of_rank) {
+  Xop op{Xop::ALL_TO_ALL};
+  op.send = send;
+  op.recv = c->me == root ? recv : nullptr;
+  op.sb.assign(c->G, 0);
+  op.rb.assign(c->G, 0);
+  op.sb[root] = bytes_of_rank[c->me];
+  if (c->me == root) op.rb = bytes_of_rank;
+  op.ready = c->ev_ready;
+  op.s = c->s;
+  return op;
+}
+
 }  // namespace
 
 // ================================================================= C ABI
@@ -1118,6 +1133,104 @@ lcpc_status lcpc_sharded_prove(lcpc_sharded_commit *c, const uint64_t *outer, si
   if ((st = stage_paths(c))) return st;
   wd.mark(2 * c->rounds + 2, 0, "the opened columns and paths");
   return host_proof(c, out);
+}
+
+// ---------------------------------------------------------------- proof-of-storage request
+// networking/server.rs:652-737 on a row-sharded file commitment: verifiable_polynomial_evaluation
+// (lcpc_online.rs:454-484, u^T Enc(M) over the ENCODED matrix) from the ranks' partial sums over
+// their rows, gathered at `root` and folded mod p, and the client's columns (open_column,
+// lcpc-2d/src/lib.rs:818-855) from the ranks' row pieces, with paths off the whole tree.
+
+lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *left, size_t n_rows,
+                                                const uint64_t *idx, size_t n_open, int root, uint64_t *eval_out,
+                                                uint64_t *cols_out, uint8_t *paths_out) {
+  prof::HostScope hs_total("host_sharded_pos_request");
+  if (!c || !left || (!idx && n_open)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (n_rows != c->n_rows) return fail(LCPC_ERR_INVALID_ARG, "left vector length != n_rows");
+  if (root < 0 || root >= c->G) return fail(LCPC_ERR_INVALID_ARG, "root rank");
+  for (size_t k = 0; k < n_open; k++)
+    if (idx[k] >= c->nc) return fail(LCPC_PROVER_COLUMN_NUMBER, "ProverError::ColumnNumber");
+  std::lock_guard<std::mutex> lk(c->comm->mu);
+  HIP_TRY(hipSetDevice(c->dev->id));
+  Watchdog wd(c->G, c->me);
+  const size_t wb = c->wb, nc = c->nc, nr = c->nr, r0 = c->part[c->me].r_lo;
+  const bool am_root = c->me == root;
+  lcpc_status st;
+  DBuf tens, part, scratch, all, sum, didx, mycols, allcols, dpaths;
+  HostBuf h_left, h_idx;
+  // this rank's partial u^T Enc(M) over its rows.  The codeword holds canonical values (ntt_rows
+  // canon_out), so the Montgomery products sum_r u_r R * m_rj R^-1 come out canonical.
+  HIP_TRY(salloc(c, part, nc * wb));
+  if (nr) {
+    if ((st = h_left.get(c->dev, nr * wb))) return st;
+    std::memcpy(h_left.p, (const uint8_t *)left + r0 * wb, nr * wb);
+    HIP_TRY(salloc(c, tens, nr * wb));
+    HIP_TRY(salloc(c, scratch, collapse_scratch_bytes(c->fid, nr, nc, 1)));
+    HIP_TRY(h2d(tens.p, h_left.p, nr * wb, c->s));
+    HIP_TRY(collapse_rows(c->fid, c->comm_rows.as<uint32_t>(), nr, nc, tens.as<uint32_t>(), 1, part.as<uint32_t>(),
+                          scratch.p, c->s));
+  } else {
+    HIP_TRY(hipMemsetAsync(part.p, 0, nc * wb, c->s));
+  }
+  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  if (am_root) HIP_TRY(salloc(c, all, (size_t)c->G * nc * wb));
+  if ((st = one_group(c, gather_to_root(c, part.as<uint8_t>(), all.as<uint8_t>(), root,
+                                        std::vector<size_t>(c->G, nc * wb)),
+                      &wd, 0, "partial u^T Enc(M) gather")))
+    return st;
+  // my rows of the requested columns
+  if (n_open) {
+    if ((st = h_idx.get(c->dev, n_open * 8))) return st;
+    std::memcpy(h_idx.p, idx, n_open * 8);
+    HIP_TRY(salloc(c, didx, n_open * 8));
+    HIP_TRY(h2d(didx.p, h_idx.p, n_open * 8, c->s));
+  }
+  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(salloc(c, mycols, std::max<size_t>(n_open * nr, 1) * wb));
+  if (n_open && nr)
+    HIP_TRY(gather_columns(c->fid, c->comm_rows.as<uint32_t>(), nr, nc, didx.as<uint64_t>(), n_open,
+                           mycols.as<uint32_t>(), c->s, false, true));
+  if (am_root) {
+    // fold the partials; canonical sums -> Montgomery words (the ABI's element layout)
+    HIP_TRY(salloc(c, sum, nc * wb));
+    HIP_TRY(collapse_fold_rows(c->fid, all.as<uint32_t>(), c->G, nc, sum.as<uint32_t>(), c->s));
+    HIP_TRY(convert(c->fid, sum.as<uint32_t>(), sum.as<uint32_t>(), nc, true, c->s));
+    HIP_TRY(salloc(c, allcols, std::max<size_t>(n_open * c->n_rows, 1) * wb));
+  }
+  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  std::vector<size_t> col_bytes(c->G);
+  for (int k = 0; k < c->G; k++) col_bytes[k] = n_open * (c->part[k].r_hi - c->part[k].r_lo) * wb;
+  if ((st = one_group(c, gather_to_root(c, mycols.as<uint8_t>(), allcols.as<uint8_t>(), root, col_bytes), &wd, 1,
+                      "requested-column gather")))
+    return st;
+  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  if (am_root) {
+    const size_t pl = log2_np2(nc);
+    HIP_TRY(salloc(c, dpaths, std::max<size_t>(n_open * pl, 1) * 32));
+    if (n_open && pl)
+      HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), 2 * nc - 1, didx.as<uint64_t>(), n_open, pl,
+                           dpaths.as<uint8_t>(), c->s));
+    if (eval_out) HIP_TRY(d2h_staged(eval_out, sum.p, nc * wb, c->s));
+    // columns arrive as [rank][col][rank's rows]: reassemble [col][all rows] on the host
+    std::vector<uint8_t> h_cols(std::max<size_t>(n_open * c->n_rows, 1) * wb);
+    if (n_open) HIP_TRY(d2h_staged(h_cols.data(), allcols.p, n_open * c->n_rows * wb, c->s));
+    if (paths_out && n_open && pl) HIP_TRY(d2h_staged(paths_out, dpaths.p, n_open * pl * 32, c->s));
+    wd.mark(2, 0, "the request's results");
+    HIP_TRY(hipStreamSynchronize(c->s));
+    if (cols_out) {
+      const uint8_t *src = h_cols.data();
+      uint8_t *dst = (uint8_t *)cols_out;
+      for (int k = 0; k < c->G; k++) {
+        const size_t kr0 = c->part[k].r_lo, knr = c->part[k].r_hi - kr0;
+        for (size_t j = 0; j < n_open; j++) std::memcpy(dst + (j * c->n_rows + kr0) * wb, src + j * knr * wb, knr * wb);
+        src += n_open * knr * wb;
+      }
+    }
+  } else {
+    wd.mark(2, 0, "the request's exchanges");
+    HIP_TRY(hipStreamSynchronize(c->s));
+  }
+  return LCPC_OK;
 }
 
 // ---------------------------------------------------------------- the pipelined driver

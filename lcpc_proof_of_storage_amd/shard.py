@@ -682,6 +682,47 @@ class ShardedCommit:
         return LcEvalProof(h.value) if h.value else None
 
 
+    def pos_request(self, left, columns, root: int = 0):
+        """Collective proof-of-storage request (lcpc_sharded_pos_request; networking/server.rs:652-737):
+        on rank `root` returns (u^T Enc(M) as an (n_cols, limbs) array, [LcColumn] of the requested
+        columns with their Merkle paths); None elsewhere."""
+        from .lcpc2d import LcColumn, _elems, limbs, log2
+        nl = limbs(self.enc.field)
+        u = np.ascontiguousarray(_elems(left, self.enc.field))
+        idx = np.ascontiguousarray(list(columns), dtype=np.uint64)
+        n = len(idx)
+        nc = self.enc.n_cols
+        pl = log2(nc)
+        mine = self.comm.rank == root
+        ev = np.zeros((nc, nl), np.uint64) if mine else None
+        cols = np.zeros((max(n, 1), self.n_rows, nl), np.uint64) if mine else None
+        paths = (C.c_uint8 * max(32 * pl * n, 1))() if mine else None
+        p64 = C.POINTER(C.c_uint64)
+        _check(_lib().lcpc_sharded_pos_request(
+            self._h, u.ctypes.data_as(p64), u.shape[0], idx.ctypes.data_as(p64) if n else None, n, root,
+            ev.ctypes.data_as(p64) if mine else None, cols.ctypes.data_as(p64) if mine else None,
+            C.cast(paths, C.POINTER(C.c_uint8)) if mine else None))
+        if not mine:
+            return None
+        pb = bytes(paths)
+        return ev, [LcColumn(cols[k].copy(), [pb[32 * (k * pl + i):32 * (k * pl + i + 1)] for i in range(pl)])
+                    for k in range(n)]
+
+
+def pos_pack_shard(d_bytes: int, n_bytes: int, n_per_row: int, row0: int, n_shard_rows: int, d_out: int,
+                   stream=None):
+    """This rank's rows of a proof-of-storage file on device: the file's bytes (device, d_bytes,
+    n_bytes in all) of rows [row0, row0 + n_shard_rows) packed 7 per WriteableFt63 element
+    (lcpc_pos_bytes_to_field_device; data_field.rs:38-46) into d_out, which must hold
+    n_shard_rows * n_per_row zeroed elements (the last row's tail stays zero, as the file's
+    zero padding does).  Row r starts at byte 7 n_per_row r, so each rank packs on its own."""
+    lo = min(n_bytes, 7 * n_per_row * row0)
+    hi = min(n_bytes, 7 * n_per_row * (row0 + n_shard_rows))
+    if hi > lo:
+        _check(_lib().lcpc_pos_bytes_to_field_device(C.c_void_p(d_bytes + lo), hi - lo, C.c_void_p(d_out),
+                                                     C.c_void_p(stream) if stream else None))
+
+
 def sharded_commit_prove_many(enc, comm: NativeComm, d_rows: Sequence[int], n_rows: int, outer, make_transcript,
                               lag: int = 0, keep_proofs: bool = True):
     """lcpc_sharded_commit_prove_many: pipelined commit + prove of len(d_rows) polynomials.
