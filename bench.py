@@ -8,8 +8,8 @@ LcCommit::prove (2 degree tests + evaluation row combination, Merlin transcript 
 row-combination coefficient, 309 column openings with Merkle paths): lcpc-2d/src/lib.rs:651-700
 and :1034-1123, dims 512 x 32768 -> 65536 (rho = 1/2, lcpc-ligero-pc/src/lib.rs:70-112).
 
-Engines (--mode):
-  sharded (default, cfg3): every step is ONE commitment whose rows are split over the N ranks
+Engines (--mode; the default, auto, is sharded for --gpus > 1 and replicas on one GPU):
+  sharded (cfg3): every step is ONE commitment whose rows are split over the N ranks
     (one process per GPU, RCCL over xGMI through liblcpc_mi's own communicator), run by the
     library's pipelined driver lcpc_sharded_commit_prove_many (csrc/shard_native.cpp): the
     exchanges of the steps in flight go out in one fixed order per tick, the transcript of step
@@ -56,6 +56,9 @@ def parse():
                          "commitments per rank on host threads; auto (default): sharded for --gpus > 1, "
                          "replicas on one GPU, where there is nothing to split and independent "
                          "commitments in flight are the faster single-GPU engine")
+    ap.add_argument("--sharded-n1", type=int, default=1,
+                    help="N = 1 replicas lines (ligero): also time the row-sharded engine on the one GPU "
+                         "(the N = 1 base of the sharded N > 1 lines) and report it as \"sharded_n1\"")
     ap.add_argument("--lag", type=int, default=0,
                     help="sharded driver: ticks between a row-combination gather and the next challenge "
                          "broadcast (0: the library's choice)")
@@ -631,6 +634,9 @@ def ligero_sharded(args, L, torch, dist, rank, world, device, backend, share):
     def serial_commit():
         return shard.ShardedCommit(enc, comm, d_mine.data_ptr(), n_rows)
 
+    def reserve(k):
+        shard.sharded_reserve(enc, comm, n_rows, k, args.lag)
+
     def serial_prove(sc):
         root = sc.get_root()
         return sc.prove(outer, make_tr(0, root) if rank == 0 else None, root=0)
@@ -638,7 +644,7 @@ def ligero_sharded(args, L, torch, dist, rank, world, device, backend, share):
     B = 8 * nl
     return dict(
         fid=fid, enc=enc, n=n, n_rows=n_rows, n_per_row=n_per_row, n_cols=n_cols, nco=nco, ndt=ndt, nr=nr,
-        coeffs=coeffs, outer=outer, inner=inner, run=run, serial_commit=serial_commit,
+        coeffs=coeffs, outer=outer, inner=inner, run=run, serial_commit=serial_commit, reserve=reserve,
         serial_prove=serial_prove, make_tr=make_tr,
         comm_kind=comm_kind, d_mine=d_mine, d_out=d_out, B=B)
 
@@ -673,18 +679,45 @@ def main():
     import lcpc_proof_of_storage_amd as L
 
     L.set_device(device_idx)
+    sharded_n1 = None
     if args.mode == "sharded" and args.code == "pos":
         out = run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share)
     elif args.mode == "sharded":
         out = run_sharded(args, L, torch, dist, rank, world, device, backend, share)
     else:
         out = run_replicas(args, L, torch, dist, rank, world, device_idx, backend)
+        if world == 1 and args.code == "ligero" and args.sharded_n1:
+            # the row-sharded engine on this one GPU, like for like with the N > 1 lines
+            # (--mode auto runs it there): same steps and warm-up, after the replicas' figures
+            sharded_n1 = sharded_n1_figure(args, L, torch, device)
+    if sharded_n1 is not None:
+        out["sharded_n1"] = sharded_n1
     if rank == 0:
         out["world_formed"] = formed
         print(json.dumps(out))
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def sharded_n1_figure(args, L, torch, device):
+    """The sharded engine's one-GPU throughput on the same workload (lcpc_sharded_commit_prove_many
+    with a one-rank comm: the N = 1 base of the N > 1 sharded lines): pools reserved, exactly
+    --warmup untimed steps, then --steps timed, device-synchronised on both sides."""
+    S = ligero_sharded(args, L, torch, None, 0, 1, device, "nccl", False)
+    S["reserve"](max(args.steps, args.warmup))
+    roots, _ = S["run"](max(1, args.warmup))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    troots, _ = S["run"](args.steps)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    assert all(r == roots[0] for r in troots), "sharded engine: roots differ across steps"
+    return {"value": S["n"] * args.steps / elapsed, "unit": "field-elements/s", "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "scaling": "strong",
+            "engine": "lcpc_sharded_commit_prove_many, one rank (no exchanges): the N = 1 point of the "
+                      "--mode sharded (--gpus N > 1) curve",
+            "lag": args.lag or None, "root": roots[0].hex()}
 
 
 def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
@@ -696,7 +729,9 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
     def barrier():
         sync_barrier(dist, torch.cuda.synchronize)
 
-    # warm-up (pools, streams, RCCL connections); polynomial 0's proof is kept on rank 0
+    # the pools the timed run's pipeline depth needs (buffers, page-locked staging, streams: not
+    # steps), then the warm-up (RCCL connections); polynomial 0's proof is kept on rank 0
+    S["reserve"](max(args.steps, args.warmup))
     roots, proofs = S["run"](max(1, args.warmup), keep=True)
     warm_proof = proofs[0]
     assert all(r == roots[0] for r in roots), "nondeterministic root across steps"

@@ -508,6 +508,13 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
                                            void *user, size_t lag, lcpc_proof **proofs,
                                            uint8_t *roots);
 
+/* Pre-populates this rank's device pool, page-locked staging and stream pool with what
+ * lcpc_sharded_commit_prove_many(n_polys, lag) keeps in flight at once (every polynomial in
+ * the pipeline holds its own rows, codeword, exchange and proof buffers), so the first call
+ * at a new depth does not pay for hipMalloc / hipHostMalloc / stream creation inside it.  The
+ * counterpart of lcpc_reserve for the sharded driver; no exchange. */
+lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_comm *comm,
+                                 size_t n_polys, size_t lag);
 /* Host-only (no device): the point-to-point transfers rank `rank` issues, in order, in every
  * exchange group of lcpc_sharded_commit_prove_many(n_polys, lag) -- the exact list run_group
  * hands RCCL as ncclSend / ncclRecv between ncclGroupStart / ncclGroupEnd.  Lets a single host

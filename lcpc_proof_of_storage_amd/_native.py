@@ -181,6 +181,7 @@ SIGNATURES = {
     "lcpc_sharded_prove": (i32, [vp, u64p, sz, vp, vp, i32, C.POINTER(vp)]),
     "lcpc_sharded_commit_prove_many": (i32, [vp, C.POINTER(vp), sz, sz, u64p, vp, MAKE_TRANSCRIPT_FN, vp, sz,
                                              C.POINTER(vp), u8p]),
+    "lcpc_sharded_reserve": (i32, [vp, sz, vp, sz, sz]),
     "lcpc_sharded_pos_request": (i32, [vp, u64p, sz, u64p, sz, i32, u64p, u64p, u8p]),
     "lcpc_sharded_p2p_schedule": (i32, [i32, sz, sz, sz, sz, sz, i32, i32, sz, sz, C.POINTER(P2pRecord), sz,
                                         szp]),

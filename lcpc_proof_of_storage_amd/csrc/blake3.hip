@@ -106,6 +106,15 @@ __device__ __forceinline__ void store8(uint32_t *p, const uint32_t v[8]) {
   reinterpret_cast<uint4 *>(p)[1] = make_uint4(v[4], v[5], v[6], v[7]);
 }
 
+// Slot of the chaining value of (col, chunk) in a chunk range [chunk0, chunk_end): [chunk][col],
+// or with blk > 0 the row-shard exchange's layout [col / blk][chunk][col % blk] (each destination
+// rank's column block contiguous, ready to send).
+__device__ __forceinline__ size_t cv_slot(size_t col, int chunk, int chunk0, int chunk_end, size_t n_cols,
+                                          size_t blk) {
+  const size_t c = (size_t)(chunk - chunk0);
+  return blk ? ((col / blk) * (size_t)(chunk_end - chunk0) + c) * blk + col % blk : c * n_cols + col;
+}
+
 // One thread per (column, chunk).  Message word w of a column: w < 8 is the zero prefix,
 // else word (w-8) % N of element row (w-8) / N.  N in {2, 4, 8} divides both 8 and 16, so
 // every 16-word block holds whole elements.  The launch covers chunks [chunk0, chunk_end) of
@@ -117,11 +126,13 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
                                                      size_t row_stride, size_t col_stride,
                                                      uint32_t *__restrict__ cvs,
                                                      uint8_t *__restrict__ leaves, int n_chunks,
-                                                     size_t row0, int chunk0, int chunk_end) {
+                                                     size_t row0, int chunk0, int chunk_end, size_t blk) {
   constexpr int N = F::N;
   static_assert(16 % N == 0 && 8 % N == 0, "element must tile a BLAKE3 block");
-  const size_t col = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int chunk = chunk0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  // a block = 4 waves on 256 adjacent columns of one chunk (every wave of a block does the same
+  // amount of work; a chunk per wave left the waves of chunks >= n_chunks idle)
+  const size_t col = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int chunk = chunk0 + blockIdx.y;
   if (col >= n_cols || chunk >= chunk_end) return;
   const size_t total_words = 8 + n_rows * N;
   const size_t w0 = (size_t)chunk * 256;
@@ -178,7 +189,7 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
         to_msg(eb, msg);
         compress(cv, msg, (uint64_t)chunk, 64u, b + 1 == 15 ? CHUNK_END : 0u);
       }
-      store8(cvs + ((size_t)(chunk - chunk0) * n_cols + col) * 8, cv);
+      store8(cvs + cv_slot(col, chunk, chunk0, chunk_end, n_cols, blk) * 8, cv);
       return;
     }
   }
@@ -216,7 +227,7 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
   if (n_chunks == 1 && leaves) {
     store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
   } else {
-    store8(cvs + ((size_t)(chunk - chunk0) * n_cols + col) * 8, cv);
+    store8(cvs + cv_slot(col, chunk, chunk0, chunk_end, n_cols, blk) * 8, cv);
   }
 }
 
@@ -225,7 +236,7 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
 // a wave touches 64 columns n_rows * B bytes apart; here the wave loads each 64-byte block of its
 // 64 columns cooperatively instead -- 4 adjacent lanes read one column's block, so a load
 // instruction covers 16 columns x 64 contiguous bytes -- and hands the blocks over through LDS
-// (double buffered, rows padded to 80 B so the per-column reads are bank-conflict free).  Needs
+// (rows padded to 80 B so the per-column reads are bank-conflict free).  Needs
 // n_rows * N % 4 == 0 (16-B aligned columns); the message word w of a column is memory word w - 8
 // of the column (w >= 8), and a 4-word unit lies wholly inside or outside the message.
 template <class F, bool CANON>
@@ -235,11 +246,11 @@ __global__ __launch_bounds__(256) void k_leaf_chunks_cm(const uint32_t *__restri
   constexpr int N = F::N;
   static_assert(16 % N == 0 && 8 % N == 0, "element must tile a BLAKE3 block");
   constexpr int EPB = 16 / N;
-  __shared__ uint4 stage[4][2][64][5];
+  __shared__ uint4 stage[4][64][5];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t col0 = (size_t)blockIdx.x * 64, col = col0 + lane;
-  const int chunk = blockIdx.y * 4 + wave;
-  if (chunk >= n_chunks) return;  // whole waves
+  const size_t col0 = ((size_t)blockIdx.x * 4 + wave) * 64, col = col0 + lane;
+  const int chunk = blockIdx.y;
+  if (col0 >= n_cols) return;  // whole waves
   const size_t msg_words = 8 + n_rows * N;  // the column's message, in words
   const size_t w0 = (size_t)chunk * 256;
   const size_t cw = msg_words - w0 < 256 ? msg_words - w0 : 256;
@@ -256,30 +267,34 @@ __global__ __launch_bounds__(256) void k_leaf_chunks_cm(const uint32_t *__restri
                               : make_uint4(0, 0, 0, 0);
     }
   };
-  auto lput = [&](int buf, const uint4 r[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) stage[wave][buf][csub + 16 * i][unit] = r[i];
+  auto wave_sync = [] {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto lput = [&](const uint4 r[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) stage[wave][csub + 16 * i][unit] = r[i];
+    wave_sync();
   };
   uint32_t cv[8];
   iv(cv);
   uint4 r[4];
   gload(0, r);
-  lput(0, r);
+  lput(r);
   for (int b = 0; b < nb; b++) {
     const bool more = b + 1 < nb;
     if (more) gload(b + 1, r);
     uint32_t msg[16];
     {
-      const uint4 *row = stage[wave][b & 1][lane];
+      const uint4 *row = stage[wave][lane];
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const uint4 q = row[k];
         msg[4 * k] = q.x; msg[4 * k + 1] = q.y; msg[4 * k + 2] = q.z; msg[4 * k + 3] = q.w;
       }
     }
+    wave_sync();  // every lane has read block b before block b + 1 overwrites the stage
     // element words -> repr words (Montgomery -> canonical unless CANON); the zero prefix and
     // words past the message stay zero either way (from_mont(0) = 0, and they load as zero)
 #pragma unroll
@@ -300,7 +315,7 @@ __global__ __launch_bounds__(256) void k_leaf_chunks_cm(const uint32_t *__restri
     uint32_t flags = b == 0 ? CHUNK_START : 0u;
     if (b == nb - 1) flags |= CHUNK_END | (n_chunks == 1 ? ROOT : 0u);
     compress(cv, msg, (uint64_t)chunk, blen, flags);
-    if (more) lput((b + 1) & 1, r);
+    if (more) lput(r);
   }
   if (col >= n_cols) return;
   if (n_chunks == 1 && leaves) {
@@ -320,11 +335,12 @@ template <class F, bool CANON>
 __global__ __launch_bounds__(256) void k_leaf_chunks_words(const uint32_t *__restrict__ m, size_t n_rows,
                                                            size_t n_cols, size_t row_stride, size_t col_stride,
                                                            uint32_t *__restrict__ cvs, uint8_t *__restrict__ leaves,
-                                                           int n_chunks, size_t row0, int chunk0, int chunk_end) {
+                                                           int n_chunks, size_t row0, int chunk0, int chunk_end,
+                                                           size_t blk) {
   constexpr int N = F::N;
   static_assert(4 * N >= N - 1 + 16, "four elements cover a block");
-  const size_t col = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int chunk = chunk0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const size_t col = (size_t)blockIdx.x * 256 + threadIdx.x;  // 4 waves, 256 columns, one chunk
+  const int chunk = chunk0 + blockIdx.y;
   if (col >= n_cols || chunk >= chunk_end) return;
   const size_t total_words = 8 + n_rows * N;
   const size_t w0 = (size_t)chunk * 256;
@@ -376,7 +392,7 @@ __global__ __launch_bounds__(256) void k_leaf_chunks_words(const uint32_t *__res
   if (n_chunks == 1 && leaves) {
     store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
   } else {
-    store8(cvs + ((size_t)(chunk - chunk0) * n_cols + col) * 8, cv);
+    store8(cvs + cv_slot(col, chunk, chunk0, chunk_end, n_cols, blk) * 8, cv);
   }
 }
 
@@ -515,7 +531,7 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
   if (n_cols == 0) return hipSuccess;
   const size_t words = 8 + n_rows * (size_t)field_words(fid);
   const int n_chunks = (int)((words + 255) / 256);
-  dim3 grid((unsigned)((n_cols + 63) / 64), (unsigned)((n_chunks + 3) / 4));
+  dim3 grid((unsigned)((n_cols + 255) / 256), (unsigned)n_chunks);
   hipError_t e = dispatch_field(fid, [&]<class F>() {
     if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
       prof::Scope ps("leaf_chunks", s);
@@ -530,19 +546,19 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
       }
       if (canon)
         hipLaunchKernelGGL((k_leaf_chunks<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
-                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
+                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks, (size_t)0);
       else
         hipLaunchKernelGGL((k_leaf_chunks<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
-                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
+                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks, (size_t)0);
       return hipGetLastError();
     } else {
       prof::Scope ps("leaf_chunks", s);
       if (canon)
         hipLaunchKernelGGL((k_leaf_chunks_words<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
-                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
+                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks, (size_t)0);
       else
         hipLaunchKernelGGL((k_leaf_chunks_words<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, row_stride,
-                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks);
+                           col_stride, (uint32_t *)scratch, leaves, n_chunks, (size_t)0, 0, n_chunks, (size_t)0);
       return hipGetLastError();
     }
   });
@@ -559,30 +575,32 @@ size_t leaf_n_chunks(int fid, size_t n_rows) {
 
 hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows, size_t n_cols,
                           size_t stride, size_t chunk_lo, size_t chunk_hi, uint32_t *cvs,
-                          hipStream_t s, bool canon) {
+                          hipStream_t s, bool canon, size_t blk) {
   if (n_cols == 0 || chunk_hi <= chunk_lo) return hipSuccess;
   const int n_chunks = (int)leaf_n_chunks(fid, n_rows);
-  dim3 grid((unsigned)((n_cols + 63) / 64), (unsigned)((chunk_hi - chunk_lo + 3) / 4));
+  dim3 grid((unsigned)((n_cols + 255) / 256), (unsigned)(chunk_hi - chunk_lo));
   return dispatch_field(fid, [&]<class F>() {
     if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
       prof::Scope ps("leaf_chunks", s);
       if (canon)
         hipLaunchKernelGGL((k_leaf_chunks<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
                            (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
-                           (int)chunk_hi);
+                           (int)chunk_hi, blk);
       else
         hipLaunchKernelGGL((k_leaf_chunks<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
                            (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
-                           (int)chunk_hi);
+                           (int)chunk_hi, blk);
       return hipGetLastError();
     } else {
       prof::Scope ps("leaf_chunks", s);
       if (canon)
         hipLaunchKernelGGL((k_leaf_chunks_words<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
-                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi);
+                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi,
+                           blk);
       else
         hipLaunchKernelGGL((k_leaf_chunks_words<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
-                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi);
+                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi,
+                           blk);
       return hipGetLastError();
     }
   });

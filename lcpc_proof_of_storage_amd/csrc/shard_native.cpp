@@ -233,11 +233,13 @@ lcpc_status run_group(lcpc_comm *c, std::vector<Xop> &ops, const std::vector<hip
   if (G == 1) {
     // one rank: nothing crosses a process, so each exchange is its own-piece copy on the
     // polynomial's stream (no comm stream: polynomials in flight do not wait for each other)
+    // (an exchange whose receive buffer is its send buffer moves nothing)
     for (size_t i = 0; i < ops.size(); i++) {
       const Xop &op = ops[i];
-      if (op.kind == Xop::ALL_GATHER && op.bytes)
+      if (op.ready) HIP_TRY(hipStreamWaitEvent(op.s, op.ready, 0));
+      if (op.kind == Xop::ALL_GATHER && op.bytes && op.recv != op.send)
         HIP_TRY(d2d(op.recv, op.send, op.bytes, op.s));
-      if (op.kind == Xop::ALL_TO_ALL && op.rb[0])
+      if (op.kind == Xop::ALL_TO_ALL && op.rb[0] && op.recv != op.send)
         HIP_TRY(d2d(op.recv, op.send, op.rb[0], op.s));
       if (i < done.size()) HIP_TRY(hipEventRecord(done[i], op.s));
     }
@@ -352,12 +354,15 @@ struct lcpc_sharded_commit {
   int fid = 1, wb = 16, G = 1, me = 0;
   size_t n_rows = 0, np = 0, nc = 0, B = 0, n_chunks = 0, nr = 0;
   std::vector<Part> part;
-  hipStream_t s = nullptr;        // this polynomial's compute stream
+  hipStream_t s = nullptr;        // this polynomial's encode stream (shared, in order, by the
+                                  // pipelined driver's polynomials: encodes finish first come first)
+  bool own_s = true;              // s is this polynomial's own (released with it)
+  hipStream_t sp = nullptr;       // its prove stream (high priority: short latency-critical kernels)
   hipEvent_t ev_ready = nullptr;  // send data of the next exchange written
   hipEvent_t ev_done = nullptr;   // the last exchange completed (comm stream)
   hipEvent_t ev_host = nullptr;   // device -> host copies of the last stage landed
   DBuf coeffs, comm_rows, hashes;  // kept for prove
-  DBuf cv, cv_send, cv_recv, sub, subs;  // commit scratch
+  DBuf cv_send, cv_recv, sub, subs;  // commit scratch
   uint8_t root[32] = {0};
   // prove state
   int root_rank = 0;
@@ -369,7 +374,8 @@ struct lcpc_sharded_commit {
   std::vector<uint64_t> p_random, p_eval, col_idx;
   std::future<lcpc_status> next;  // root rank: the next challenge vector is in h_t / h_idx
   ~lcpc_sharded_commit() {
-    if (s) (void)hipStreamSynchronize(s);
+    if (s && own_s) (void)hipStreamSynchronize(s);
+    if (sp && sp != s) (void)hipStreamSynchronize(sp);
     if (own_tr) delete tr;
     if (ev_ready) (void)hipEventDestroy(ev_ready);
     if (ev_done) (void)hipEventDestroy(ev_done);
@@ -380,29 +386,33 @@ struct lcpc_sharded_commit {
 
 namespace {
 
-void release_stream(lcpc_sharded_commit *c) {
-  if (c->s) {
-    (void)hipStreamSynchronize(c->s);
-    c->dev->release_stream(c->s, false);
-    c->s = nullptr;
-  }
+// LCPC_SHARD_PRIO=0: the prove stages share the commit stream (A/B runs)
+bool shard_prio_streams() {
+  static const bool v = [] {
+    const char *e = getenv("LCPC_SHARD_PRIO");
+    return !(e && e[0] == '0');
+  }();
+  return v;
 }
 
 struct ShardDeleter {
   void operator()(lcpc_sharded_commit *c) const {
     if (!c) return;
-    hipStream_t s = c->s;
+    hipStream_t s = c->own_s ? c->s : nullptr, sp = c->sp != c->s ? c->sp : nullptr;
     Device *d = c->dev;
     c->s = nullptr;
+    c->sp = nullptr;
     if (s) (void)hipStreamSynchronize(s);
+    if (sp) (void)hipStreamSynchronize(sp);
     // the stream has drained: no buffer needs its own drain on release (one hipStreamSynchronize
     // per buffer cost ~0.4 ms per polynomial)
-    for (DBuf *b : {&c->coeffs, &c->comm_rows, &c->hashes, &c->cv, &c->cv_send, &c->cv_recv, &c->sub, &c->subs,
+    for (DBuf *b : {&c->coeffs, &c->comm_rows, &c->hashes, &c->cv_send, &c->cv_recv, &c->sub, &c->subs,
                     &c->bt, &c->tens, &c->part_d, &c->allpart, &c->sum, &c->canon, &c->didx, &c->mycols,
                     &c->allcols, &c->dpaths, &c->scratch})
       b->settle();
     delete c;
     if (s) d->release_stream(s, false);
+    if (sp) d->release_stream(sp, true);
   }
 };
 using ShardPtr = std::unique_ptr<lcpc_sharded_commit, ShardDeleter>;
@@ -450,15 +460,21 @@ void prove_geom(lcpc_sharded_commit *c, size_t ndt, size_t nco, int root_rank) {
   c->rounds = std::max<size_t>(ndt, 1);
 }
 
-lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, ShardPtr &out) {
+// bulk: a stream the caller owns for the encode (the pipelined driver's shared one), or null for
+// a stream of this commitment's own
+lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, ShardPtr &out,
+                       hipStream_t bulk = nullptr) {
   ShardPtr c(new lcpc_sharded_commit());
   c->e = e;
   c->comm = comm;
   c->dev = e->dev;
   shard_geom(c.get(), e->fid, e->n_per_row, e->n_cols, n_rows, comm->nranks, comm->rank);
   HIP_TRY(hipSetDevice(c->dev->id));
-  c->s = c->dev->acquire_stream(false);
+  c->own_s = bulk == nullptr;
+  c->s = bulk ? bulk : c->dev->acquire_stream(false);
   if (!c->s) return fail(LCPC_ERR_DEVICE, "no HIP stream");
+  c->sp = shard_prio_streams() ? c->dev->acquire_stream(true) : c->s;
+  if (!c->sp) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   HIP_TRY(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_host, hipEventDisableTiming));
@@ -466,14 +482,17 @@ lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, S
   return LCPC_OK;
 }
 
-// DBuf allocations drain the polynomial's stream (not the caller's lease) when released
-hipError_t salloc(lcpc_sharded_commit *c, DBuf &b, size_t bytes) {
+// DBuf allocations drain the polynomial's stream (not the caller's lease) when released: the
+// commit stream for the commit's buffers, the prove stream for the prove's
+hipError_t salloc_on(lcpc_sharded_commit *c, DBuf &b, size_t bytes, hipStream_t s) {
   hipStream_t prev = t_stream;
-  t_stream = c->s;
+  t_stream = s;
   hipError_t e = b.alloc(c->dev, bytes);
   t_stream = prev;
   return e;
 }
+hipError_t salloc(lcpc_sharded_commit *c, DBuf &b, size_t bytes) { return salloc_on(c, b, bytes, c->s); }
+hipError_t salloc_p(lcpc_sharded_commit *c, DBuf &b, size_t bytes) { return salloc_on(c, b, bytes, c->sp); }
 
 // ---- commit
 // encode this rank's rows (the first NTT pass writes the commitment's own coefficient copy),
@@ -484,24 +503,15 @@ lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
   HIP_TRY(salloc(c, c->coeffs, c->nr * c->np * wb + 16));
   HIP_TRY(salloc(c, c->comm_rows, c->nr * c->nc * wb + 16));
   HIP_TRY(salloc(c, c->cv_send, nch * c->nc * 32 + 16));
-  HIP_TRY(salloc(c, c->cv_recv, c->n_chunks * c->B * 32 + 16));
+  if (c->G > 1) HIP_TRY(salloc(c, c->cv_recv, c->n_chunks * c->B * 32 + 16));  // (one rank: cv_send itself)
   if (c->nr) {
     if (!d_rows) return fail(LCPC_ERR_INVALID_ARG, "null rows");
     HIP_TRY(ntt_rows(c->e->plan, (const uint32_t *)d_rows, c->np, c->np, c->comm_rows.as<uint32_t>(), c->nc, c->nr,
                      c->s, c->coeffs.as<uint32_t>(), c->np, true));
   }
-  if (nch) {
-    // (a member, released once the commit is complete: a local would drain the stream here)
-    HIP_TRY(salloc(c, c->cv, nch * c->nc * 32));
-    DBuf &cv = c->cv;
+  if (nch)  // chaining values straight into the exchange layout [dest rank][chunk][block col]
     HIP_TRY(leaf_chunk_cvs(c->fid, c->comm_rows.as<uint32_t>(), pm.r_lo, c->n_rows, c->nc, c->nc, pm.c_lo, pm.c_hi,
-                           cv.as<uint32_t>(), c->s, true));
-    // [chunk][G][B] -> [G][chunk][B]
-    const size_t row = c->B * 32;
-    for (int k = 0; k < c->G; k++)
-      HIP_TRY(hipMemcpy2DAsync(c->cv_send.as<uint8_t>() + (size_t)k * nch * row, row, cv.as<uint8_t>() + k * row,
-                               c->nc * 32, row, nch, hipMemcpyDeviceToDevice, c->s));
-  }
+                           c->cv_send.as<uint32_t>(), c->s, true, c->B));
   HIP_TRY(hipEventRecord(c->ev_ready, c->s));
   return LCPC_OK;
 }
@@ -510,48 +520,50 @@ Xop op_cv_exchange(lcpc_sharded_commit *c) {
   Xop op{Xop::ALL_TO_ALL};
   const size_t nch_me = c->part[c->me].c_hi - c->part[c->me].c_lo;
   op.send = c->cv_send.as<uint8_t>();
-  op.recv = c->cv_recv.as<uint8_t>();
+  op.recv = c->G > 1 ? c->cv_recv.as<uint8_t>() : c->cv_send.as<uint8_t>();
   op.sb.assign(c->G, nch_me * c->B * 32);
   op.rb.resize(c->G);
   for (int k = 0; k < c->G; k++) op.rb[k] = (c->part[k].c_hi - c->part[k].c_lo) * c->B * 32;
   op.ready = c->ev_ready;
-  op.s = c->s;
+  op.s = c->sp;  // (one rank: where the post stage waits for the encode)
   return op;
 }
 
-// leaves of my column block from all chunks' chaining values, and the block's subtree
+// leaves of my column block from all chunks' chaining values, and the block's subtree (the
+// commit's short latency-critical kernels go on the prove stream, ahead of bulk encodes)
 lcpc_status stage_post_cv(lcpc_sharded_commit *c) {
-  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
-  HIP_TRY(salloc(c, c->sub, (2 * c->B - 1) * 32));
-  HIP_TRY(leaves_from_cvs(c->cv_recv.as<uint32_t>(), c->B, (int)c->n_chunks, c->sub.as<uint8_t>(), c->s));
-  if (c->B > 1) HIP_TRY(merkle_tree(c->sub.as<uint8_t>(), c->B, c->s));
-  HIP_TRY(salloc(c, c->subs, (size_t)c->G * (2 * c->B - 1) * 32));
-  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
+  HIP_TRY(salloc_p(c, c->sub, (2 * c->B - 1) * 32));
+  uint32_t *cvs = (c->G > 1 ? c->cv_recv : c->cv_send).as<uint32_t>();
+  HIP_TRY(leaves_from_cvs(cvs, c->B, (int)c->n_chunks, c->sub.as<uint8_t>(), c->sp));
+  if (c->B > 1) HIP_TRY(merkle_tree(c->sub.as<uint8_t>(), c->B, c->sp));
+  if (c->G > 1) HIP_TRY(salloc_p(c, c->subs, (size_t)c->G * (2 * c->B - 1) * 32));  // (one rank: sub itself)
+  HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
   return LCPC_OK;
 }
 
 Xop op_subtree_exchange(lcpc_sharded_commit *c) {
   Xop op{Xop::ALL_GATHER};
   op.send = c->sub.as<uint8_t>();
-  op.recv = c->subs.as<uint8_t>();
+  op.recv = (c->G > 1 ? c->subs : c->sub).as<uint8_t>();
   op.bytes = (2 * c->B - 1) * 32;
   op.ready = c->ev_ready;
-  op.s = c->s;
+  op.s = c->sp;
   return op;
 }
 
 // every rank: the whole tree [leaves | level 1 | ... | root] from the G subtrees + top levels
 lcpc_status stage_post_subtrees(lcpc_sharded_commit *c) {
-  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
   const size_t nc = c->nc, B = c->B, G = c->G;
-  HIP_TRY(salloc(c, c->hashes, (2 * nc - 1) * 32));
+  HIP_TRY(salloc_p(c, c->hashes, (2 * nc - 1) * 32));
   uint8_t *h = c->hashes.as<uint8_t>();
-  HIP_TRY(assemble_subtrees(c->subs.as<uint8_t>(), B, G, h, c->s));  // one launch for every level
-  if (G > 1) HIP_TRY(merkle_tree_io(h + (2 * nc - 2 * G) * 32, G, h + (2 * nc - G) * 32, c->s));
+  HIP_TRY(assemble_subtrees((G > 1 ? c->subs : c->sub).as<uint8_t>(), B, G, h, c->sp));  // one launch, every level
+  if (G > 1) HIP_TRY(merkle_tree_io(h + (2 * nc - 2 * G) * 32, G, h + (2 * nc - G) * 32, c->sp));
   lcpc_status st = c->h_root.get(c->dev, 32);
   if (st) return st;
-  HIP_TRY(d2h(c->h_root.p, h + (2 * nc - 2) * 32, 32, c->s));
-  HIP_TRY(hipEventRecord(c->ev_host, c->s));
+  HIP_TRY(d2h(c->h_root.p, h + (2 * nc - 2) * 32, 32, c->sp));
+  HIP_TRY(hipEventRecord(c->ev_host, c->sp));
   return LCPC_OK;
 }
 
@@ -560,8 +572,7 @@ lcpc_status finish_commit(lcpc_sharded_commit *c) {
   HIP_TRY(hipEventSynchronize(c->ev_host));
   std::memcpy(c->root, c->h_root.p, 32);
   // every use of the commit scratch precedes ev_host on the stream: no drain on release
-  for (DBuf *b : {&c->cv, &c->cv_send, &c->cv_recv, &c->sub, &c->subs}) b->settle();
-  c->cv.reset();
+  for (DBuf *b : {&c->cv_send, &c->cv_recv, &c->sub, &c->subs}) b->settle();
   c->cv_send.reset();
   c->cv_recv.reset();
   c->sub.reset();
@@ -576,27 +587,27 @@ lcpc_status prove_alloc(lcpc_sharded_commit *c, const uint64_t *outer, int root_
   prove_geom(c, pe->n_degree_tests, pe->n_col_opens, root_rank);
   const size_t wb = c->wb, np = c->np;
   lcpc_status st;
-  HIP_TRY(salloc(c, c->bt, c->n_rows * wb));
-  HIP_TRY(salloc(c, c->tens, 2 * std::max<size_t>(c->nr, 1) * wb));
-  HIP_TRY(salloc(c, c->part_d, 2 * np * wb));
-  HIP_TRY(salloc(c, c->scratch, collapse_scratch_bytes(c->fid, std::max<size_t>(c->nr, 1), np, 2)));
-  HIP_TRY(salloc(c, c->didx, std::max<size_t>(c->nco, 1) * 8));
-  HIP_TRY(salloc(c, c->mycols, std::max<size_t>(c->nco * c->nr, 1) * wb));
+  HIP_TRY(salloc_p(c, c->bt, c->n_rows * wb));
+  HIP_TRY(salloc_p(c, c->tens, 2 * std::max<size_t>(c->nr, 1) * wb));
+  HIP_TRY(salloc_p(c, c->part_d, 2 * np * wb));
+  HIP_TRY(salloc_p(c, c->scratch, collapse_scratch_bytes(c->fid, std::max<size_t>(c->nr, 1), np, 2)));
+  HIP_TRY(salloc_p(c, c->didx, std::max<size_t>(c->nco, 1) * 8));
+  HIP_TRY(salloc_p(c, c->mycols, std::max<size_t>(c->nco * c->nr, 1) * wb));
   // the outer tensor's slice (host -> device once per proof)
   if ((st = c->h_t.get(c->dev, c->n_rows * wb))) return st;
   if ((st = c->h_idx.get(c->dev, std::max<size_t>(c->nco, 1) * 8))) return st;
   if (c->nr) {  // (h_outer lives until the proof is released, so the copy needs no drain here)
     if ((st = c->h_outer.get(c->dev, c->nr * wb))) return st;
     std::memcpy(c->h_outer.p, (const uint8_t *)outer + c->part[c->me].r_lo * wb, c->nr * wb);
-    HIP_TRY(h2d(c->tens.as<uint8_t>() + c->nr * wb, c->h_outer.p, c->nr * wb, c->s));
+    HIP_TRY(h2d(c->tens.as<uint8_t>() + c->nr * wb, c->h_outer.p, c->nr * wb, c->sp));
   }
   if (c->me == root_rank) {
-    HIP_TRY(salloc(c, c->allpart, (size_t)c->G * 2 * np * wb));
-    HIP_TRY(salloc(c, c->sum, 2 * np * wb));
-    HIP_TRY(salloc(c, c->canon, 2 * np * wb));
+    HIP_TRY(salloc_p(c, c->allpart, (size_t)c->G * 2 * np * wb));
+    HIP_TRY(salloc_p(c, c->sum, 2 * np * wb));
+    HIP_TRY(salloc_p(c, c->canon, 2 * np * wb));
     size_t all_rows = c->n_rows;
-    HIP_TRY(salloc(c, c->allcols, std::max<size_t>(c->nco * all_rows, 1) * wb));
-    HIP_TRY(salloc(c, c->dpaths, std::max<size_t>(c->nco * log2_np2(c->nc), 1) * 32));
+    HIP_TRY(salloc_p(c, c->allcols, std::max<size_t>(c->nco * all_rows, 1) * wb));
+    HIP_TRY(salloc_p(c, c->dpaths, std::max<size_t>(c->nco * log2_np2(c->nc), 1) * 32));
     if ((st = c->h_sum.get(c->dev, 2 * np * wb))) return st;
     if ((st = c->h_repr.get(c->dev, 2 * np * wb))) return st;
     if ((st = c->h_repr_eval.get(c->dev, np * wb))) return st;
@@ -634,12 +645,12 @@ Xop op_tensor_bcast(lcpc_sharded_commit *c, size_t r) {
   op.recv = c->bt.as<uint8_t>();
   op.bytes = (r < c->ndt) ? c->n_rows * c->wb : 0;
   op.root = c->root_rank;
-  op.s = c->s;
+  op.s = c->sp;
   return op;
 }
 
 // the root's host -> device challenge copies go on the stream its exchanges run on
-hipStream_t upload_stream(const lcpc_sharded_commit *c) { return c->G == 1 ? c->s : c->comm->cs; }
+hipStream_t upload_stream(const lcpc_sharded_commit *c) { return c->G == 1 ? c->sp : c->comm->cs; }
 
 // root: the challenge vector onto the comm stream before the exchange group is issued
 lcpc_status stage_tensor_upload(lcpc_sharded_commit *c, size_t r) {
@@ -650,23 +661,23 @@ lcpc_status stage_tensor_upload(lcpc_sharded_commit *c, size_t r) {
 
 // partial row combinations over my rows: [t_r slice | outer slice] (round 0) or t_r slice
 lcpc_status stage_collapse(lcpc_sharded_commit *c, size_t r) {
-  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
   const size_t wb = c->wb, np = c->np, nr = c->nr;
   const int nt = round_tensors(c, r);
   const bool eval_only = c->ndt == 0;  // round 0 = the evaluation tensor alone
   if (nr == 0) {
-    HIP_TRY(hipMemsetAsync(c->part_d.p, 0, nt * np * wb, c->s));
+    HIP_TRY(hipMemsetAsync(c->part_d.p, 0, nt * np * wb, c->sp));
   } else {
     const uint32_t *tens = c->tens.as<uint32_t>();
     if (!eval_only) {
-      HIP_TRY(d2d(c->tens.p, c->bt.as<uint8_t>() + c->part[c->me].r_lo * wb, nr * wb, c->s));
+      HIP_TRY(d2d(c->tens.p, c->bt.as<uint8_t>() + c->part[c->me].r_lo * wb, nr * wb, c->sp));
     } else {
       tens = (const uint32_t *)(c->tens.as<uint8_t>() + nr * wb);
     }
     HIP_TRY(collapse_rows(c->fid, c->coeffs.as<uint32_t>(), nr, np, tens, nt, c->part_d.as<uint32_t>(), c->scratch.p,
-                          c->s));
+                          c->sp));
   }
-  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
   return LCPC_OK;
 }
 
@@ -680,7 +691,7 @@ Xop op_partial_gather(lcpc_sharded_commit *c, size_t r) {
   op.sb[c->root_rank] = bytes;
   if (c->me == c->root_rank) op.rb.assign(c->G, bytes);
   op.ready = c->ev_ready;
-  op.s = c->s;
+  op.s = c->sp;
   return op;
 }
 
@@ -688,14 +699,14 @@ Xop op_partial_gather(lcpc_sharded_commit *c, size_t r) {
 // transcript) to the host
 lcpc_status stage_fold(lcpc_sharded_commit *c, size_t r) {
   if (c->me != c->root_rank) return LCPC_OK;
-  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
   const size_t wb = c->wb, np = c->np;
   const size_t len = (size_t)round_tensors(c, r) * np;
-  HIP_TRY(collapse_fold_rows(c->fid, c->allpart.as<uint32_t>(), c->G, len, c->sum.as<uint32_t>(), c->s));
-  HIP_TRY(convert(c->fid, c->sum.as<uint32_t>(), c->canon.as<uint32_t>(), len, false, c->s));
-  HIP_TRY(d2h(c->h_sum.p, c->sum.p, len * wb, c->s));
-  HIP_TRY(d2h(c->h_repr.p, c->canon.p, len * wb, c->s));
-  HIP_TRY(hipEventRecord(c->ev_host, c->s));
+  HIP_TRY(collapse_fold_rows(c->fid, c->allpart.as<uint32_t>(), c->G, len, c->sum.as<uint32_t>(), c->sp));
+  HIP_TRY(convert(c->fid, c->sum.as<uint32_t>(), c->canon.as<uint32_t>(), len, false, c->sp));
+  HIP_TRY(d2h(c->h_sum.p, c->sum.p, len * wb, c->sp));
+  HIP_TRY(d2h(c->h_repr.p, c->canon.p, len * wb, c->sp));
+  HIP_TRY(hipEventRecord(c->ev_host, c->sp));
   return LCPC_OK;
 }
 
@@ -743,7 +754,7 @@ Xop op_idx_bcast(lcpc_sharded_commit *c) {
   op.recv = c->didx.as<uint8_t>();
   op.bytes = c->nco * 8;
   op.root = c->root_rank;
-  op.s = c->s;
+  op.s = c->sp;
   return op;
 }
 
@@ -755,11 +766,11 @@ lcpc_status stage_idx_upload(lcpc_sharded_commit *c) {
 
 // my rows of the opened columns (open_column, :818-855): [col][my rows], Montgomery
 lcpc_status stage_gather_cols(lcpc_sharded_commit *c) {
-  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
   if (c->nco && c->nr)
     HIP_TRY(gather_columns(c->fid, c->comm_rows.as<uint32_t>(), c->nr, c->nc, c->didx.as<uint64_t>(), c->nco,
-                           c->mycols.as<uint32_t>(), c->s, false, true));
-  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+                           c->mycols.as<uint32_t>(), c->sp, false, true));
+  HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
   return LCPC_OK;
 }
 
@@ -773,25 +784,25 @@ Xop op_cols_gather(lcpc_sharded_commit *c) {
   if (c->me == c->root_rank)
     for (int k = 0; k < c->G; k++) op.rb[k] = c->nco * (c->part[k].r_hi - c->part[k].r_lo) * c->wb;
   op.ready = c->ev_ready;
-  op.s = c->s;
+  op.s = c->sp;
   return op;
 }
 
 // root: Merkle paths off the whole tree, everything to the host
 lcpc_status stage_paths(lcpc_sharded_commit *c) {
-  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
   if (c->me != c->root_rank) {
-    HIP_TRY(hipEventRecord(c->ev_host, c->s));
+    HIP_TRY(hipEventRecord(c->ev_host, c->sp));
     return LCPC_OK;
   }
   const size_t pl = log2_np2(c->nc);
   if (c->nco) {
     HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), 2 * c->nc - 1, c->didx.as<uint64_t>(), c->nco, pl,
-                         c->dpaths.as<uint8_t>(), c->s));
-    HIP_TRY(d2h(c->h_cols.p, c->allcols.p, c->nco * c->n_rows * c->wb, c->s));
-    if (pl) HIP_TRY(d2h(c->h_paths.p, c->dpaths.p, c->nco * pl * 32, c->s));
+                         c->dpaths.as<uint8_t>(), c->sp));
+    HIP_TRY(d2h(c->h_cols.p, c->allcols.p, c->nco * c->n_rows * c->wb, c->sp));
+    if (pl) HIP_TRY(d2h(c->h_paths.p, c->dpaths.p, c->nco * pl * 32, c->sp));
   }
-  HIP_TRY(hipEventRecord(c->ev_host, c->s));
+  HIP_TRY(hipEventRecord(c->ev_host, c->sp));
   return LCPC_OK;
 }
 
@@ -854,8 +865,9 @@ struct Sched {
 
 Sched make_sched(size_t ndt, int G, size_t lag, size_t n_polys) {
   Sched sc;
-  // ~1.3 ms of absorption per round over ~1.1 ms / G per tick (cfg3)
-  sc.lag = lag ? lag : 1 + (size_t)G;
+  // ~1.2 ms of absorption per round (cfg3) over ~1.05 ms / G per tick, plus the fold's trip to
+  // the host: lag 3 at one rank measured 10.8-11.0 G/s at K = 20 against 10.3-10.6 with lag 2
+  sc.lag = lag ? lag : 2 + (size_t)G;
   sc.ndt = ndt;
   sc.rounds = std::max<size_t>(ndt, 1);
   sc.n_stages = 2 + 2 * sc.rounds + 2;
@@ -1260,7 +1272,23 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   const size_t hw = std::max(2u, std::thread::hardware_concurrency());
   TaskPool pool(std::min<size_t>(16, hw), e->dev->id);
   TaskPool launch(std::min<size_t>(4, hw), e->dev->id);
+  // every polynomial's encode goes on one stream, issued in polynomial order by one thread: the
+  // encodes finish first come first (on streams of their own they ran side by side and each
+  // commitment's root arrived late), while the short exchange-side and prove kernels run on each
+  // polynomial's priority stream
+  TaskPool encoder(1, e->dev->id);
+  hipStream_t bulk = e->dev->acquire_stream(false);
+  if (!bulk) return fail(LCPC_ERR_DEVICE, "no HIP stream");
+  struct BulkRelease {  // (destroyed after cs: returns the stream to the pool)
+    Device *d;
+    hipStream_t s;
+    ~BulkRelease() { d->release_stream(s, false); }
+  } bulk_release{e->dev, bulk};
   std::vector<ShardPtr> cs(n_polys);
+  struct BulkDrain {  // (destroyed before cs: no polynomial is torn down under its running encode)
+    hipStream_t s;
+    ~BulkDrain() { (void)hipStreamSynchronize(s); }
+  } bulk_drain{bulk};
   std::vector<std::future<lcpc_status>> pending(n_polys);  // the polynomial's outstanding launch task
   std::deque<std::pair<size_t, std::future<lcpc_status>>> finals;  // (poly, host_proof)
   std::vector<size_t> to_finalize;
@@ -1304,15 +1332,16 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
                         })));
   };
   auto start = [&](size_t k) {
-    pending[k] = launch.submit(wrap([&, k]() -> lcpc_status {
-      lcpc_status s2 = shard_init(e, comm, n_rows, cs[k]);
+    pending[k] = encoder.submit(wrap([&, k]() -> lcpc_status {
+      lcpc_status s2 = shard_init(e, comm, n_rows, cs[k], bulk);
       if (s2) return s2;
       return stage_pre_commit(cs[k].get(), d_rows[k]);
     }));
   };
-  // polynomial k's encode is launched two ticks before its chaining-value exchange, so a tick's
+  // polynomial k's encode is launched AHEAD ticks before its chaining-value exchange, so a tick's
   // exchange group (which waits for every producer in it) does not wait on a just-launched encode
-  constexpr size_t AHEAD = 2;
+  // and the encode stream stays fed while a tick waits on the host
+  constexpr size_t AHEAD = 3;
   for (size_t k = 0; k < std::min(AHEAD, n_polys); k++) start(k);
   for (size_t t = 0; t < n_ticks; t++) {
     prof::HostScope hs_tick("tick_total");
@@ -1426,6 +1455,71 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   }
   HIP_TRY(hipStreamSynchronize(comm->cs));
   return first ? fail(first, msg) : LCPC_OK;
+}
+
+lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_comm *comm, size_t n_polys,
+                                 size_t lag) {
+  lcpc_status st = check_shardable(e, comm, n_rows);
+  if (st) return st;
+  if (n_polys == 0) return LCPC_OK;
+  Device *dev = e->dev;
+  HIP_TRY(hipSetDevice(dev->id));
+  const int G = comm->nranks, me = comm->rank;
+  const Sched sc = make_sched(e->n_degree_tests, G, lag, n_polys);
+  // polynomials alive at once: launched AHEAD ticks early, released a tick after their last stage
+  const size_t depth = std::min(n_polys, sc.off[sc.s_cols] + 4);
+  lcpc_sharded_commit g;  // descriptor only: the sizes the stages ask of the pools
+  shard_geom(&g, e->fid, e->n_per_row, e->n_cols, n_rows, G, me);
+  const size_t wb = g.wb, np = g.np, nc = g.nc, nr = g.nr, B = g.B, nco = e->n_col_opens;
+  const size_t nch = g.part[me].c_hi - g.part[me].c_lo, pl = log2_np2(nc);
+  // (the expressions of stage_pre_commit, stage_post_cv, stage_post_subtrees and prove_alloc)
+  std::vector<size_t> dsz = {nr * np * wb + 16, nr * nc * wb + 16, nch * nc * 32 + 16, (2 * B - 1) * 32,
+                             (2 * nc - 1) * 32, n_rows * wb, 2 * std::max<size_t>(nr, 1) * wb, 2 * np * wb,
+                             collapse_scratch_bytes(e->fid, std::max<size_t>(nr, 1), np, 2),
+                             std::max<size_t>(nco, 1) * 8, std::max<size_t>(nco * nr, 1) * wb};
+  if (G > 1) {  // (one rank exchanges in place)
+    dsz.push_back(g.n_chunks * B * 32 + 16);
+    dsz.push_back((size_t)G * (2 * B - 1) * 32);
+  }
+  std::vector<size_t> psz = {32, n_rows * wb, std::max<size_t>(nco, 1) * 8};
+  if (nr) psz.push_back(nr * wb);
+  // the transcript rank of polynomial k is k % G: its share of the depth
+  const size_t root_depth = (depth + G - 1) / G;
+  std::vector<size_t> rdsz = {(size_t)G * 2 * np * wb, 2 * np * wb, 2 * np * wb,
+                              std::max<size_t>(nco * n_rows, 1) * wb, std::max<size_t>(nco * pl, 1) * 32};
+  std::vector<size_t> rpsz = {2 * np * wb, 2 * np * wb, np * wb, std::max<size_t>(nco * n_rows, 1) * wb,
+                              std::max<size_t>(nco * pl, 1) * 32};
+  std::vector<void *> blocks, pins;
+  auto take = [&](const std::vector<size_t> &d, const std::vector<size_t> &h, size_t count) -> lcpc_status {
+    for (size_t k = 0; k < count; k++) {
+      for (size_t b : d) {
+        void *p = nullptr;
+        if (dev->alloc(&p, b) != hipSuccess) return fail(LCPC_ERR_OUT_OF_MEMORY, "reserve: device pool");
+        blocks.push_back(p);
+      }
+      for (size_t b : h) {
+        void *p = dev->pinned_get(b);
+        if (!p) return fail(LCPC_ERR_OUT_OF_MEMORY, "reserve: pinned staging");
+        pins.push_back(p);
+      }
+    }
+    return LCPC_OK;
+  };
+  st = take(dsz, psz, depth);
+  if (!st) st = take(rdsz, rpsz, root_depth);
+  for (void *p : blocks) dev->release(p);
+  for (void *p : pins) dev->pinned_put(p);
+  // two streams per polynomial in flight (commit, prove)
+  std::vector<hipStream_t> lo, hi;
+  for (size_t k = 0; k < depth; k++) {
+    lo.push_back(dev->acquire_stream(false));
+    if (shard_prio_streams()) hi.push_back(dev->acquire_stream(true));
+  }
+  for (hipStream_t x : lo)
+    if (x) dev->release_stream(x, false);
+  for (hipStream_t x : hi)
+    if (x) dev->release_stream(x, true);
+  return st;
 }
 
 lcpc_status lcpc_sharded_p2p_schedule(lcpc_field f, size_t n_rows, size_t n_per_row, size_t n_cols,

@@ -723,6 +723,11 @@ def pos_pack_shard(d_bytes: int, n_bytes: int, n_per_row: int, row0: int, n_shar
                                                      C.c_void_p(stream) if stream else None))
 
 
+def sharded_reserve(enc, comm: NativeComm, n_rows: int, n_polys: int, lag: int = 0):
+    """lcpc_sharded_reserve: pre-populate the pools for sharded_commit_prove_many(n_polys, lag)."""
+    _check(_lib().lcpc_sharded_reserve(enc._h, n_rows, comm._h, n_polys, lag))
+
+
 def sharded_commit_prove_many(enc, comm: NativeComm, d_rows: Sequence[int], n_rows: int, outer, make_transcript,
                               lag: int = 0, keep_proofs: bool = True):
     """lcpc_sharded_commit_prove_many: pipelined commit + prove of len(d_rows) polynomials.
