@@ -349,6 +349,9 @@ __global__ __launch_bounds__(256) void k_leaf_chunks_words(const uint32_t *__res
   uint32_t cv[8];
   iv(cv);
   const uint32_t *colp = m + col * col_stride * N;
+  // elements that start before the end of the launch's chunk range: a row shard holds exactly
+  // those (its range ends on an element boundary), so nothing past it is ever loaded
+  const size_t w_end = (size_t)chunk_end * 256;
   for (int b = 0; b < nb; b++) {
     const long long sw0 = (long long)(w0 + 16 * (size_t)b) - 8;  // stream word of the block's word 0
     const long long e0 = sw0 >= 0 ? sw0 / N : -((-sw0 + N - 1) / N);
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(256) void k_leaf_chunks_words(const uint32_t *__res
     for (int k = 0; k < 4; k++) {
       const long long e = e0 + k;
       uint32_t r[N];
-      if (e < 0 || (size_t)e >= n_rows) {
+      if (e < 0 || (size_t)e >= n_rows || 8 + (size_t)e * N >= w_end) {
 #pragma unroll
         for (int i = 0; i < N; i++) r[i] = 0;
       } else {

@@ -126,6 +126,28 @@ struct Device {
     if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? hi : lo) != hipSuccess) return nullptr;
     return s;
   }
+  // Commitments in FIFO order (LCPC_COMMIT_FIFO=1; off by default): every commit enqueues its
+  // whole kernel sequence on this one stream under commit_mu, so concurrent commits run back to
+  // back at the full GPU, first come first finished, instead of side by side on streams of their
+  // own.  Same-box A/B (profiles/r03_commit_fifo_ab.json): cfg3 K = 20 12.2 either way (the
+  // commits then complete every 1.15 ms and the last proof's 4.1 ms is the tail), K = 256
+  // 15.6 against 16.3, cfg5 29.2 against 27.8, cfg4 5.5 against 6.6: not the default.
+  std::mutex commit_mu;
+  hipStream_t commit_s = nullptr;
+  static bool fifo_commits() {
+    static const bool v = [] {
+      const char *e = getenv("LCPC_COMMIT_FIFO");
+      return e && e[0] == '1' && !serial_mode();
+    }();
+    return v;
+  }
+  hipStream_t commit_stream() {  // (under commit_mu)
+    if (!commit_s) {
+      (void)hipSetDevice(id);
+      if (hipStreamCreateWithFlags(&commit_s, hipStreamNonBlocking) != hipSuccess) commit_s = nullptr;
+    }
+    return commit_s;
+  }
   void release_stream(hipStream_t s, bool high) {
     if (serial_mode()) return;
     std::lock_guard<std::mutex> lk(mu);
@@ -248,6 +270,21 @@ inline Device *get_device(int id, lcpc_status *st) {
 }
 
 inline thread_local hipStream_t t_stream = nullptr;  // stream of the innermost live Lease
+
+// this thread's completion event for device `id` (created on first use; the calling thread has
+// made that device current)
+inline hipEvent_t t_event(int id) {
+  thread_local struct Events {
+    hipEvent_t e[64] = {};
+    ~Events() {
+      for (hipEvent_t x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } te;
+  if (id < 0 || id >= 64) return nullptr;
+  if (!te.e[id] && hipEventCreateWithFlags(&te.e[id], hipEventDisableTiming) != hipSuccess) te.e[id] = nullptr;
+  return te.e[id];
+}
 
 // A stream leased for the duration of one API call (also makes the device current).
 struct Lease {

@@ -99,6 +99,19 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   hipStream_t s = lease.s;
+  // FIFO commits: the whole sequence below goes on the device's commit stream while commit_mu is
+  // held (buffers allocated meanwhile record that stream), then this call waits for its own
+  // completion event only
+  std::unique_lock<std::mutex> fifo;
+  hipEvent_t done = nullptr;
+  if (Device::fifo_commits()) {
+    fifo = std::unique_lock<std::mutex>(dev->commit_mu);
+    if (hipStream_t cs = dev->commit_stream()) {
+      s = cs;
+      t_stream = cs;  // (restored by ~Lease)
+      done = t_event(dev->id);
+    }
+  }
   const int fid = e->fid, wb = field_bytes(fid);
   auto c = std::make_unique<lcpc_commit>();
   c->fid = fid;
@@ -113,6 +126,7 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   HIP_TRY(c->comm.alloc(dev, n_rows * nc * wb));
   uint8_t *cf = c->coeffs.as<uint8_t>();
   uint8_t *cm = c->comm.as<uint8_t>();
+  DBuf tmp;  // (SDIG scratch; at function scope, so that no block exit drains the stream)
   if (e->kind == KIND_SDIG) {
     // element-major codeword [n_cols][n_rows]: the message part is the coefficient matrix
     // transposed, the SDIG levels fill the rest, and each leaf is a contiguous column
@@ -127,7 +141,6 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
       HIP_TRY(transpose_elems(fid, (const uint32_t *)d_src, n_rows, np, np, np, (uint32_t *)cm, n_rows, s,
                               TR_PLAIN, nullptr, len, (uint32_t *)cf, np));
     }
-    DBuf tmp;
     HIP_TRY(tmp.alloc(dev, e->sdig.tmp_elems * n_rows * wb));
     HIP_TRY(sdig_encode_cm(e->sdig, (uint32_t *)cm, n_rows, tmp.as<uint32_t>(), s));
   } else if (src_is_host) {
@@ -165,7 +178,16 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   uint8_t *h_root = (uint8_t *)t_pin[PIN_OUTER].get(32);
   if (!h_root) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
   HIP_TRY(d2h(h_root, c->hashes.as<uint8_t>() + (c->n_hashes - 1) * 32, 32, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  if (done) {
+    HIP_TRY(hipEventRecord(done, s));
+    fifo.unlock();
+    HIP_TRY(hipEventSynchronize(done));
+    // this commit's work is complete: its scratch needs no drain of the shared stream
+    tmp.settle();
+    scratch.settle();
+  } else {
+    HIP_TRY(hipStreamSynchronize(s));
+  }
   std::memcpy(c->root, h_root, 32);
   c->coeffs.settle();
   c->comm.settle();

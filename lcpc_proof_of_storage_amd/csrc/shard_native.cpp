@@ -314,12 +314,22 @@ size_t chunk_first_row(int fid, size_t chunk, size_t n_chunks, size_t n_rows) {
   return std::min(n_rows, (1024 * chunk - 32 + wb - 1) / wb);
 }
 
+// A rank boundary must fall on a chunk boundary that is also an element boundary, so that every
+// element of a rank's chunks is its own: chunk c (message byte 1024 c) qualifies iff
+// (1024 c - 32) is a multiple of the element size -- every chunk for 8/16/32-byte elements, one
+// chunk in three for Ft191's 24 bytes (c = 2 mod 3).  The qualifying boundaries cut the message
+// into units that are dealt to the ranks evenly.
 std::vector<Part> partition(int fid, size_t n_rows, int G) {
-  const size_t nch = leaf_n_chunks(fid, n_rows);
+  const size_t nch = leaf_n_chunks(fid, n_rows), wb = (size_t)field_bytes(fid);
+  std::vector<size_t> cuts{0};
+  for (size_t c = 1; c < nch; c++)
+    if ((1024 * c - 32) % wb == 0) cuts.push_back(c);
+  cuts.push_back(nch);
+  const size_t units = cuts.size() - 1;
   std::vector<Part> p(G);
   for (int g = 0; g < G; g++) {
-    p[g].c_lo = (size_t)g * nch / G;
-    p[g].c_hi = (size_t)(g + 1) * nch / G;
+    p[g].c_lo = cuts[(size_t)g * units / G];
+    p[g].c_hi = cuts[(size_t)(g + 1) * units / G];
     p[g].r_lo = chunk_first_row(fid, p[g].c_lo, nch, n_rows);
     p[g].r_hi = chunk_first_row(fid, p[g].c_hi, nch, n_rows);
   }
@@ -420,8 +430,6 @@ using ShardPtr = std::unique_ptr<lcpc_sharded_commit, ShardDeleter>;
 // the shape conditions of a row-sharded commitment (no device needed)
 lcpc_status check_geom(int fid, int kind, size_t n_cols, int G, size_t n_rows) {
   if (kind != KIND_RS) return fail(LCPC_ERR_UNSUPPORTED, "row shards: Ligero / R-S encodings only");
-  if (1024 % field_bytes(fid))  // Ft191: an element would straddle two ranks' chunks
-    return fail(LCPC_ERR_UNSUPPORTED, "row shards: the element size must divide a 1 KiB BLAKE3 chunk");
   if (G < 1 || (G & (G - 1)) || n_cols % (size_t)G)
     return fail(LCPC_ERR_UNSUPPORTED, "row shards need a power-of-two rank count dividing n_cols");
   if (n_rows == 0) return fail(LCPC_ERR_INVALID_ARG, "n_rows");

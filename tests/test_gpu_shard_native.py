@@ -21,7 +21,14 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-CASES = {"ft127": (1, 1 << 16), "ft63": (0, 3 * 4096 + 17), "ft255": (3, 20000), "ft127_ragged": (1, 5 * 2048 + 3)}
+CASES = {"ft127": (1, 1 << 16), "ft63": (0, 3 * 4096 + 17), "ft255": (3, 20000), "ft127_ragged": (1, 5 * 2048 + 3),
+         # Ft191's 24-byte elements: rank cuts only where a 1 KiB chunk starts on an element
+         # (rows 84 + 128 k); 300 rows of 64 -> 128 give three such units
+         "ft191": (2, 300 * 64 - 5, (64, 128))}
+
+
+def _encoding(L, fid, n, dims=None):
+    return L.LigeroEncoding.new_from_dims(fid, *dims) if dims else L.LigeroEncoding.new(fid, n)
 
 
 def _transcript(L, root, nco):
@@ -65,10 +72,10 @@ def _oracle_same(fid, enc, coeffs, outer, root, fields):
             and b"".join(fields["paths"]) == op.paths.tobytes())
 
 
-def _run_rank(L, hipmem, comm, fid, n, seed=9, root_rank=0):
+def _run_rank(L, hipmem, comm, fid, n, seed=9, root_rank=0, dims=None):
     """commit + prove through the native sharded entry points; returns what rank-0 checks."""
     from lcpc_proof_of_storage_amd import shard
-    enc = L.LigeroEncoding.new(fid, n)
+    enc = _encoding(L, fid, n, dims)
     coeffs = L.field_random(fid, n, seed)
     single = L.LcCommit.commit(coeffs, enc)
     outer = L.field_random(fid, single.get_n_rows(), seed + 1)
@@ -155,8 +162,7 @@ def test_native_sharded_world1(gpu, hipmem, kind, case):
         assert L.lcpc_comm_rccl_new(uid, 1, 0, C.byref(h)) == 0, N.last_error()
         comm = shard.NativeComm(h.value)
         assert comm.is_rccl
-    fid, n = CASES[case]
-    res = _run_rank(gpu, hipmem, comm, fid, n)
+    res = _run_rank(gpu, hipmem, comm, *CASES[case][:2], dims=(CASES[case][2] if len(CASES[case]) > 2 else None))
     assert all(res.values()), res
 
 
@@ -221,10 +227,10 @@ def _spawn(job, args, timeout=280, world=2):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("root_rank", [0, 1])
-@pytest.mark.parametrize("case", ["ft127", "ft63", "ft127_ragged"])
+@pytest.mark.parametrize("case", ["ft127", "ft63", "ft127_ragged", "ft191"])
 def test_native_sharded_world2_one_gpu(gpu, case, root_rank):
-    fid, n = CASES[case]
-    res = _spawn("rank", (fid, n, 9, root_rank))
+    fid, n = CASES[case][:2]
+    res = _spawn("rank", (fid, n, 9, root_rank, CASES[case][2] if len(CASES[case]) > 2 else None))
     for r in (0, 1):
         assert "error" not in res[r] and all(res[r].values()), (r, res[r])
 
@@ -241,9 +247,10 @@ def test_native_pipeline_world2_one_gpu(gpu):
 # leaves three ranks without rows, 2^20's three chunks leave one)
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("root_rank", [0, 3])
-@pytest.mark.parametrize("fid,n", [(1, 1 << 22), (1, 1 << 16), (0, 3 * 4096 + 17)])
-def test_native_sharded_world4_one_gpu(gpu, fid, n, root_rank):
-    res = _spawn("rank", (fid, n, 9, root_rank), world=4)
+@pytest.mark.parametrize("fid,n,dims", [(1, 1 << 22, None), (1, 1 << 16, None), (0, 3 * 4096 + 17, None),
+                                        (2, 300 * 64 - 5, (64, 128))])
+def test_native_sharded_world4_one_gpu(gpu, fid, n, dims, root_rank):
+    res = _spawn("rank", (fid, n, 9, root_rank, dims), world=4)
     for r in range(4):
         assert "error" not in res[r] and all(res[r].values()), (r, res[r])
 

@@ -109,6 +109,7 @@ def test_cfg3_groups_match(G):
     (FT127, 3, 16, 32, 1, 5, 4),     # fewer rows than ranks: empty shards
     (FT63, 100, 128, 256, 3, 11, 8),
     (FT255, 9, 64, 128, 0, 4, 2),    # no degree tests: round 0 is the evaluation alone
+    (2, 700, 256, 512, 2, 9, 4),     # Ft191: 24-byte elements, cuts every third chunk
     (FT127, 512, 32768, 65536, 2, 309, 8),
 ])
 @pytest.mark.parametrize("lag", [0, 1, 5])
@@ -129,4 +130,20 @@ def test_schedule_rejects_bad_rank_counts():
     lib = _native.load()
     n = C.c_size_t()
     assert lib.lcpc_sharded_p2p_schedule(FT127, 512, 32768, 65536, 2, 309, 3, 0, 4, 0, None, 0, C.byref(n)) != 0
-    assert lib.lcpc_sharded_p2p_schedule(2, 512, 32768, 65536, 2, 309, 2, 0, 4, 0, None, 0, C.byref(n)) != 0  # Ft191
+    assert lib.lcpc_sharded_p2p_schedule(FT127, 512, 32768, 65536, 2, 309, 16, 0, 4, 0, None, 0, C.byref(n)) == 30
+
+
+@pytest.mark.parametrize("fid,wb", [(0, 8), (1, 16), (2, 24), (3, 32)])
+@pytest.mark.parametrize("n_rows", [1, 41, 84, 85, 512, 9363])
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+def test_row_cuts_fall_on_chunk_and_element_boundaries(fid, wb, n_rows, G):
+    """lcpc_sharded_rows: the ranks' rows tile [0, n_rows) in order, and every cut is where a
+    1 KiB BLAKE3 chunk of the leaf message (32 zero bytes || column) starts on an element
+    boundary, so a rank's chunks hold only its own elements (Ft191: 24-byte elements)."""
+    rows = rows_of(fid, n_rows, G)
+    assert rows[0][0] == 0 and sum(nr for _, nr in rows) == n_rows
+    for (r0, nr), (r1, _) in zip(rows, rows[1:]):
+        assert r0 + nr == r1
+    for r0, _ in rows[1:]:
+        if 0 < r0 < n_rows:
+            assert (32 + r0 * wb) % 1024 == 0, (r0, wb)
