@@ -617,6 +617,9 @@ def ligero_sharded(args, L, torch, dist, rank, world, device, backend, share):
         comm, comm_kind = shard.NativeComm.single(), "none (one rank)"
     elif backend == "nccl" and not share:
         comm, comm_kind = shard.NativeComm.rccl(dist), "RCCL (liblcpc_mi lcpc_comm_rccl_new, device send/recv)"
+    elif os.environ.get("LCPC_BENCH_RCCL_SAME_GPU") == "1":
+        comm, comm_kind = (shard.NativeComm.rccl(dist),
+                           "RCCL with the ranks sharing one GPU (per-rank NCCL_HOSTID: socket transport over loopback)")
     else:
         comm, comm_kind = shard.NativeComm.host(dist), "host-staged gloo collectives (ranks share one GPU)"
     assert comm.world == world and comm.rank == rank, (comm.world, comm.rank)
@@ -667,6 +670,11 @@ def main():
     # rank per GPU over RCCL
     backend = os.environ.get("LCPC_BENCH_BACKEND", "nccl")
     share = os.environ.get("LCPC_BENCH_SHARE_GPU") == "1"
+    # LCPC_BENCH_RCCL_SAME_GPU=1 (with the two above): the ranks share GPU 0 but the library's
+    # exchanges still go through RCCL -- a distinct NCCL_HOSTID per rank makes RCCL treat them as
+    # separate nodes (loopback sockets), so its multi-rank send / receive groups run on one GPU
+    if os.environ.get("LCPC_BENCH_RCCL_SAME_GPU") == "1" and share:
+        os.environ.update(NCCL_HOSTID=f"lcpc-bench-rank-{rank}", NCCL_IB_DISABLE="1", NCCL_SOCKET_IFNAME="lo")
     device_idx = 0 if share else local_rank
     dist = init_dist(world, device_idx, backend=backend)
     formed = dist.get_world_size() if dist is not None else 1

@@ -454,7 +454,7 @@ int lcpc_comm_is_rccl(const lcpc_comm *c);
 void lcpc_comm_free(lcpc_comm *c);
 
 /* ------------------------------------------------------------------ row-sharded commitments
- * One Ligero commitment whose n_rows coefficient rows are split over the comm's ranks
+ * One Ligero or Brakedown commitment whose n_rows coefficient rows are split over the comm's ranks
  * (SURVEY.md §8e), reproducing commit (lcpc-2d/src/lib.rs:651-815) and prove (:1034-1123) bit
  * for bit.  Rank g encodes rows [row0_g, row0_g + n_g) -- cut on BLAKE3 chunk boundaries of the
  * leaf message -- and the chaining values of its chunks of every column; an all-to-all by column
@@ -462,7 +462,11 @@ void lcpc_comm_free(lcpc_comm *c);
  * every rank the whole Merkle tree (the bytes of lcpc_commit_copy_hashes).  prove runs the
  * Merlin transcript on one `root` rank: it broadcasts each challenge vector, gathers the ranks'
  * partial row combinations and folds them mod p (RCCL has no mod-p reduction), then gathers the
- * opened columns' row pieces.  Needs a power-of-two rank count dividing n_cols. */
+ * opened columns' row pieces.  Needs a power-of-two rank count of at most next_pow2(n_cols).
+ * Rows are cut where a 1 KiB chunk starts on an element boundary (every chunk for 8/16/32-byte
+ * elements, every third for Ft191).  Brakedown shards are element-major ([n_cols][rows], the
+ * rows encoded independently, lcpc-brakedown-pc/src/encode.rs:36-94); the tree's leaves past
+ * n_cols are zero digests, as in the single-GPU commit. */
 /* the rows of rank `rank` */
 lcpc_status lcpc_sharded_rows(lcpc_field f, size_t n_rows, int nranks, int rank, size_t *row0,
                               size_t *n_shard_rows);

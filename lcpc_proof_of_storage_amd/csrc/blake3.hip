@@ -578,7 +578,7 @@ size_t leaf_n_chunks(int fid, size_t n_rows) {
 
 hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows, size_t n_cols,
                           size_t stride, size_t chunk_lo, size_t chunk_hi, uint32_t *cvs,
-                          hipStream_t s, bool canon, size_t blk) {
+                          hipStream_t s, bool canon, size_t blk, size_t col_stride) {
   if (n_cols == 0 || chunk_hi <= chunk_lo) return hipSuccess;
   const int n_chunks = (int)leaf_n_chunks(fid, n_rows);
   dim3 grid((unsigned)((n_cols + 255) / 256), (unsigned)(chunk_hi - chunk_lo));
@@ -587,22 +587,22 @@ hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows
       prof::Scope ps("leaf_chunks", s);
       if (canon)
         hipLaunchKernelGGL((k_leaf_chunks<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
-                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
+                           col_stride, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
                            (int)chunk_hi, blk);
       else
         hipLaunchKernelGGL((k_leaf_chunks<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
-                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
+                           col_stride, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo,
                            (int)chunk_hi, blk);
       return hipGetLastError();
     } else {
       prof::Scope ps("leaf_chunks", s);
       if (canon)
         hipLaunchKernelGGL((k_leaf_chunks_words<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
-                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi,
+                           col_stride, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi,
                            blk);
       else
         hipLaunchKernelGGL((k_leaf_chunks_words<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
-                           (size_t)1, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi,
+                           col_stride, cvs, (uint8_t *)nullptr, n_chunks, row0, (int)chunk_lo, (int)chunk_hi,
                            blk);
       return hipGetLastError();
     }

@@ -52,11 +52,12 @@ hipError_t leaf_hashes(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
 // (messages of n_rows rows in total) from a row-major shard m holding rows [row0, ...);
 // cvs[(chunk - chunk_lo) * n_cols + col] (8 words), or with blk > 0 the exchange layout
 // cvs[((col / blk) * (chunk_hi - chunk_lo) + chunk - chunk_lo) * blk + col % blk].  Chunk c starts
-// at message byte 1024 c.
+// at message byte 1024 c.  col_stride: elements between columns (1: row-major m; the shard's row
+// count with stride 1: an element-major [n_cols][rows] shard).
 size_t leaf_n_chunks(int fid, size_t n_rows);
 hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows, size_t n_cols,
                           size_t stride, size_t chunk_lo, size_t chunk_hi, uint32_t *cvs,
-                          hipStream_t s, bool canon = false, size_t blk = 0);
+                          hipStream_t s, bool canon = false, size_t blk = 0, size_t col_stride = 1);
 // leaf digests from all n_chunks chaining values ([chunk][col] layout; cvs is clobbered)
 hipError_t leaves_from_cvs(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t *leaves,
                            hipStream_t s);

@@ -362,7 +362,8 @@ struct lcpc_sharded_commit {
   lcpc_comm *comm = nullptr;
   Device *dev = nullptr;
   int fid = 1, wb = 16, G = 1, me = 0;
-  size_t n_rows = 0, np = 0, nc = 0, B = 0, n_chunks = 0, nr = 0;
+  bool sdig = false;  // Brakedown: element-major shard [n_cols][nr], Montgomery codeword
+  size_t n_rows = 0, np = 0, nc = 0, np2 = 0, B = 0, n_chunks = 0, nr = 0;  // np2 leaves, B = np2 / G
   std::vector<Part> part;
   hipStream_t s = nullptr;        // this polynomial's encode stream (shared, in order, by the
                                   // pipelined driver's polynomials: encodes finish first come first)
@@ -372,7 +373,7 @@ struct lcpc_sharded_commit {
   hipEvent_t ev_done = nullptr;   // the last exchange completed (comm stream)
   hipEvent_t ev_host = nullptr;   // device -> host copies of the last stage landed
   DBuf coeffs, comm_rows, hashes;  // kept for prove
-  DBuf cv_send, cv_recv, sub, subs;  // commit scratch
+  DBuf cv_send, cv_recv, sub, subs, sdig_tmp;  // commit scratch
   uint8_t root[32] = {0};
   // prove state
   int root_rank = 0;
@@ -416,7 +417,7 @@ struct ShardDeleter {
     if (sp) (void)hipStreamSynchronize(sp);
     // the stream has drained: no buffer needs its own drain on release (one hipStreamSynchronize
     // per buffer cost ~0.4 ms per polynomial)
-    for (DBuf *b : {&c->coeffs, &c->comm_rows, &c->hashes, &c->cv_send, &c->cv_recv, &c->sub, &c->subs,
+    for (DBuf *b : {&c->coeffs, &c->comm_rows, &c->hashes, &c->cv_send, &c->cv_recv, &c->sub, &c->subs, &c->sdig_tmp,
                     &c->bt, &c->tens, &c->part_d, &c->allpart, &c->sum, &c->canon, &c->didx, &c->mycols,
                     &c->allcols, &c->dpaths, &c->scratch})
       b->settle();
@@ -429,9 +430,9 @@ using ShardPtr = std::unique_ptr<lcpc_sharded_commit, ShardDeleter>;
 
 // the shape conditions of a row-sharded commitment (no device needed)
 lcpc_status check_geom(int fid, int kind, size_t n_cols, int G, size_t n_rows) {
-  if (kind != KIND_RS) return fail(LCPC_ERR_UNSUPPORTED, "row shards: Ligero / R-S encodings only");
-  if (G < 1 || (G & (G - 1)) || n_cols % (size_t)G)
-    return fail(LCPC_ERR_UNSUPPORTED, "row shards need a power-of-two rank count dividing n_cols");
+  if (kind != KIND_RS && kind != KIND_SDIG) return fail(LCPC_ERR_UNSUPPORTED, "row shards: unknown encoding");
+  if (G < 1 || (G & (G - 1)) || next_pow2(n_cols) % (size_t)G)
+    return fail(LCPC_ERR_UNSUPPORTED, "row shards need a power-of-two rank count of at most next_pow2(n_cols)");
   if (n_rows == 0) return fail(LCPC_ERR_INVALID_ARG, "n_rows");
   return LCPC_OK;
 }
@@ -445,7 +446,9 @@ lcpc_status check_shardable(const lcpc_encoding *e, lcpc_comm *comm, size_t n_ro
 }
 
 // the partition and sizes every exchange descriptor reads (host only)
-void shard_geom(lcpc_sharded_commit *c, int fid, size_t np, size_t nc, size_t n_rows, int G, int me) {
+void shard_geom(lcpc_sharded_commit *c, int fid, size_t np, size_t nc, size_t n_rows, int G, int me,
+                bool sdig = false) {
+  c->sdig = sdig;
   c->fid = fid;
   c->wb = field_bytes(fid);
   c->G = G;
@@ -453,7 +456,8 @@ void shard_geom(lcpc_sharded_commit *c, int fid, size_t np, size_t nc, size_t n_
   c->n_rows = n_rows;
   c->np = np;
   c->nc = nc;
-  c->B = nc / G;
+  c->np2 = next_pow2(nc);  // the Merkle tree's leaves: columns, then zero digests (SDIG)
+  c->B = c->np2 / G;
   c->n_chunks = leaf_n_chunks(fid, n_rows);
   c->part = partition(fid, n_rows, G);
   c->nr = c->part[me].r_hi - c->part[me].r_lo;
@@ -476,7 +480,7 @@ lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, S
   c->e = e;
   c->comm = comm;
   c->dev = e->dev;
-  shard_geom(c.get(), e->fid, e->n_per_row, e->n_cols, n_rows, comm->nranks, comm->rank);
+  shard_geom(c.get(), e->fid, e->n_per_row, e->n_cols, n_rows, comm->nranks, comm->rank, e->kind == KIND_SDIG);
   HIP_TRY(hipSetDevice(c->dev->id));
   c->own_s = bulk == nullptr;
   c->s = bulk ? bulk : c->dev->acquire_stream(false);
@@ -510,16 +514,26 @@ lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
   const size_t nch = pm.c_hi - pm.c_lo, wb = c->wb;
   HIP_TRY(salloc(c, c->coeffs, c->nr * c->np * wb + 16));
   HIP_TRY(salloc(c, c->comm_rows, c->nr * c->nc * wb + 16));
-  HIP_TRY(salloc(c, c->cv_send, nch * c->nc * 32 + 16));
+  HIP_TRY(salloc(c, c->cv_send, nch * c->np2 * 32 + 16));
   if (c->G > 1) HIP_TRY(salloc(c, c->cv_recv, c->n_chunks * c->B * 32 + 16));  // (one rank: cv_send itself)
-  if (c->nr) {
-    if (!d_rows) return fail(LCPC_ERR_INVALID_ARG, "null rows");
+  if (c->nr && !d_rows) return fail(LCPC_ERR_INVALID_ARG, "null rows");
+  if (c->nr && c->sdig) {
+    // Brakedown rows (lcpc-brakedown-pc/src/encode.rs:36-94, independent per row): this rank's
+    // rows transposed to the element-major shard [n_cols][nr] (one pass also writes the padded
+    // row-major coefficient copy), then the expander levels on those rows
+    HIP_TRY(transpose_elems(c->fid, (const uint32_t *)d_rows, c->nr, c->np, c->np, c->np,
+                            c->comm_rows.as<uint32_t>(), c->nr, c->s, TR_PLAIN, nullptr, c->nr * c->np,
+                            c->coeffs.as<uint32_t>(), c->np));
+    HIP_TRY(salloc(c, c->sdig_tmp, c->e->sdig.tmp_elems * c->nr * wb + 16));
+    HIP_TRY(sdig_encode_cm(c->e->sdig, c->comm_rows.as<uint32_t>(), c->nr, c->sdig_tmp.as<uint32_t>(), c->s));
+  } else if (c->nr) {
     HIP_TRY(ntt_rows(c->e->plan, (const uint32_t *)d_rows, c->np, c->np, c->comm_rows.as<uint32_t>(), c->nc, c->nr,
                      c->s, c->coeffs.as<uint32_t>(), c->np, true));
   }
   if (nch)  // chaining values straight into the exchange layout [dest rank][chunk][block col]
-    HIP_TRY(leaf_chunk_cvs(c->fid, c->comm_rows.as<uint32_t>(), pm.r_lo, c->n_rows, c->nc, c->nc, pm.c_lo, pm.c_hi,
-                           c->cv_send.as<uint32_t>(), c->s, true, c->B));
+    HIP_TRY(leaf_chunk_cvs(c->fid, c->comm_rows.as<uint32_t>(), pm.r_lo, c->n_rows, c->nc, c->sdig ? 1 : c->nc,
+                           pm.c_lo, pm.c_hi, c->cv_send.as<uint32_t>(), c->s, !c->sdig, c->B,
+                           c->sdig ? c->nr : 1));
   HIP_TRY(hipEventRecord(c->ev_ready, c->s));
   return LCPC_OK;
 }
@@ -544,6 +558,9 @@ lcpc_status stage_post_cv(lcpc_sharded_commit *c) {
   HIP_TRY(salloc_p(c, c->sub, (2 * c->B - 1) * 32));
   uint32_t *cvs = (c->G > 1 ? c->cv_recv : c->cv_send).as<uint32_t>();
   HIP_TRY(leaves_from_cvs(cvs, c->B, (int)c->n_chunks, c->sub.as<uint8_t>(), c->sp));
+  // leaves past n_cols are zero digests (lcpc-2d/src/lib.rs:685-697; SDIG's n_cols is no power of 2)
+  const size_t b0 = (size_t)c->me * c->B, valid = c->nc > b0 ? std::min(c->B, c->nc - b0) : 0;
+  if (valid < c->B) HIP_TRY(hipMemsetAsync(c->sub.as<uint8_t>() + valid * 32, 0, (c->B - valid) * 32, c->sp));
   if (c->B > 1) HIP_TRY(merkle_tree(c->sub.as<uint8_t>(), c->B, c->sp));
   if (c->G > 1) HIP_TRY(salloc_p(c, c->subs, (size_t)c->G * (2 * c->B - 1) * 32));  // (one rank: sub itself)
   HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
@@ -563,7 +580,7 @@ Xop op_subtree_exchange(lcpc_sharded_commit *c) {
 // every rank: the whole tree [leaves | level 1 | ... | root] from the G subtrees + top levels
 lcpc_status stage_post_subtrees(lcpc_sharded_commit *c) {
   HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
-  const size_t nc = c->nc, B = c->B, G = c->G;
+  const size_t nc = c->np2, B = c->B, G = c->G;  // (the tree's leaf count)
   HIP_TRY(salloc_p(c, c->hashes, (2 * nc - 1) * 32));
   uint8_t *h = c->hashes.as<uint8_t>();
   HIP_TRY(assemble_subtrees((G > 1 ? c->subs : c->sub).as<uint8_t>(), B, G, h, c->sp));  // one launch, every level
@@ -580,7 +597,8 @@ lcpc_status finish_commit(lcpc_sharded_commit *c) {
   HIP_TRY(hipEventSynchronize(c->ev_host));
   std::memcpy(c->root, c->h_root.p, 32);
   // every use of the commit scratch precedes ev_host on the stream: no drain on release
-  for (DBuf *b : {&c->cv_send, &c->cv_recv, &c->sub, &c->subs}) b->settle();
+  for (DBuf *b : {&c->cv_send, &c->cv_recv, &c->sub, &c->subs, &c->sdig_tmp}) b->settle();
+  c->sdig_tmp.reset();
   c->cv_send.reset();
   c->cv_recv.reset();
   c->sub.reset();
@@ -777,7 +795,7 @@ lcpc_status stage_gather_cols(lcpc_sharded_commit *c) {
   HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
   if (c->nco && c->nr)
     HIP_TRY(gather_columns(c->fid, c->comm_rows.as<uint32_t>(), c->nr, c->nc, c->didx.as<uint64_t>(), c->nco,
-                           c->mycols.as<uint32_t>(), c->sp, false, true));
+                           c->mycols.as<uint32_t>(), c->sp, c->sdig, !c->sdig));
   HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
   return LCPC_OK;
 }
@@ -805,7 +823,7 @@ lcpc_status stage_paths(lcpc_sharded_commit *c) {
   }
   const size_t pl = log2_np2(c->nc);
   if (c->nco) {
-    HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), 2 * c->nc - 1, c->didx.as<uint64_t>(), c->nco, pl,
+    HIP_TRY(gather_paths(c->hashes.as<uint8_t>(), 2 * c->np2 - 1, c->didx.as<uint64_t>(), c->nco, pl,
                          c->dpaths.as<uint8_t>(), c->sp));
     HIP_TRY(d2h(c->h_cols.p, c->allcols.p, c->nco * c->n_rows * c->wb, c->sp));
     if (pl) HIP_TRY(d2h(c->h_paths.p, c->dpaths.p, c->nco * pl * 32, c->sp));
@@ -1107,12 +1125,12 @@ lcpc_status lcpc_sharded_commit_get_root(const lcpc_sharded_commit *c, uint8_t r
   return LCPC_OK;
 }
 
-size_t lcpc_sharded_commit_n_hashes(const lcpc_sharded_commit *c) { return c ? 2 * c->nc - 1 : 0; }
+size_t lcpc_sharded_commit_n_hashes(const lcpc_sharded_commit *c) { return c ? 2 * c->np2 - 1 : 0; }
 
 lcpc_status lcpc_sharded_commit_copy_hashes(const lcpc_sharded_commit *c, uint8_t *out) {
   if (!c || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   HIP_TRY(hipSetDevice(c->dev->id));
-  HIP_TRY(d2h(out, c->hashes.p, (2 * c->nc - 1) * 32, c->s));
+  HIP_TRY(d2h(out, c->hashes.p, (2 * c->np2 - 1) * 32, c->s));
   HIP_TRY(hipStreamSynchronize(c->s));
   return LCPC_OK;
 }
@@ -1168,6 +1186,7 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
   if (!c || !left || (!idx && n_open)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   if (n_rows != c->n_rows) return fail(LCPC_ERR_INVALID_ARG, "left vector length != n_rows");
   if (root < 0 || root >= c->G) return fail(LCPC_ERR_INVALID_ARG, "root rank");
+  if (c->sdig) return fail(LCPC_ERR_UNSUPPORTED, "proof-of-storage requests: Ligero file commitments only");
   for (size_t k = 0; k < n_open; k++)
     if (idx[k] >= c->nc) return fail(LCPC_PROVER_COLUMN_NUMBER, "ProverError::ColumnNumber");
   std::lock_guard<std::mutex> lk(c->comm->mu);
@@ -1477,14 +1496,15 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
   // polynomials alive at once: launched AHEAD ticks early, released a tick after their last stage
   const size_t depth = std::min(n_polys, sc.off[sc.s_cols] + 4);
   lcpc_sharded_commit g;  // descriptor only: the sizes the stages ask of the pools
-  shard_geom(&g, e->fid, e->n_per_row, e->n_cols, n_rows, G, me);
+  shard_geom(&g, e->fid, e->n_per_row, e->n_cols, n_rows, G, me, e->kind == KIND_SDIG);
   const size_t wb = g.wb, np = g.np, nc = g.nc, nr = g.nr, B = g.B, nco = e->n_col_opens;
   const size_t nch = g.part[me].c_hi - g.part[me].c_lo, pl = log2_np2(nc);
   // (the expressions of stage_pre_commit, stage_post_cv, stage_post_subtrees and prove_alloc)
-  std::vector<size_t> dsz = {nr * np * wb + 16, nr * nc * wb + 16, nch * nc * 32 + 16, (2 * B - 1) * 32,
-                             (2 * nc - 1) * 32, n_rows * wb, 2 * std::max<size_t>(nr, 1) * wb, 2 * np * wb,
+  std::vector<size_t> dsz = {nr * np * wb + 16, nr * nc * wb + 16, nch * g.np2 * 32 + 16, (2 * B - 1) * 32,
+                             (2 * g.np2 - 1) * 32, n_rows * wb, 2 * std::max<size_t>(nr, 1) * wb, 2 * np * wb,
                              collapse_scratch_bytes(e->fid, std::max<size_t>(nr, 1), np, 2),
                              std::max<size_t>(nco, 1) * 8, std::max<size_t>(nco * nr, 1) * wb};
+  if (g.sdig && nr) dsz.push_back(e->sdig.tmp_elems * nr * wb + 16);
   if (G > 1) {  // (one rank exchanges in place)
     dsz.push_back(g.n_chunks * B * 32 + 16);
     dsz.push_back((size_t)G * (2 * B - 1) * 32);

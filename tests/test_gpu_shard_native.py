@@ -24,11 +24,22 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CASES = {"ft127": (1, 1 << 16), "ft63": (0, 3 * 4096 + 17), "ft255": (3, 20000), "ft127_ragged": (1, 5 * 2048 + 3),
          # Ft191's 24-byte elements: rank cuts only where a 1 KiB chunk starts on an element
          # (rows 84 + 128 k); 300 rows of 64 -> 128 give three such units
-         "ft191": (2, 300 * 64 - 5, (64, 128))}
+         "ft191": (2, 300 * 64 - 5, (64, 128)),
+         # Brakedown (SdigCode3, seed 5): element-major shards, n_cols no power of two (the tree's
+         # padded leaves are zero digests); 2^16 Ft127 has 48 rows of 1330 -> 2081
+         "sdig_ft127": (1, 1 << 16, ("sdig", 5)), "sdig_ft63": (0, 3 * 4096 + 17, ("sdig", 5))}
 
 
 def _encoding(L, fid, n, dims=None):
+    if dims and dims[0] == "sdig":
+        return L.SdigEncoding.new(fid, n, dims[1], 3)
     return L.LigeroEncoding.new_from_dims(fid, *dims) if dims else L.LigeroEncoding.new(fid, n)
+
+
+def _oracle_encoding(O, fid, enc, dims=None):
+    if dims and dims[0] == "sdig":
+        return O.Encoding.sdig(fid, enc.n_per_row, seed=dims[1], code_id=3)
+    return O.Encoding.ligero(fid, enc.n_per_row, enc.n_cols, enc.get_n_col_opens(), enc.get_n_degree_tests())
 
 
 def _transcript(L, root, nco):
@@ -57,13 +68,13 @@ def _same_proof(a, b):
             and np.array_equal(a["cols"], b["cols"]) and a["paths"] == b["paths"])
 
 
-def _oracle_same(fid, enc, coeffs, outer, root, fields):
+def _oracle_same(fid, enc, coeffs, outer, root, fields, dims=None):
     """the CPU oracle's commit + proof of the same polynomial (the reference's algorithm) against
     a sharded proof's fields"""
     sys.path.insert(0, HERE)
     import oracle_ffi as O
     nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
-    o_enc = O.Encoding.ligero(fid, enc.n_per_row, enc.n_cols, nco, ndt)
+    o_enc = _oracle_encoding(O, fid, enc, dims)
     oc = O.Commit(o_enc, coeffs.reshape(-1))
     op = oc.prove(o_enc, outer.reshape(-1), O.standard_transcript(nco, oc.root()))
     pr = np.concatenate([x.reshape(-1) for x in fields["p_random"]]) if ndt else np.zeros(0, np.uint64)
@@ -92,7 +103,7 @@ def _run_rank(L, hipmem, comm, fid, n, seed=9, root_rank=0, dims=None):
         if comm.rank == root_rank:
             pf = single.prove(outer, enc, _transcript(L, single.get_root(), nco))
             res["proof"] = _same_proof(_proof_fields(spf), _proof_fields(pf))
-            res["oracle"] = _oracle_same(fid, enc, coeffs, outer, sc.get_root(), _proof_fields(spf))
+            res["oracle"] = _oracle_same(fid, enc, coeffs, outer, sc.get_root(), _proof_fields(spf), dims)
             # and the sharded proof verifies
             inner = L.field_random(fid, enc.n_per_row, seed + 2)
             ev = spf.verify(single.get_root(), outer, inner, enc, _transcript(L, single.get_root(), nco))
@@ -107,10 +118,10 @@ def _run_rank(L, hipmem, comm, fid, n, seed=9, root_rank=0, dims=None):
     return res
 
 
-def _run_many(L, hipmem, comm, fid, n, n_polys=5, lag=0):
+def _run_many(L, hipmem, comm, fid, n, n_polys=5, lag=0, dims=None):
     """the pipelined driver over n_polys polynomials (transcript rank i % world)."""
     from lcpc_proof_of_storage_amd import shard
-    enc = L.LigeroEncoding.new(fid, n)
+    enc = _encoding(L, fid, n, dims)
     nco = enc.get_n_col_opens()
     polys = [L.field_random(fid, n, 100 + i) for i in range(n_polys)]
     singles = [L.LcCommit.commit(c, enc) for c in polys]
@@ -177,15 +188,27 @@ def test_native_sharded_errors(gpu, hipmem):
     comm = shard.NativeComm.single()
     sdig = gpu.SdigEncoding.new(1, 5000, 0)
     with pytest.raises(gpu.LcpcError):
-        shard.ShardedCommit(sdig, comm, 0, 4)           # R-S encodings only
+        shard.ShardedCommit(sdig, comm, 0, 4)           # rows given, but no device pointer
     enc = gpu.LigeroEncoding.new(1, 1 << 12)
     with pytest.raises(gpu.LcpcError):
         shard.ShardedCommit(enc, comm, 0, 0)            # no rows
 
 
 # ---------------------------------------------------------------- two ranks on the one GPU
+# RCCL refuses two ranks on one GPU ("Duplicate GPU detected"): it compares (host hash, bus id).
+# Giving every rank its own NCCL_HOSTID makes the ranks look like separate nodes, so RCCL connects
+# them over its socket transport (loopback) and the multi-rank exchange path -- ncclGroupStart,
+# the p2p_plan's ncclSend / ncclRecv on device buffers, ncclGroupEnd on the comm stream -- runs
+# for real on the one GPU of this box.
+RCCL_SAME_GPU_ENV = {"NCCL_IB_DISABLE": "1", "NCCL_SOCKET_IFNAME": "lo", "LCPC_SHARD_WATCHDOG_S": "90"}
+
+
 def _worker(rank, world, port, job, args, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    rccl = job.endswith("_rccl")
+    if rccl:
+        os.environ.update(RCCL_SAME_GPU_ENV, NCCL_HOSTID=f"lcpc-test-rank-{rank}")
+        job = job[:-len("_rccl")]
     sys.path.insert(0, ROOT)
     sys.path.insert(0, HERE)
     import torch.distributed as dist
@@ -195,7 +218,8 @@ def _worker(rank, world, port, job, args, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         L.set_device(0)
-        comm = shard.NativeComm.host(dist)
+        comm = shard.NativeComm.rccl(dist) if rccl else shard.NativeComm.host(dist)
+        assert comm.is_rccl == rccl and comm.world == world
         hm = _HipMem()
         if job == "rank":
             q.put((rank, _run_rank(L, hm, comm, *args)))
@@ -227,11 +251,37 @@ def _spawn(job, args, timeout=280, world=2):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("root_rank", [0, 1])
-@pytest.mark.parametrize("case", ["ft127", "ft63", "ft127_ragged", "ft191"])
+@pytest.mark.parametrize("case", ["ft127", "ft63", "ft127_ragged", "ft191", "sdig_ft127", "sdig_ft63"])
 def test_native_sharded_world2_one_gpu(gpu, case, root_rank):
     fid, n = CASES[case][:2]
     res = _spawn("rank", (fid, n, 9, root_rank, CASES[case][2] if len(CASES[case]) > 2 else None))
     for r in (0, 1):
+        assert "error" not in res[r] and all(res[r].values()), (r, res[r])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("case,root_rank", [("ft127", 0), ("ft127_ragged", 1), ("ft63", 0), ("sdig_ft127", 1)])
+def test_native_sharded_world2_rccl_one_gpu(gpu, case, root_rank):
+    """two ranks through RCCL itself (device-side sends / receives), on the one GPU"""
+    fid, n = CASES[case][:2]
+    res = _spawn("rank_rccl", (fid, n, 9, root_rank, CASES[case][2] if len(CASES[case]) > 2 else None))
+    for r in (0, 1):
+        assert "error" not in res[r] and all(res[r].values()), (r, res[r])
+
+
+@pytest.mark.timeout(300)
+def test_native_pipeline_world2_rccl_one_gpu(gpu):
+    """the pipelined driver's tick groups (several polynomials' exchanges per ncclGroupStart /
+    ncclGroupEnd) through RCCL, two ranks on the one GPU"""
+    res = _spawn("many_rccl", (1, 1 << 14, 6, 2))
+    for r in (0, 1):
+        assert "error" not in res[r] and all(res[r].values()), (r, res[r])
+
+
+@pytest.mark.timeout(300)
+def test_native_sharded_world4_rccl_one_gpu(gpu):
+    res = _spawn("rank_rccl", (1, 1 << 22, 9, 3, None), world=4)
+    for r in range(4):
         assert "error" not in res[r] and all(res[r].values()), (r, res[r])
 
 
@@ -242,13 +292,27 @@ def test_native_pipeline_world2_one_gpu(gpu):
         assert "error" not in res[r] and all(res[r].values()), (r, res[r])
 
 
+@pytest.mark.timeout(300)
+def test_native_pipeline_sdig_world2_one_gpu(gpu):
+    """the pipelined driver on Brakedown rows (element-major shards), two ranks"""
+    res = _spawn("many", (1, 1 << 16, 5, 0, ("sdig", 5)))
+    for r in (0, 1):
+        assert "error" not in res[r] and all(res[r].values()), (r, res[r])
+
+
+def test_native_pipeline_sdig_world1(gpu, hipmem):
+    from lcpc_proof_of_storage_amd import shard
+    res = _run_many(gpu, hipmem, shard.NativeComm.single(), 1, 1 << 16, n_polys=4, dims=("sdig", 5))
+    assert all(res.values()), res
+
+
 # ---------------------------------------------------------------- four ranks on the one GPU
 # (the rank count of a 4-GPU node; 2^22 splits its 5 BLAKE3 chunks 1/1/1/2, 2^16's single chunk
 # leaves three ranks without rows, 2^20's three chunks leave one)
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("root_rank", [0, 3])
 @pytest.mark.parametrize("fid,n,dims", [(1, 1 << 22, None), (1, 1 << 16, None), (0, 3 * 4096 + 17, None),
-                                        (2, 300 * 64 - 5, (64, 128))])
+                                        (2, 300 * 64 - 5, (64, 128)), (1, 1 << 16, ("sdig", 5))])
 def test_native_sharded_world4_one_gpu(gpu, fid, n, dims, root_rank):
     res = _spawn("rank", (fid, n, 9, root_rank, dims), world=4)
     for r in range(4):
