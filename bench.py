@@ -899,6 +899,9 @@ def run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share):
         comm, comm_kind = shard.NativeComm.single(), "none (one rank)"
     elif backend == "nccl" and not share:
         comm, comm_kind = shard.NativeComm.rccl(dist), "RCCL (liblcpc_mi lcpc_comm_rccl_new, device send/recv)"
+    elif os.environ.get("LCPC_BENCH_RCCL_SAME_GPU") == "1":
+        comm, comm_kind = (shard.NativeComm.rccl(dist),
+                           "RCCL with the ranks sharing one GPU (per-rank NCCL_HOSTID: socket transport over loopback)")
     else:
         comm, comm_kind = shard.NativeComm.host(dist), "host-staged gloo collectives (ranks share one GPU)"
 
