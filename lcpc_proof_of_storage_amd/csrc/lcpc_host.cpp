@@ -129,17 +129,23 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   DBuf tmp;  // (SDIG scratch; at function scope, so that no block exit drains the stream)
   if (e->kind == KIND_SDIG) {
     // element-major codeword [n_cols][n_rows]: the message part is the coefficient matrix
-    // transposed, the SDIG levels fill the rest, and each leaf is a contiguous column
+    // transposed, the SDIG levels fill the rest, and each leaf is a contiguous column.  The
+    // codeword is held canonical: the transpose writes canonical values, and every level is a
+    // sum of Montgomery products by Montgomery constants (SpMM values, Reed-Solomon points), so
+    // canonical inputs give canonical outputs -- the leaves then hash it without a per-element
+    // conversion, as the Ligero codeword (opened columns convert back, as there)
     c->col_major = true;
+    c->canon = true;
     if (src_is_host) {
       HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb, hipMemcpyHostToDevice, s));
       if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
-      HIP_TRY(transpose_elems(fid, (const uint32_t *)cf, n_rows, np, np, np, (uint32_t *)cm, n_rows, s));
+      HIP_TRY(transpose_elems(fid, (const uint32_t *)cf, n_rows, np, np, np, (uint32_t *)cm, n_rows, s,
+                              TR_FROM_MONT));
     } else {
       // one pass over the caller's coefficients writes both the transposed message part and
       // the commitment's zero-padded row-major copy (no separate device-to-device copy)
       HIP_TRY(transpose_elems(fid, (const uint32_t *)d_src, n_rows, np, np, np, (uint32_t *)cm, n_rows, s,
-                              TR_PLAIN, nullptr, len, (uint32_t *)cf, np));
+                              TR_FROM_MONT, nullptr, len, (uint32_t *)cf, np));
     }
     HIP_TRY(tmp.alloc(dev, e->sdig.tmp_elems * n_rows * wb));
     HIP_TRY(sdig_encode_cm(e->sdig, (uint32_t *)cm, n_rows, tmp.as<uint32_t>(), s));
@@ -170,7 +176,8 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   DBuf scratch;
   HIP_TRY(scratch.alloc(dev, leaf_hash_scratch_bytes(fid, n_rows, nc)));
   if (c->col_major)
-    HIP_TRY(leaf_hashes_cols(fid, c->comm.as<uint32_t>(), n_rows, nc, c->hashes.as<uint8_t>(), scratch.p, s));
+    HIP_TRY(leaf_hashes_cols(fid, c->comm.as<uint32_t>(), n_rows, nc, c->hashes.as<uint8_t>(), scratch.p, s,
+                             c->canon));
   else
     HIP_TRY(leaf_hashes(fid, c->comm.as<uint32_t>(), n_rows, nc, nc, c->hashes.as<uint8_t>(), scratch.p, s,
                         c->canon));
@@ -546,7 +553,7 @@ static lcpc_status copy_out(const lcpc_commit *c, void *dst, const void *src, si
 }
 lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out) {
   const size_t bytes = c->n_rows * c->n_cols * field_bytes(c->fid);
-  if (c->canon) {  // canonical on the device -> the reference's Montgomery words
+  if (c->canon && !c->col_major) {  // canonical on the device -> the reference's Montgomery words
     Lease lease(c->dev);
     HIP_TRY(hipSetDevice(c->dev->id));
     DBuf mm;
@@ -564,6 +571,7 @@ lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out) {
   HIP_TRY(rm.alloc(c->dev, bytes));
   HIP_TRY(transpose_elems(c->fid, c->comm.as<uint32_t>(), c->n_cols, c->n_rows, c->n_rows, c->n_rows,
                           rm.as<uint32_t>(), c->n_cols, lease.s));
+  if (c->canon) HIP_TRY(convert(c->fid, rm.as<uint32_t>(), rm.as<uint32_t>(), c->n_rows * c->n_cols, true, lease.s));
   HIP_TRY(hipMemcpyAsync(out, rm.p, bytes, hipMemcpyDeviceToHost, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;

@@ -481,7 +481,7 @@ hipError_t transpose_elems(int fid, const uint32_t *src, size_t rows, size_t col
                            size_t copy_stride) {
   if (!rows || !cols) return hipSuccess;
   if (mode == TR_TO_MONT && !bad) return hipErrorInvalidValue;
-  if (copy && mode != TR_PLAIN) return hipErrorInvalidValue;
+  if (copy && mode == TR_TO_MONT) return hipErrorInvalidValue;  // (the copy holds the source words)
   return dispatch_field(fid, [&]<class F>() {
     prof::Scope ps("transpose", s);
     dim3 grid((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32));

@@ -362,7 +362,7 @@ struct lcpc_sharded_commit {
   lcpc_comm *comm = nullptr;
   Device *dev = nullptr;
   int fid = 1, wb = 16, G = 1, me = 0;
-  bool sdig = false;  // Brakedown: element-major shard [n_cols][nr], Montgomery codeword
+  bool sdig = false;  // Brakedown: element-major shard [n_cols][nr] (canonical codeword, as Ligero's)
   size_t n_rows = 0, np = 0, nc = 0, np2 = 0, B = 0, n_chunks = 0, nr = 0;  // np2 leaves, B = np2 / G
   std::vector<Part> part;
   hipStream_t s = nullptr;        // this polynomial's encode stream (shared, in order, by the
@@ -519,10 +519,11 @@ lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
   if (c->nr && !d_rows) return fail(LCPC_ERR_INVALID_ARG, "null rows");
   if (c->nr && c->sdig) {
     // Brakedown rows (lcpc-brakedown-pc/src/encode.rs:36-94, independent per row): this rank's
-    // rows transposed to the element-major shard [n_cols][nr] (one pass also writes the padded
-    // row-major coefficient copy), then the expander levels on those rows
+    // rows transposed to the element-major shard [n_cols][nr] as canonical values (one pass also
+    // writes the padded row-major Montgomery coefficient copy), then the expander levels on those
+    // rows -- canonical in, canonical out, as the single-GPU commit (csrc/lcpc_host.cpp)
     HIP_TRY(transpose_elems(c->fid, (const uint32_t *)d_rows, c->nr, c->np, c->np, c->np,
-                            c->comm_rows.as<uint32_t>(), c->nr, c->s, TR_PLAIN, nullptr, c->nr * c->np,
+                            c->comm_rows.as<uint32_t>(), c->nr, c->s, TR_FROM_MONT, nullptr, c->nr * c->np,
                             c->coeffs.as<uint32_t>(), c->np));
     HIP_TRY(salloc(c, c->sdig_tmp, c->e->sdig.tmp_elems * c->nr * wb + 16));
     HIP_TRY(sdig_encode_cm(c->e->sdig, c->comm_rows.as<uint32_t>(), c->nr, c->sdig_tmp.as<uint32_t>(), c->s));
@@ -532,7 +533,7 @@ lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
   }
   if (nch)  // chaining values straight into the exchange layout [dest rank][chunk][block col]
     HIP_TRY(leaf_chunk_cvs(c->fid, c->comm_rows.as<uint32_t>(), pm.r_lo, c->n_rows, c->nc, c->sdig ? 1 : c->nc,
-                           pm.c_lo, pm.c_hi, c->cv_send.as<uint32_t>(), c->s, !c->sdig, c->B,
+                           pm.c_lo, pm.c_hi, c->cv_send.as<uint32_t>(), c->s, true, c->B,
                            c->sdig ? c->nr : 1));
   HIP_TRY(hipEventRecord(c->ev_ready, c->s));
   return LCPC_OK;
@@ -795,7 +796,7 @@ lcpc_status stage_gather_cols(lcpc_sharded_commit *c) {
   HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
   if (c->nco && c->nr)
     HIP_TRY(gather_columns(c->fid, c->comm_rows.as<uint32_t>(), c->nr, c->nc, c->didx.as<uint64_t>(), c->nco,
-                           c->mycols.as<uint32_t>(), c->sp, c->sdig, !c->sdig));
+                           c->mycols.as<uint32_t>(), c->sp, c->sdig, true));
   HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
   return LCPC_OK;
 }
