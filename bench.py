@@ -332,6 +332,8 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
         # also streams its code matrices once: 16-B values + 4-B indices)
         algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B + (enc.matrix_nnz * (B + 4) if sdig else 0),
         leaf_compressions=leaf_compressions(n_rows, n_cols, B),
+        gather_bytes=(n_rows * enc.matrix_nnz * B + n_rows * (n_cols - n_per_row) * B + enc.matrix_nnz * 20
+                      + 3 * n_rows * n_per_row * B) if sdig else 0,
         traffic_key=(n, args.field, args.code),
         mul_count=(n_rows * enc.matrix_nnz if sdig else n_rows * ntt_muls(n_cols)),
         mul_model=("one product per nonzero per row" if sdig else
@@ -567,6 +569,17 @@ def roofline_objects(wl, iso, stats, args, traffic_rows_frac=1.0):
         if field == "Ft127" and ach:
             out["roofline_valu"]["mad_issue_peak"] = 20600.0 / 28
             out["roofline_valu"]["frac_of_mad_issue_peak"] = ach / (20600.0 / 28)
+    gb = getattr(wl, "gather_bytes", 0)
+    if gb and enc_ms:
+        # Brakedown: the levels gather every nonzero's input run (R rows) from HBM -- an expander
+        # has no locality for the caches to exploit -- so the traffic the encode cannot avoid is
+        # the gathers plus the transpose and the outputs, not one read of the input
+        ach = gb / (enc_ms * 1e-3) / 1e9
+        out["roofline_gather"] = {
+            "kernel": wl.enc_kernel_desc, "bound": "hbm (gathers)", "achieved": ach, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "gather_model_bytes": gb, "avg_ms": enc_ms,
+            "model": "nnz x R x B input gathers + R x (n_cols - n_per_row) x B outputs + nnz x 20 B matrix "
+                     "+ the transpose (R x n_per_row x B read, element-major and row-major copies written)"}
     lc = getattr(wl, "leaf_compressions", 0)
     if lc and "leaf_chunks" in iso:
         leaf_ms = sum(iso[k][0] / max(iso[k][1], 1) for k in ("leaf_chunks", "leaf_merge") if k in iso)
