@@ -23,7 +23,14 @@ struct NttPlan {
   int log_n = 0, l1 = 0, l2 = 0;
   uint32_t *d_tw = nullptr;        // w^e, e in [0, n): n elements (Montgomery)
   uint32_t *d_tw_canon = nullptr;  // forward plans: the same values' canonical words (below)
+  // pass A's inter-pass twiddles w^(c * bitrev_l1(t)) laid out [t][c] (t < 2^l1, c < 2^l2): the
+  // lanes of a pass-A store are adjacent columns c, so their twiddle loads are contiguous (from
+  // the flat table they were c * bitrev(t) apart, one cache line per lane); log_n > 12 only
+  uint32_t *d_tw2 = nullptr;
+  uint32_t *d_tw2_canon = nullptr;  // forward plans: canonical words
 };
+// the [t][c] table above for a pass-A split l1 from a flat table tw (n = 2^log_n elements)
+hipError_t ntt_tw2_table(int fid, const uint32_t *tw, int log_n, int l1, uint32_t *out, hipStream_t s);
 hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream_t s);
 void ntt_plan_free(NttPlan &p);
 // rows r in [0, n_rows): in = src + r * src_stride (elements), n_valid leading elements

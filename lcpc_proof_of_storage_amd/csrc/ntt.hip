@@ -15,6 +15,26 @@ DECL(ft255)
 DECL(ft253)
 #undef DECL
 
+namespace {
+// out[(t << l2) + c] = tw[c * bitrev_l1(t)]: an element copy of `words` u32 words
+__global__ __launch_bounds__(256) void k_tw2(const uint32_t *__restrict__ tw, uint32_t *__restrict__ out, int l1,
+                                             int l2, int words) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ((size_t)1 << (l1 + l2))) return;
+  const size_t t = i >> l2, c = i & (((size_t)1 << l2) - 1);
+  const size_t bt = l1 ? (size_t)(__builtin_bitreverse32((uint32_t)t) >> (32 - l1)) : 0;
+  const size_t e = c * bt;
+  for (int w = 0; w < words; w++) out[i * words + w] = tw[e * words + w];
+}
+}  // namespace
+
+hipError_t ntt_tw2_table(int fid, const uint32_t *tw, int log_n, int l1, uint32_t *out, hipStream_t s) {
+  const size_t n = (size_t)1 << log_n;
+  hipLaunchKernelGGL(k_tw2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tw, out, l1, log_n - l1,
+                     field_words(fid));
+  return hipGetLastError();
+}
+
 int field_words(int fid) {
   return dispatch_field(fid, []<class F>() { return F::N; });
 }
@@ -42,18 +62,32 @@ hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream
     case 3: e = ntt_tw_table_ft255(p.d_tw, log_n, inverse, s); break;
     default: e = ntt_tw_table_ft253(p.d_tw, log_n, inverse, s); break;
   }
-  if (e != hipSuccess || inverse) return e;
+  if (e != hipSuccess) return e;
+  if (log_n > 12) {  // the pass-A kernels' [t][c] inter-pass twiddles
+    if ((e = hipMalloc(&p.d_tw2, n * field_bytes(fid))) != hipSuccess) return e;
+    if ((e = ntt_tw2_table(fid, p.d_tw, log_n, p.l1, p.d_tw2, s)) != hipSuccess) return e;
+  }
+  if (inverse) return hipSuccess;
   // canonical words of w^e = Montgomery words of w^e R^-1 (canon_out encodes)
   e = hipMalloc(&p.d_tw_canon, n * field_bytes(fid));
   if (e != hipSuccess) return e;
-  return convert(fid, p.d_tw, p.d_tw_canon, n, false, s);
+  if ((e = convert(fid, p.d_tw, p.d_tw_canon, n, false, s)) != hipSuccess) return e;
+  if (log_n > 12) {
+    if ((e = hipMalloc(&p.d_tw2_canon, n * field_bytes(fid))) != hipSuccess) return e;
+    if ((e = ntt_tw2_table(fid, p.d_tw_canon, log_n, p.l1, p.d_tw2_canon, s)) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 void ntt_plan_free(NttPlan &p) {
   if (p.d_tw) (void)hipFree(p.d_tw);
   if (p.d_tw_canon) (void)hipFree(p.d_tw_canon);
+  if (p.d_tw2) (void)hipFree(p.d_tw2);
+  if (p.d_tw2_canon) (void)hipFree(p.d_tw2_canon);
   p.d_tw = nullptr;
   p.d_tw_canon = nullptr;
+  p.d_tw2 = nullptr;
+  p.d_tw2_canon = nullptr;
 }
 
 hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,

@@ -137,6 +137,7 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
                       size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
   if (n_rows == 0) return hipSuccess;
   if (canon && !p.d_tw_canon) return hipErrorInvalidValue;
+  if (p.log_n > 12 && !(canon ? p.d_tw2_canon : p.d_tw2)) return hipErrorInvalidValue;
   if (p.log_n == 0) {  // length-1 transform is the identity (fffft returns early)
     if (cp && nv) {
       hipError_t e = hipMemcpy2DAsync(cp, cs * F::N * 4, src, ss * F::N * 4, F::N * 4, n_rows,
@@ -162,14 +163,15 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
   constexpr int HI = F::N >= 8 ? 11 : 12;  // LDS budget of 32-byte fields
   auto pass_a = [&]<int L, int CW>() {
     constexpr int T = L + CW - R;
-    const uint32_t *tc = p.d_tw_canon;
+    // the inter-pass twiddles in [t][c] layout (canonical words for canon_out)
+    const uint32_t *t2 = canon ? p.d_tw2_canon : p.d_tw2;
     if (halfz && canon)
-      return ntt_v2::launch_a<F, L, CW, T, true, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, tc);
+      return ntt_v2::launch_a<F, L, CW, T, true, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, t2);
     if (halfz)
-      return ntt_v2::launch_a<F, L, CW, T, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs);
+      return ntt_v2::launch_a<F, L, CW, T, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, t2);
     if (canon)
-      return ntt_v2::launch_a<F, L, CW, T, false, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, tc);
-    return ntt_v2::launch_a<F, L, CW, T, false>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs);
+      return ntt_v2::launch_a<F, L, CW, T, false, true>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, t2);
+    return ntt_v2::launch_a<F, L, CW, T, false>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, t2);
   };
   hipError_t e;
   if constexpr (F::ID == 0) {

@@ -115,16 +115,18 @@ constexpr int last_s0() {  // first stage of the last round
   return s0;
 }
 
-// CANON: the inter-pass multiplier is w^e R^-1 (twc: the canonical words of w^e), applied to
-// every element including e = 0, so the whole transform comes out scaled by R^-1 -- i.e. in
-// canonical form (see ntt_rows' canon_out).
+// CANON: the inter-pass multiplier is w^e R^-1 (the canonical words of w^e), applied to every
+// element including e = 0, so the whole transform comes out scaled by R^-1 -- i.e. in canonical
+// form (see ntt_rows' canon_out).  tw2: the inter-pass twiddles w^(c bitrev(t)) laid out [t][c]
+// (NttPlan::d_tw2 / d_tw2_canon), so the lanes of a store (adjacent columns c) load adjacent
+// twiddles.
 template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ, bool CANON>
 __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restrict__ src,
                                                        size_t src_stride, size_t n_valid,
                                                        uint32_t *__restrict__ dst,
                                                        size_t dst_stride,
                                                        const uint32_t *__restrict__ twn,
-                                                       const uint32_t *__restrict__ twc,
+                                                       const uint32_t *__restrict__ tw2,
                                                        int log_n, uint32_t *__restrict__ copy,
                                                        size_t copy_stride) {
   constexpr int S = 1 << LOG_S, CW = 1 << LOG_CW, LD = CW > 1 ? CW + 1 : 1, T = 1 << LOG_T;
@@ -172,13 +174,10 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
 #pragma unroll
       for (int j = 0; j < K; j++) {
         const int t = q + j * GL;  // GL == 1 here
-        const size_t e = c * (size_t)brev(t, LOG_S);
+        const size_t at = c + ((size_t)t << log_m);  // (also the [t][c] twiddle's index)
         Fe<F> y = x[j];
-        if (CANON)
-          y = NTT_MUL<F>(y, fe_load<F>(twc, e));
-        else if (e)
-          y = NTT_MUL<F>(y, fe_load<F>(twn, e));
-        fe_store<F>(out, c + ((size_t)t << log_m), y);
+        if (CANON || (c && t)) y = NTT_MUL<F>(y, fe_load<F>(tw2, at));  // (w^0 = 1 otherwise)
+        fe_store<F>(out, at, y);
       }
       return;
     } else {
@@ -204,13 +203,10 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
 #pragma unroll
       for (int j = 0; j < K; j++) {
         const int t = b + j;
-        const size_t e = c * (size_t)brev(t, LOG_S);
+        const size_t at = c + ((size_t)t << log_m);  // (also the [t][c] twiddle's index)
         Fe<F> y = x[j];
-        if (CANON)
-          y = NTT_MUL<F>(y, fe_load<F>(twc, e));
-        else if (e)
-          y = NTT_MUL<F>(y, fe_load<F>(twn, e));
-        fe_store<F>(out, c + ((size_t)t << log_m), y);
+        if (CANON || (c && t)) y = NTT_MUL<F>(y, fe_load<F>(tw2, at));  // (w^0 = 1 otherwise)
+        fe_store<F>(out, at, y);
       }
     }
   }
@@ -261,11 +257,11 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_b(uint32_t *__restrict__ da
 template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ, bool CANON = false>
 hipError_t launch_a(const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                     const uint32_t *tw, int log_n, size_t n_rows, hipStream_t s, uint32_t *cp,
-                    size_t cs, const uint32_t *twc = nullptr) {
+                    size_t cs, const uint32_t *tw2) {
   const size_t groups = (size_t)1 << (log_n - LOG_S - LOG_CW);
   prof::Scope ps("ntt_pass_a", s);
   hipLaunchKernelGGL((k_pass_a<F, LOG_S, LOG_CW, LOG_T, HALFZ, CANON>), dim3((unsigned)(n_rows * groups)),
-                     dim3(1 << LOG_T), 0, s, src, ss, nv, dst, ds, tw, twc, log_n, cp, cs);
+                     dim3(1 << LOG_T), 0, s, src, ss, nv, dst, ds, tw, tw2, log_n, cp, cs);
   return hipGetLastError();
 }
 

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -51,10 +52,31 @@ void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
   hipLaunchKernelGGL(k_fill<F>, dim3((rows * np * W + 255) / 256), dim3(256), 0, 0, coeffs, rows * np * W, 12345u);
   hipLaunchKernelGGL((ntt_detail::k_tw_table<F>), dim3((n + 255) / 256), dim3(256), 0, 0, tw, log_n, 0);
   CK(hipDeviceSynchronize());
-  NttPlan plan;
-  plan.fid = F::ID; plan.log_n = log_n; plan.l1 = log_n / 2; plan.l2 = log_n - plan.l1; plan.d_tw = tw;
   hipStream_t s;
   CK(hipStreamCreate(&s));
+  // pass A's [t][c] inter-pass twiddles, one table per pass-A split
+  std::map<int, uint32_t *> tw2s;
+  auto tw2_for = [&](int l1) {
+    uint32_t *&t2 = tw2s[l1];
+    if (!t2) {
+      // (the same permutation as ntt.hip's ntt_tw2_table, done on the host here)
+      std::vector<uint32_t> h(n * W), h2(n * W);
+      CK(hipMemcpy(h.data(), tw, n * W * 4, hipMemcpyDeviceToHost));
+      const int l2 = log_n - l1;
+      for (size_t t = 0; t < ((size_t)1 << l1); t++) {
+        size_t bt = 0;
+        for (int b = 0; b < l1; b++) bt |= ((t >> b) & 1) << (l1 - 1 - b);
+        for (size_t c = 0; c < ((size_t)1 << l2); c++)
+          std::memcpy(&h2[((t << l2) + c) * W], &h[c * bt * W], W * 4);
+      }
+      CK(hipMalloc(&t2, n * W * 4));
+      CK(hipMemcpy(t2, h2.data(), n * W * 4, hipMemcpyHostToDevice));
+    }
+    return t2;
+  };
+  NttPlan plan;
+  plan.fid = F::ID; plan.log_n = log_n; plan.l1 = log_n / 2; plan.l2 = log_n - plan.l1; plan.d_tw = tw;
+  plan.d_tw2 = tw2_for(plan.l1);
   CK(ntt_detail::ntt_rows_t<F>(plan, coeffs, np, np, ref, n, rows, s, nullptr, 0, false));
   CK(hipStreamSynchronize(s));
 
@@ -65,7 +87,8 @@ void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
 #define V2(LA, CWA, TA, LB, CWB, TB)                                                           \
   vs.push_back({"v2 A(S=2^" #LA ",CW=2^" #CWA ",T=2^" #TA ") B(S=2^" #LB ",CW=2^" #CWB ",T=2^" #TB ")", \
                 [&](const uint32_t *c, uint32_t *o, hipStream_t st) {                          \
-                  CK((ntt_v2::launch_a<F, LA, CWA, TA, true>(c, np, np, o, n, tw, log_n, rows, st, cpy, np))); \
+                  CK((ntt_v2::launch_a<F, LA, CWA, TA, true>(c, np, np, o, n, tw, log_n, rows, st, cpy, np,  \
+                                                             tw2_for(LA))));                    \
                   CK((ntt_v2::launch_b<F, LB, CWB, TB>(o, n, tw, log_n, rows, st)));           \
                 }});
   if constexpr (F::ID == 1) {
