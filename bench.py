@@ -523,9 +523,14 @@ def roofline_objects(wl, iso, stats, args, traffic_rows_frac=1.0):
     out = {}
     if not iso or not wl.algo_bytes:
         return out
-    ki = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in iso.items()}
+    # iso holds (total ms, launches) over args.roofline_steps serial steps.  The roofline time is
+    # the encode's kernel time PER STEP: a step may launch a kernel more than once (the PoS file's
+    # ragged last row is its own one-row NTT), so a per-launch average would mix a one-row launch
+    # with the full-size one
+    nst = max(args.roofline_steps, 1)
+    ki = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "ms_per_step": v[0] / nst} for k, v in iso.items()}
     out["kernels"] = ki
-    enc_ms = sum(ki[k]["avg_ms"] for k in wl.enc_kernels if k in ki)
+    enc_ms = sum(ki[k]["ms_per_step"] for k in wl.enc_kernels if k in ki)
     traffic, tsrc = None, None
     for tpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
         try:
@@ -548,8 +553,9 @@ def roofline_objects(wl, iso, stats, args, traffic_rows_frac=1.0):
         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic, "traffic_source": tsrc,
         "algorithmic_bytes": wl.algo_bytes, "avg_ms": enc_ms,
         "launches": min((ki[k]["launches"] for k in wl.enc_kernels if k in ki), default=0),
+        "launches_per_step": {k: ki[k]["launches"] / nst for k in wl.enc_kernels if k in ki},
         "measured": f"HIP events on the launching stream, {args.roofline_steps} serial steps after the timed "
-                    f"region (same process, inputs and kernels)",
+                    f"region (same process, inputs and kernels); avg_ms = the encode kernels' time per step",
         "timed_region_avg_ms": tr_ms,
     }
     if wl.mul_count:
@@ -582,7 +588,7 @@ def roofline_objects(wl, iso, stats, args, traffic_rows_frac=1.0):
                      "+ the transpose (R x n_per_row x B read, element-major and row-major copies written)"}
     lc = getattr(wl, "leaf_compressions", 0)
     if lc and "leaf_chunks" in iso:
-        leaf_ms = sum(iso[k][0] / max(iso[k][1], 1) for k in ("leaf_chunks", "leaf_merge") if k in iso)
+        leaf_ms = sum(iso[k][0] / nst for k in ("leaf_chunks", "leaf_merge") if k in iso)
         ach = lc / (leaf_ms * 1e-3) / 1e9
         out["roofline_leaf"] = {
             "kernel": "leaf_chunks + leaf_merge (BLAKE3 column leaves)", "bound": "valu (BLAKE3 compressions)",

@@ -22,7 +22,8 @@ KERNELS = {"ntt_pass_a": "k_pass_a", "ntt_pass_b": "k_pass_b", "leaf_chunks": "k
            "collapse_partial": "k_collapse_partial", "collapse_mfma": "k_collapse_mfma",
            # Brakedown (--code sdig): the transpose into element-major form, the SpMM levels
            # (matrix-core or VALU kernel) and the Reed-Solomon base
-           "transpose": "k_transpose", "spmm": "k_spmm", "reed_solomon": "k_reed_solomon"}
+           "transpose": "k_transpose", "spmm": "k_spmm", "reed_solomon": "k_reed_solomon",
+           "pos_pack7": "k_pack7"}
 SDIG_ENCODE = ("transpose", "spmm", "reed_solomon")
 
 
@@ -56,17 +57,24 @@ def main():
         wr = write.get(k, 0.0)
         kern[k] = {"fetch_bytes_raw": fetch[k], "read_bytes_corrected": rd, "write_bytes": wr,
                    "hbm_bytes": rd + wr, "launches": nf[k]}
+    # per step (one commitment), not per launch: total over the run / the launches of a kernel that
+    # runs once per step.  A PoS step encodes the file's ragged last row with a one-row NTT of its
+    # own, so its NTT kernels launch twice per step and a per-launch mean would halve the figure.
     if a.code == "sdig":
-        # one encode = one transpose + every SpMM level + the R-S base: total over the run / encodes
+        # one encode = one transpose + every SpMM level + the R-S base
         n_enc = nf["transpose"]
         enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in SDIG_ENCODE) / n_enc
     else:
-        enc = kern["ntt_pass_a"]["hbm_bytes"] + kern["ntt_pass_b"]["hbm_bytes"]
+        n_enc = nf["pos_pack7"] if a.code == "pos" else nf["leaf_chunks"]
+        enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in ("ntt_pass_a", "ntt_pass_b")) / n_enc
+    for k in kern:
+        kern[k]["hbm_bytes_per_step"] = (2.0 * ftot[k] + wtot.get(k, 0.0)) / n_enc
     out = {
         "config_len": a.len, "field": a.field, "code": a.code,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
                   "(bench.py --pipeline 1); FETCH_SIZE x2 (gfx950 wide-read correction), KiB -> B",
-        "ntt_encode_bytes_per_launch": enc,
+        "ntt_encode_bytes_per_launch": enc,  # (per step: every encode launch of one commitment)
+        "steps": n_enc,
         "kernels": kern,
         "source": os.path.relpath(a.run_dir),
     }
