@@ -412,7 +412,10 @@ def pos_workload(args, L, torch, rank, local_rank):
     host = rng.integers(0, 256, n_bytes, dtype=np.uint8)
     dev = f"cuda:{local_rank}"
     d_bytes = torch.from_numpy(host).to(dev)
-    slots = [torch.empty(n_el, dtype=torch.int64, device=dev) for _ in range(max(1, args.pipeline))]
+    # element buffers of whole-row capacity whose tail past n_el stays zero: commit pads the last
+    # row with zeros (lcpc-2d/src/lib.rs:665-674), so committing the n_rows x n_per_row buffer is
+    # the same commitment, and the ragged row needs no separate one-row encode
+    slots = [torch.zeros(n_rows * np_, dtype=torch.int64, device=dev) for _ in range(max(1, args.pipeline))]
     x = L.field_random(L.FT63, 1, 1337)
     left, _ = P.form_side_vectors_for_polynomial_evaluation_from_point(x, n_rows, nc)
     cols = P.get_column_indicies_from_random_seed(1337, 256, nc)
@@ -429,7 +432,7 @@ def pos_workload(args, L, torch, rank, local_rank):
             rc = lib.lcpc_pos_bytes_to_field_device(d_bytes.data_ptr(), n_bytes, d_el.data_ptr(), None)
             if rc:
                 raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
-            c = L.LcCommit.commit_device(d_el.data_ptr(), n_el, enc)
+            c = L.LcCommit.commit_device(d_el.data_ptr(), n_rows * np_, enc)
         finally:
             if gate is not None:
                 gate.release()

@@ -399,29 +399,82 @@ __global__ __launch_bounds__(256) void k_leaf_chunks_words(const uint32_t *__res
   }
 }
 
-// Fold n_chunks chaining values of each column into its BLAKE3 root (in place in cvs).
-__global__ __launch_bounds__(256) void k_leaf_merge(uint32_t *__restrict__ cvs, size_t n_cols,
-                                                    int n_chunks, uint8_t *__restrict__ leaves) {
-  const size_t col = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= n_cols) return;
-  int nodes = n_chunks;
-  uint32_t l[8], r[8], o[8];
+// Fold `count` chaining values of column col -- chunk slots first, first + stride, ... of the
+// [chunk][col] scratch -- pairwise per level, an odd node carried up (BLAKE3's left-balanced tree
+// over those chunks), in place; the result lands in slot `first`.  ROOT marks the last parent when
+// this fold is the whole tree.
+__device__ __forceinline__ void fold_cvs(uint32_t *__restrict__ cvs, size_t n_cols, size_t col, int first,
+                                         int count, int stride, bool root, uint32_t o[8]) {
+  int nodes = count;
+  uint32_t l[8], r[8];
+  auto slot = [&](int i) { return cvs + ((size_t)(first + i * stride) * n_cols + col) * 8; };
   while (nodes > 1) {
     const int pairs = nodes / 2;
     for (int i = 0; i < pairs; i++) {
-      load8(cvs + ((size_t)(2 * i) * n_cols + col) * 8, l);
-      load8(cvs + ((size_t)(2 * i + 1) * n_cols + col) * 8, r);
-      parent_cv(l, r, nodes == 2, o);
-      store8(cvs + ((size_t)i * n_cols + col) * 8, o);
+      load8(slot(2 * i), l);
+      load8(slot(2 * i + 1), r);
+      parent_cv(l, r, root && nodes == 2, o);
+      store8(slot(i), o);
     }
     if (nodes & 1) {
-      load8(cvs + ((size_t)(nodes - 1) * n_cols + col) * 8, l);
-      store8(cvs + ((size_t)pairs * n_cols + col) * 8, l);
+      load8(slot(nodes - 1), l);
+      store8(slot(pairs), l);
     }
     nodes = pairs + (nodes & 1);
   }
-  load8(cvs + col * 8, o);
+  load8(slot(0), o);
+}
+
+// Chunk groups of the leaf merge: groups of MERGE_GROUP consecutive chunks, aligned, are whole
+// subtrees of the pairwise fold (an aligned block of 2^k nodes pairs only within itself for k
+// levels, and a ragged last group's own pairwise fold is the node the whole-tree fold carries up),
+// so the fold runs in two passes: every group in parallel, then each column's group nodes.
+constexpr int MERGE_GROUP = 8;
+
+// pass 1: one thread per (column, group); the group's node goes to its first chunk slot, or --
+// when one group is the whole tree -- the column's leaf
+__global__ __launch_bounds__(256) void k_leaf_merge_groups(uint32_t *__restrict__ cvs, size_t n_cols,
+                                                           int n_chunks, uint8_t *__restrict__ leaves) {
+  const size_t col = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  if (col >= n_cols) return;
+  const int first = g * MERGE_GROUP;
+  const int count = n_chunks - first < MERGE_GROUP ? n_chunks - first : MERGE_GROUP;
+  const bool whole = n_chunks <= MERGE_GROUP;
+  uint32_t o[8];
+  fold_cvs(cvs, n_cols, col, first, count, 1, whole, o);
+  if (whole) store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), o);
+}
+
+// one thread per column folds its `count` nodes (slots 0, stride, 2 stride, ...) into the leaf:
+// the group nodes after pass 1 (stride MERGE_GROUP), or every chunk (stride 1)
+__global__ __launch_bounds__(256) void k_leaf_merge(uint32_t *__restrict__ cvs, size_t n_cols, int count,
+                                                    int stride, uint8_t *__restrict__ leaves) {
+  const size_t col = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= n_cols) return;
+  uint32_t o[8];
+  fold_cvs(cvs, n_cols, col, 0, count, stride, true, o);
   store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), o);
+}
+
+// Up to 2 groups (16 chunks, e.g. cfg3's 9) one serial fold per column is as short as the two
+// passes and saves a launch (measured: 256-thread blocks 21.5 us at cfg3, 64-thread 29 us); longer
+// leaves (PoS: 74 chunks, 0.16 -> 0.09 ms) fold in two passes of 64-thread blocks, so pass 2's
+// one thread per column still spreads over every SIMD.
+hipError_t launch_leaf_merge(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t *leaves, hipStream_t s) {
+  prof::Scope ps("leaf_merge", s);
+  const unsigned bx = (unsigned)((n_cols + 63) / 64);
+  const int n_groups = (n_chunks + MERGE_GROUP - 1) / MERGE_GROUP;
+  if (n_groups <= 2) {
+    hipLaunchKernelGGL(k_leaf_merge, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, s, cvs, n_cols, n_chunks,
+                       1, leaves);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_leaf_merge_groups, dim3(bx, (unsigned)n_groups), dim3(64), 0, s, cvs, n_cols, n_chunks,
+                     leaves);
+  hipLaunchKernelGGL(k_leaf_merge, dim3(bx), dim3(64), 0, s, cvs, n_cols, (n_chunks + MERGE_GROUP - 1) / MERGE_GROUP,
+                     MERGE_GROUP, leaves);
+  return hipGetLastError();
 }
 
 // Merkle levels: each workgroup folds 2^levels consecutive nodes of level `lvl` (starting at
@@ -566,10 +619,7 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
     }
   });
   if (e != hipSuccess || n_chunks == 1) return e;
-  prof::Scope ps("leaf_merge", s);
-  hipLaunchKernelGGL(k_leaf_merge, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, s,
-                     (uint32_t *)scratch, n_cols, n_chunks, leaves);
-  return hipGetLastError();
+  return launch_leaf_merge((uint32_t *)scratch, n_cols, n_chunks, leaves, s);
 }
 
 size_t leaf_n_chunks(int fid, size_t n_rows) {
@@ -613,10 +663,7 @@ hipError_t leaves_from_cvs(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t *
                            hipStream_t s) {
   if (!n_cols) return hipSuccess;
   if (n_chunks == 1) return hipMemcpyAsync(leaves, cvs, n_cols * 32, hipMemcpyDeviceToDevice, s);
-  prof::Scope ps("leaf_merge", s);
-  hipLaunchKernelGGL(k_leaf_merge, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, s, cvs, n_cols,
-                     n_chunks, leaves);
-  return hipGetLastError();
+  return launch_leaf_merge(cvs, n_cols, n_chunks, leaves, s);
 }
 
 hipError_t leaf_hashes(int fid, const uint32_t *m, size_t n_rows, size_t n_cols, size_t stride,

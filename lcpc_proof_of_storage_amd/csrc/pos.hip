@@ -11,8 +11,8 @@
 // verifiable_polynomial_evaluation (lcpc_online.rs:454-484) is collapse_rows over the encoded
 // matrix (collapse.hip).
 //
-// Byte kernels move 8 elements (56 bytes = 7 aligned u64) per thread, so loads and stores are
-// 8-byte vectors over a contiguous 3.5-KiB run per wave.
+// Byte kernels move 8 elements (56 bytes = 7 aligned u64) per thread; k_pack7 stages a block's
+// bytes and elements through LDS so its global loads and stores are coalesced 16-byte vectors.
 #include "field.hpp"
 #include "kernels.hpp"
 #include "pos.hpp"
@@ -22,9 +22,44 @@ namespace lcpc {
 
 namespace {
 
+// element k = bits [56k, 56k + 56) of the 448-bit little-endian run q
+__device__ __forceinline__ uint64_t pack7_elem(const uint64_t q[7], int k) {
+  const int bit = 56 * k, wi = bit >> 6, sh = bit & 63;
+  uint64_t v = q[wi] >> sh;
+  if (sh > 8 && wi + 1 < 7) v |= q[wi + 1] << (64 - sh);
+  return v & 0x00ffffffffffffffull;
+}
+
+// A block packs 2048 elements (14336 bytes): the bytes come in as coalesced 16-byte loads into
+// LDS, each thread unpacks its 56-byte run from there, and the 16 KiB of elements go out through
+// LDS again as coalesced 16-byte stores (a lane's 7 and 8 u64 accesses straight to memory are
+// 56 and 64 bytes apart across the wave).  A partial last block takes the per-thread path.
+constexpr int PACK_EL = 2048, PACK_BYTES = 7 * PACK_EL;
 __global__ __launch_bounds__(256) void k_pack7(const uint8_t *__restrict__ bytes, size_t n_bytes,
                                                uint64_t *__restrict__ out, size_t n_elems) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ __align__(16) uint64_t s_in[PACK_BYTES / 8];
+  __shared__ __align__(16) uint64_t s_out[PACK_EL];
+  const int tid = threadIdx.x;
+  const size_t eb = (size_t)blockIdx.x * PACK_EL, bb = (size_t)blockIdx.x * PACK_BYTES;
+  if (eb + PACK_EL <= n_elems && bb + PACK_BYTES <= n_bytes) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(bytes + bb);  // 16-byte aligned
+    uint4 *si = reinterpret_cast<uint4 *>(s_in);
+#pragma unroll
+    for (int i = tid; i < PACK_BYTES / 16; i += 256) si[i] = src[i];
+    __syncthreads();
+    uint64_t q[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) q[i] = s_in[7 * tid + i];
+#pragma unroll
+    for (int k = 0; k < 8; k++) s_out[8 * tid + k] = pack7_elem(q, k);
+    __syncthreads();
+    uint4 *dst = reinterpret_cast<uint4 *>(out + eb);
+    const uint4 *so = reinterpret_cast<const uint4 *>(s_out);
+#pragma unroll
+    for (int i = tid; i < PACK_EL / 2; i += 256) dst[i] = so[i];
+    return;
+  }
+  const size_t t = (size_t)blockIdx.x * PACK_EL / 8 + tid;
   const size_t e0 = 8 * t;
   if (e0 >= n_elems) return;
   const size_t b0 = 56 * t;
@@ -33,14 +68,8 @@ __global__ __launch_bounds__(256) void k_pack7(const uint8_t *__restrict__ bytes
     uint64_t q[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) q[i] = w[i];
-    // element k = bits [56k, 56k + 56) of the 448-bit little-endian run q
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int bit = 56 * k, wi = bit >> 6, sh = bit & 63;
-      uint64_t v = q[wi] >> sh;
-      if (sh > 8 && wi + 1 < 7) v |= q[wi + 1] << (64 - sh);
-      out[e0 + k] = v & 0x00ffffffffffffffull;
-    }
+    for (int k = 0; k < 8; k++) out[e0 + k] = pack7_elem(q, k);
   } else {
     for (size_t e = e0; e < e0 + 8 && e < n_elems; e++) {
       uint64_t v = 0;
@@ -110,9 +139,8 @@ __global__ __launch_bounds__(256) void k_powers(const uint32_t *__restrict__ bas
 hipError_t pos_pack7(const uint8_t *bytes, size_t n_bytes, uint64_t *out, hipStream_t s) {
   const size_t n = (n_bytes + 6) / 7;
   if (!n) return hipSuccess;
-  const size_t threads = (n + 7) / 8;
   prof::Scope ps("pos_pack7", s);
-  hipLaunchKernelGGL(k_pack7, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, bytes, n_bytes,
+  hipLaunchKernelGGL(k_pack7, dim3((unsigned)((n + PACK_EL - 1) / PACK_EL)), dim3(256), 0, s, bytes, n_bytes,
                      out, n);
   return hipGetLastError();
 }

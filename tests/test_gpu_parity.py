@@ -120,6 +120,17 @@ def test_commit_matches_oracle(gpu, oracle, fid, n_per_row, n_cols, length):
     assert g.get_root() == o.root()
 
 
+@pytest.mark.parametrize("n_rows", [1000, 1100, 2040, 2100, 8180, 8300, 8400])
+def test_leaf_merge_chunk_counts(gpu, oracle, n_rows):
+    """Column leaves of 8, 9, 16, 17, 65 and 65 chunks (Ft63: 32 + 8 n_rows bytes): the chaining
+    values fold in aligned groups of 8 chunks, then across groups (blake3.hip k_leaf_merge_groups,
+    k_leaf_merge) -- whole groups, a ragged last group, a last group of one chunk, one group only."""
+    coeffs, g_enc, o_enc, g, o = _commit_both(gpu, oracle, 0, 4, 8, 4 * n_rows, 5)
+    assert g.get_n_rows() == n_rows
+    assert g.hashes == o.hashes
+    assert g.get_root() == o.root()
+
+
 def test_commit_empty_and_oversized_inputs(gpu, oracle):
     """commit's shape asserts (lcpc-2d/src/lib.rs:659-661) are LcpcError here, not a panic: an
     empty polynomial has no rows ((n_rows - 1) underflows in the reference); a device commit of
