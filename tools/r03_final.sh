@@ -18,4 +18,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   $T 120 rocprofv3 --pmc "$c" -d "$OUT/pmc_$n" -o run --output-format csv -- \
     python3 bench.py --steps 2 --warmup 1 --pipeline 1 --cpu-baseline off --no-prof --verify-reps 0 --sharded-n1 0 > /dev/null 2> "$OUT/pmc_$n.err"
 done
+$T 300 python bench.py --code pos --pipeline 2 --steps 16 --warmup 4 > $OUT/bench_pos.json 2> $OUT/bench_pos.err
+$T 300 python bench.py --code sdig --steps 20 --warmup 5 > $OUT/bench_sdig.json 2> $OUT/bench_sdig.err
 echo ok
