@@ -368,7 +368,7 @@ struct lcpc_sharded_commit {
   hipStream_t s = nullptr;        // this polynomial's encode stream (shared, in order, by the
                                   // pipelined driver's polynomials: encodes finish first come first)
   bool own_s = true;              // s is this polynomial's own (released with it)
-  hipStream_t sp = nullptr;       // its prove stream (high priority: short latency-critical kernels)
+  hipStream_t sp = nullptr;       // its exchange-side and prove stream (short kernels, beside the encodes)
   hipEvent_t ev_ready = nullptr;  // send data of the next exchange written
   hipEvent_t ev_done = nullptr;   // the last exchange completed (comm stream)
   hipEvent_t ev_host = nullptr;   // device -> host copies of the last stage landed
@@ -397,14 +397,25 @@ struct lcpc_sharded_commit {
 
 namespace {
 
-// LCPC_SHARD_PRIO=0: the prove stages share the commit stream (A/B runs)
-bool shard_prio_streams() {
-  static const bool v = [] {
+// Each polynomial's exchange-side and prove kernels run on a stream of their own beside the
+// shared in-order encode stream (LCPC_SHARD_PRIO=0: on the encode stream itself, A/B runs).
+// That stream has the encode stream's priority: with a high-priority one (LCPC_SHARD_PRIO=2, kept
+// for A/B runs only) eight ranks sharing one GPU produced a wrong commitment root for one of the
+// later polynomials in about one run in four (tests/test_gpu_shard_native.py
+// ::test_native_pipeline_world8_rccl_one_gpu: every rank's subtrees of that polynomial wrong,
+// with its recommitment on one GPU right), against 0 in 16 runs with every stream at one priority
+// or the prove work on the encode stream.  The ordering between the three streams rests on
+// cross-stream event waits alone; the cause under mixed priorities was not isolated further, so
+// the driver keeps to one priority.
+int shard_prove_stream_mode() {
+  static const int v = [] {
     const char *e = getenv("LCPC_SHARD_PRIO");
-    return !(e && e[0] == '0');
+    return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
   }();
   return v;
 }
+bool shard_prio_streams() { return shard_prove_stream_mode() != 0; }
+bool shard_prove_high() { return shard_prove_stream_mode() == 2; }
 
 struct ShardDeleter {
   void operator()(lcpc_sharded_commit *c) const {
@@ -423,7 +434,7 @@ struct ShardDeleter {
       b->settle();
     delete c;
     if (s) d->release_stream(s, false);
-    if (sp) d->release_stream(sp, true);
+    if (sp) d->release_stream(sp, shard_prove_high());
   }
 };
 using ShardPtr = std::unique_ptr<lcpc_sharded_commit, ShardDeleter>;
@@ -485,7 +496,7 @@ lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, S
   c->own_s = bulk == nullptr;
   c->s = bulk ? bulk : c->dev->acquire_stream(false);
   if (!c->s) return fail(LCPC_ERR_DEVICE, "no HIP stream");
-  c->sp = shard_prio_streams() ? c->dev->acquire_stream(true) : c->s;
+  c->sp = shard_prio_streams() ? c->dev->acquire_stream(shard_prove_high()) : c->s;
   if (!c->sp) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   HIP_TRY(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
@@ -1303,7 +1314,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   // every polynomial's encode goes on one stream, issued in polynomial order by one thread: the
   // encodes finish first come first (on streams of their own they ran side by side and each
   // commitment's root arrived late), while the short exchange-side and prove kernels run on each
-  // polynomial's priority stream
+  // polynomial's own (prove) stream
   TaskPool encoder(1, e->dev->id);
   hipStream_t bulk = e->dev->acquire_stream(false);
   if (!bulk) return fail(LCPC_ERR_DEVICE, "no HIP stream");
@@ -1542,12 +1553,12 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
   std::vector<hipStream_t> lo, hi;
   for (size_t k = 0; k < depth; k++) {
     lo.push_back(dev->acquire_stream(false));
-    if (shard_prio_streams()) hi.push_back(dev->acquire_stream(true));
+    if (shard_prio_streams()) hi.push_back(dev->acquire_stream(shard_prove_high()));
   }
   for (hipStream_t x : lo)
     if (x) dev->release_stream(x, false);
   for (hipStream_t x : hi)
-    if (x) dev->release_stream(x, true);
+    if (x) dev->release_stream(x, shard_prove_high());
   return st;
 }
 

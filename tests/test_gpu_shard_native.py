@@ -140,8 +140,21 @@ def _run_many(L, hipmem, comm, fid, n, n_polys=5, lag=0, dims=None):
             return _transcript(L, root, nco)
 
         roots, proofs = shard.sharded_commit_prove_many(enc, comm, ptrs, n_rows, outer, make_tr, lag=lag)
-        res = dict(roots=all(r == s.get_root() for r, s in zip(roots, singles)),
+        bad = [i for i, (r, s) in enumerate(zip(roots, singles)) if r != s.get_root()]
+        res = dict(roots=not bad,
                    transcript_ranks=sorted(seen) == [i for i in range(n_polys) if i % comm.world == comm.rank])
+        if bad:
+            # which side is wrong: commit the polynomial again on one GPU
+            again = [L.LcCommit.commit(polys[i], enc).get_root() for i in bad]
+            res["bad_root_polys"] = [(i, a == roots[i], a == singles[i].get_root()) for i, a in zip(bad, again)]
+            # (diagnostic) the single commitment's subtree roots at the ranks' block level
+            G = comm.world
+            np2 = len(singles[0].hashes) // 32 // 2 + 1
+            for i in bad:
+                h = singles[i].hashes
+                off = 2 * np2 - 2 * G
+                res.setdefault("want", []).append((i, roots[i][:4].hex(), singles[i].get_root()[:4].hex(),
+                                                   [h[32 * (off + g):32 * (off + g) + 4].hex() for g in range(G)]))
         ok = True
         for i, (pf, s) in enumerate(zip(proofs, singles)):
             if i % comm.world != comm.rank:
@@ -286,6 +299,17 @@ def test_native_sharded_world4_rccl_one_gpu(gpu):
 
 
 @pytest.mark.timeout(300)
+def test_native_pipeline_world8_rccl_one_gpu(gpu):
+    """the N = 8 exchange groups through RCCL: eight ranks on the one GPU, the pipelined driver on
+    2^22 Ft127 (256 rows, 5 leaf chunks: three ranks own no rows), transcripts on ranks i % 8"""
+    res = _spawn("many_rccl", (1, 1 << 22, 9, 0), world=8)
+    bad = {r: res[r] for r in range(8) if "error" in res[r] or not all(res[r].values())}
+    for r, v in bad.items():
+        print("rank", r, v)
+    assert not bad, bad
+
+
+@pytest.mark.timeout(300)
 def test_native_pipeline_world2_one_gpu(gpu):
     res = _spawn("many", (1, 1 << 14, 6, 2))
     for r in (0, 1):
@@ -365,4 +389,14 @@ def _full_size(L, hipmem, comm):
 def test_native_sharded_cfg3_full_size_world2(gpu):
     res = _spawn("full", (), timeout=560)
     for r in (0, 1):
+        assert "error" not in res[r] and all(res[r].values()), (r, res[r])
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+def test_native_sharded_cfg3_full_size_world8_rccl_one_gpu(gpu):
+    """cfg3 at the driver's N = 8 (512 rows: 62-66 rows and one or two leaf chunks per rank)
+    through RCCL, the eight ranks on the one GPU: root, tree and proof against the oracle"""
+    res = _spawn("full_rccl", (), timeout=560, world=8)
+    for r in range(8):
         assert "error" not in res[r] and all(res[r].values()), (r, res[r])
