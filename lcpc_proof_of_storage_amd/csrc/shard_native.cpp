@@ -398,24 +398,28 @@ struct lcpc_sharded_commit {
 namespace {
 
 // Each polynomial's exchange-side and prove kernels run on a stream of their own beside the
-// shared in-order encode stream (LCPC_SHARD_PRIO=0: on the encode stream itself, A/B runs).
-// That stream has the encode stream's priority: with a high-priority one (LCPC_SHARD_PRIO=2, kept
-// for A/B runs only) eight ranks sharing one GPU produced a wrong commitment root for one of the
-// later polynomials in about one run in four (tests/test_gpu_shard_native.py
-// ::test_native_pipeline_world8_rccl_one_gpu: every rank's subtrees of that polynomial wrong,
-// with its recommitment on one GPU right), against 0 in 16 runs with every stream at one priority
-// or the prove work on the encode stream.  The ordering between the three streams rests on
-// cross-stream event waits alone; the cause under mixed priorities was not isolated further, so
-// the driver keeps to one priority.
+// shared in-order encode stream and the comm stream, ordered against them by cross-stream event
+// waits alone.  All three are at ONE priority.  With high-priority prove streams over
+// normal-priority encode / comm streams (LCPC_SHARD_PRIO=2, kept for A/B runs only) eight ranks
+// sharing one GPU produced a wrong commitment root for one of the later polynomials in about one
+// run in four (tests/test_gpu_shard_native.py::test_native_pipeline_world8_rccl_one_gpu: every
+// rank's subtrees of that polynomial wrong, its recommitment on one GPU right); at one priority
+// it never did (0 in 28 runs, profiles/r03_world8_priority_race.json).  The cause under mixed
+// priorities was not isolated further.  Modes (LCPC_SHARD_PRIO), with the sharded engine's
+// one-rank K = 20 rate on one box: 3 (default) every stream of the driver high priority, 10.1-10.3
+// G/s; 1 every stream normal priority, 8.5-9.0; 0 the prove work on the encode stream, 9.5-10.2;
+// 2 the old mixed priorities, 10.1-11.1 (unsafe).
 int shard_prove_stream_mode() {
   static const int v = [] {
     const char *e = getenv("LCPC_SHARD_PRIO");
-    return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
+    return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 3;
   }();
   return v;
 }
 bool shard_prio_streams() { return shard_prove_stream_mode() != 0; }
-bool shard_prove_high() { return shard_prove_stream_mode() == 2; }
+// (3: every stream of the driver -- encode, exchange, prove -- at high priority)
+bool shard_all_high() { return shard_prove_stream_mode() == 3; }
+bool shard_prove_high() { return shard_prove_stream_mode() >= 2; }
 
 struct ShardDeleter {
   void operator()(lcpc_sharded_commit *c) const {
@@ -433,7 +437,7 @@ struct ShardDeleter {
                     &c->allcols, &c->dpaths, &c->scratch})
       b->settle();
     delete c;
-    if (s) d->release_stream(s, false);
+    if (s) d->release_stream(s, shard_all_high());
     if (sp) d->release_stream(sp, shard_prove_high());
   }
 };
@@ -494,7 +498,7 @@ lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, S
   shard_geom(c.get(), e->fid, e->n_per_row, e->n_cols, n_rows, comm->nranks, comm->rank, e->kind == KIND_SDIG);
   HIP_TRY(hipSetDevice(c->dev->id));
   c->own_s = bulk == nullptr;
-  c->s = bulk ? bulk : c->dev->acquire_stream(false);
+  c->s = bulk ? bulk : c->dev->acquire_stream(shard_all_high());
   if (!c->s) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   c->sp = shard_prio_streams() ? c->dev->acquire_stream(shard_prove_high()) : c->s;
   if (!c->sp) return fail(LCPC_ERR_DEVICE, "no HIP stream");
@@ -1059,7 +1063,13 @@ static lcpc_status comm_common(lcpc_comm *c) {
   c->dev = current_device(&st);
   if (!c->dev) return st;
   HIP_TRY(hipSetDevice(c->dev->id));
-  HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+  if (shard_all_high()) {
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_TRY(hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, hi));
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+  }
   return LCPC_OK;
 }
 
@@ -1316,12 +1326,12 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   // commitment's root arrived late), while the short exchange-side and prove kernels run on each
   // polynomial's own (prove) stream
   TaskPool encoder(1, e->dev->id);
-  hipStream_t bulk = e->dev->acquire_stream(false);
+  hipStream_t bulk = e->dev->acquire_stream(shard_all_high());
   if (!bulk) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   struct BulkRelease {  // (destroyed after cs: returns the stream to the pool)
     Device *d;
     hipStream_t s;
-    ~BulkRelease() { d->release_stream(s, false); }
+    ~BulkRelease() { d->release_stream(s, shard_all_high()); }
   } bulk_release{e->dev, bulk};
   std::vector<ShardPtr> cs(n_polys);
   struct BulkDrain {  // (destroyed before cs: no polynomial is torn down under its running encode)
@@ -1552,11 +1562,11 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
   // two streams per polynomial in flight (commit, prove)
   std::vector<hipStream_t> lo, hi;
   for (size_t k = 0; k < depth; k++) {
-    lo.push_back(dev->acquire_stream(false));
+    lo.push_back(dev->acquire_stream(shard_all_high()));
     if (shard_prio_streams()) hi.push_back(dev->acquire_stream(shard_prove_high()));
   }
   for (hipStream_t x : lo)
-    if (x) dev->release_stream(x, false);
+    if (x) dev->release_stream(x, shard_all_high());
   for (hipStream_t x : hi)
     if (x) dev->release_stream(x, shard_prove_high());
   return st;
