@@ -431,19 +431,17 @@ __device__ __forceinline__ void fold_cvs(uint32_t *__restrict__ cvs, size_t n_co
 // so the fold runs in two passes: every group in parallel, then each column's group nodes.
 constexpr int MERGE_GROUP = 8;
 
-// pass 1: one thread per (column, group); the group's node goes to its first chunk slot, or --
-// when one group is the whole tree -- the column's leaf
+// pass 1 (more than one group): one thread per (column, group); the group's node goes to its
+// first chunk slot
 __global__ __launch_bounds__(256) void k_leaf_merge_groups(uint32_t *__restrict__ cvs, size_t n_cols,
-                                                           int n_chunks, uint8_t *__restrict__ leaves) {
+                                                           int n_chunks) {
   const size_t col = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int g = blockIdx.y;
   if (col >= n_cols) return;
   const int first = g * MERGE_GROUP;
   const int count = n_chunks - first < MERGE_GROUP ? n_chunks - first : MERGE_GROUP;
-  const bool whole = n_chunks <= MERGE_GROUP;
   uint32_t o[8];
-  fold_cvs(cvs, n_cols, col, first, count, 1, whole, o);
-  if (whole) store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), o);
+  fold_cvs(cvs, n_cols, col, first, count, 1, false, o);
 }
 
 // one thread per column folds its `count` nodes (slots 0, stride, 2 stride, ...) into the leaf:
@@ -470,8 +468,7 @@ hipError_t launch_leaf_merge(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t
                        1, leaves);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_leaf_merge_groups, dim3(bx, (unsigned)n_groups), dim3(64), 0, s, cvs, n_cols, n_chunks,
-                     leaves);
+  hipLaunchKernelGGL(k_leaf_merge_groups, dim3(bx, (unsigned)n_groups), dim3(64), 0, s, cvs, n_cols, n_chunks);
   hipLaunchKernelGGL(k_leaf_merge, dim3(bx), dim3(64), 0, s, cvs, n_cols, (n_chunks + MERGE_GROUP - 1) / MERGE_GROUP,
                      MERGE_GROUP, leaves);
   return hipGetLastError();

@@ -1390,7 +1390,11 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   // polynomial k's encode is launched AHEAD ticks before its chaining-value exchange, so a tick's
   // exchange group (which waits for every producer in it) does not wait on a just-launched encode
   // and the encode stream stays fed while a tick waits on the host
-  constexpr size_t AHEAD = 3;
+  static const size_t AHEAD = [] {  // (LCPC_SHARD_AHEAD: A/B runs)
+    const char *v = getenv("LCPC_SHARD_AHEAD");
+    const long n = v ? atol(v) : 0;
+    return n > 0 ? (size_t)n : (size_t)3;
+  }();
   for (size_t k = 0; k < std::min(AHEAD, n_polys); k++) start(k);
   for (size_t t = 0; t < n_ticks; t++) {
     prof::HostScope hs_tick("tick_total");
