@@ -239,25 +239,23 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
 // (rows padded to 80 B so the per-column reads are bank-conflict free).  Needs
 // n_rows * N % 4 == 0 (16-B aligned columns); the message word w of a column is memory word w - 8
 // of the column (w >= 8), and a 4-word unit lies wholly inside or outside the message.
+// fuse2: a two-chunk message hashed whole by one wave (grid.y = 1, leaves written directly).
 template <class F, bool CANON>
 __global__ __launch_bounds__(256) void k_leaf_chunks_cm(const uint32_t *__restrict__ m, size_t n_rows,
                                                         size_t n_cols, uint32_t *__restrict__ cvs,
-                                                        uint8_t *__restrict__ leaves, int n_chunks) {
+                                                        uint8_t *__restrict__ leaves, int n_chunks, int fuse2) {
   constexpr int N = F::N;
   static_assert(16 % N == 0 && 8 % N == 0, "element must tile a BLAKE3 block");
   constexpr int EPB = 16 / N;
   __shared__ uint4 stage[4][64][5];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const size_t col0 = ((size_t)blockIdx.x * 4 + wave) * 64, col = col0 + lane;
-  const int chunk = blockIdx.y;
   if (col0 >= n_cols) return;  // whole waves
   const size_t msg_words = 8 + n_rows * N;  // the column's message, in words
-  const size_t w0 = (size_t)chunk * 256;
-  const size_t cw = msg_words - w0 < 256 ? msg_words - w0 : 256;
-  const int nb = (int)((cw + 15) / 16);
   const int unit = lane & 3, csub = lane >> 2;
-  // block b's 4 loads of this lane: unit `unit` (words 4 unit .. +3) of column col0 + csub + 16 i
-  auto gload = [&](int b, uint4 r[4]) {
+  // block b (of the chunk starting at message word w0): this lane's 4 loads, unit `unit` (words
+  // 4 unit .. +3) of column col0 + csub + 16 i
+  auto gload = [&](size_t w0, int b, uint4 r[4]) {
     const size_t w = w0 + 16 * (size_t)b + 4 * unit;  // message word
     const bool in = w >= 8 && w < msg_words;
 #pragma unroll
@@ -277,46 +275,65 @@ __global__ __launch_bounds__(256) void k_leaf_chunks_cm(const uint32_t *__restri
     for (int i = 0; i < 4; i++) stage[wave][csub + 16 * i][unit] = r[i];
     wave_sync();
   };
-  uint32_t cv[8];
-  iv(cv);
-  uint4 r[4];
-  gload(0, r);
-  lput(r);
-  for (int b = 0; b < nb; b++) {
-    const bool more = b + 1 < nb;
-    if (more) gload(b + 1, r);
-    uint32_t msg[16];
-    {
-      const uint4 *row = stage[wave][lane];
+  // one chunk's chaining value (its blocks staged through LDS, the next block's loads in flight
+  // while this one compresses)
+  auto chunk_cv = [&](int chunk, uint32_t cv[8]) {
+    const size_t w0 = (size_t)chunk * 256;
+    const size_t cw = msg_words - w0 < 256 ? msg_words - w0 : 256;
+    const int nb = (int)((cw + 15) / 16);
+    iv(cv);
+    uint4 r[4];
+    gload(w0, 0, r);
+    lput(r);
+    for (int b = 0; b < nb; b++) {
+      const bool more = b + 1 < nb;
+      if (more) gload(w0, b + 1, r);
+      uint32_t msg[16];
+      {
+        const uint4 *row = stage[wave][lane];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint4 q = row[k];
-        msg[4 * k] = q.x; msg[4 * k + 1] = q.y; msg[4 * k + 2] = q.z; msg[4 * k + 3] = q.w;
+        for (int k = 0; k < 4; k++) {
+          const uint4 q = row[k];
+          msg[4 * k] = q.x; msg[4 * k + 1] = q.y; msg[4 * k + 2] = q.z; msg[4 * k + 3] = q.w;
+        }
       }
+      wave_sync();  // every lane has read block b before block b + 1 overwrites the stage
+      // element words -> repr words (Montgomery -> canonical unless CANON); the zero prefix and
+      // words past the message stay zero either way (from_mont(0) = 0, and they load as zero)
+#pragma unroll
+      for (int k = 0; k < EPB; k++) {
+        Fe<F> e;
+#pragma unroll
+        for (int i = 0; i < N; i++) e.v[i] = msg[k * N + i];
+        uint32_t w[N];
+        if constexpr (CANON)
+          fe_canon_repr_words<F>(e, w);
+        else
+          fe_repr_words<F>(e, w);
+#pragma unroll
+        for (int i = 0; i < N; i++) msg[k * N + i] = w[i];
+      }
+      const size_t left = cw - 16 * (size_t)b;
+      const uint32_t blen = left >= 16 ? 64u : (uint32_t)(4 * left);
+      uint32_t flags = b == 0 ? CHUNK_START : 0u;
+      if (b == nb - 1) flags |= CHUNK_END | (n_chunks == 1 ? ROOT : 0u);
+      compress(cv, msg, (uint64_t)chunk, blen, flags);
+      if (more) lput(r);
     }
-    wave_sync();  // every lane has read block b before block b + 1 overwrites the stage
-    // element words -> repr words (Montgomery -> canonical unless CANON); the zero prefix and
-    // words past the message stay zero either way (from_mont(0) = 0, and they load as zero)
-#pragma unroll
-    for (int k = 0; k < EPB; k++) {
-      Fe<F> e;
-#pragma unroll
-      for (int i = 0; i < N; i++) e.v[i] = msg[k * N + i];
-      uint32_t w[N];
-      if constexpr (CANON)
-        fe_canon_repr_words<F>(e, w);
-      else
-        fe_repr_words<F>(e, w);
-#pragma unroll
-      for (int i = 0; i < N; i++) msg[k * N + i] = w[i];
-    }
-    const size_t left = cw - 16 * (size_t)b;
-    const uint32_t blen = left >= 16 ? 64u : (uint32_t)(4 * left);
-    uint32_t flags = b == 0 ? CHUNK_START : 0u;
-    if (b == nb - 1) flags |= CHUNK_END | (n_chunks == 1 ? ROOT : 0u);
-    compress(cv, msg, (uint64_t)chunk, blen, flags);
-    if (more) lput(r);
+  };
+  uint32_t cv[8];
+  if (fuse2) {
+    // a two-chunk message (cfg4's 1184-byte leaves) whole in one wave: both chaining values in
+    // registers and their ROOT parent, no scratch round trip and no merge launch
+    uint32_t cv1[8], leaf[8];
+    chunk_cv(0, cv);
+    chunk_cv(1, cv1);
+    parent_cv(cv, cv1, true, leaf);
+    if (col < n_cols) store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), leaf);
+    return;
   }
+  const int chunk = blockIdx.y;
+  chunk_cv(chunk, cv);
   if (col >= n_cols) return;
   if (n_chunks == 1 && leaves) {
     store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
@@ -585,16 +602,20 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
   const size_t words = 8 + n_rows * (size_t)field_words(fid);
   const int n_chunks = (int)((words + 255) / 256);
   dim3 grid((unsigned)((n_cols + 255) / 256), (unsigned)n_chunks);
+  bool leaves_done = false;
   hipError_t e = dispatch_field(fid, [&]<class F>() {
     if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
       prof::Scope ps("leaf_chunks", s);
       if (row_stride == 1 && col_stride == n_rows && (n_rows * F::N) % 4 == 0) {  // column-major, 16-B aligned
+        const int fuse2 = n_chunks == 2 && leaves;
+        const dim3 g2(grid.x, fuse2 ? 1 : grid.y);
         if (canon)
-          hipLaunchKernelGGL((k_leaf_chunks_cm<F, true>), grid, dim3(256), 0, s, m, n_rows, n_cols,
-                             (uint32_t *)scratch, leaves, n_chunks);
+          hipLaunchKernelGGL((k_leaf_chunks_cm<F, true>), g2, dim3(256), 0, s, m, n_rows, n_cols,
+                             (uint32_t *)scratch, leaves, n_chunks, fuse2);
         else
-          hipLaunchKernelGGL((k_leaf_chunks_cm<F, false>), grid, dim3(256), 0, s, m, n_rows, n_cols,
-                             (uint32_t *)scratch, leaves, n_chunks);
+          hipLaunchKernelGGL((k_leaf_chunks_cm<F, false>), g2, dim3(256), 0, s, m, n_rows, n_cols,
+                             (uint32_t *)scratch, leaves, n_chunks, fuse2);
+        leaves_done = fuse2;  // (the leaves are written: no merge)
         return hipGetLastError();
       }
       if (canon)
@@ -615,7 +636,7 @@ static hipError_t leaf_hashes_strided(int fid, const uint32_t *m, size_t n_rows,
       return hipGetLastError();
     }
   });
-  if (e != hipSuccess || n_chunks == 1) return e;
+  if (e != hipSuccess || n_chunks == 1 || leaves_done) return e;
   return launch_leaf_merge((uint32_t *)scratch, n_cols, n_chunks, leaves, s);
 }
 

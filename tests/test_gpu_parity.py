@@ -131,6 +131,24 @@ def test_leaf_merge_chunk_counts(gpu, oracle, n_rows):
     assert g.get_root() == o.root()
 
 
+@pytest.mark.parametrize("fid", FIELDS)
+@pytest.mark.parametrize("chunks", [1, 2, 3])
+def test_column_major_leaves_by_chunk_count(gpu, oracle, fid, chunks):
+    """Column-major leaves (lcpc_hash_field_columns: the SDIG commitments' and the PoS files'
+    layout) of 1, 2 and 3 BLAKE3 chunks -- two-chunk messages (cfg4's 1184-byte leaves) are hashed
+    whole by one wave (blake3.hip k_leaf_chunks_cm, fuse2) -- against the oracle's leaves of the
+    same matrix (lcpc-2d/src/lib.rs:736-775)."""
+    from lcpc_proof_of_storage_amd import pos
+    wb = 8 * gpu.limbs(fid)
+    n_rows = {1: (1024 - 32) // wb, 2: (2048 - 32) // wb - 1, 3: (2048 - 32) // wb + 3}[chunks]
+    n_cols = 300
+    m = rand_elems(oracle, fid, n_rows * n_cols, 31 + chunks).reshape(n_rows, n_cols, -1)
+    want = oracle.hash_columns(fid, m.reshape(-1), n_rows, n_cols)
+    cols = [np.ascontiguousarray(m[:, j, :]) for j in range(n_cols)]
+    got = pos.hash_columns_to_digests(cols, fid)
+    assert b"".join(got) == want
+
+
 def test_commit_empty_and_oversized_inputs(gpu, oracle):
     """commit's shape asserts (lcpc-2d/src/lib.rs:659-661) are LcpcError here, not a panic: an
     empty polynomial has no rows ((n_rows - 1) underflows in the reference); a device commit of
