@@ -41,7 +41,9 @@ __global__ __launch_bounds__(256) void k_pack7(const uint8_t *__restrict__ bytes
   __shared__ __align__(16) uint64_t s_out[PACK_EL];
   const int tid = threadIdx.x;
   const size_t eb = (size_t)blockIdx.x * PACK_EL, bb = (size_t)blockIdx.x * PACK_BYTES;
-  if (eb + PACK_EL <= n_elems && bb + PACK_BYTES <= n_bytes) {
+  // (the API guarantees 8-byte buffers; the 16-byte path needs both 16-byte aligned)
+  const bool a16 = (((uintptr_t)bytes | (uintptr_t)out) & 15) == 0;
+  if (a16 && eb + PACK_EL <= n_elems && bb + PACK_BYTES <= n_bytes) {
     const uint4 *src = reinterpret_cast<const uint4 *>(bytes + bb);  // 16-byte aligned
     uint4 *si = reinterpret_cast<uint4 *>(s_in);
 #pragma unroll

@@ -26,18 +26,24 @@ def test_bytes_to_field_and_back(pos, oracle):
         assert pos.convert_field_elements_vec_to_byte_vec(el, n) == data
 
 
-def test_bytes_to_field_device(gpu, oracle, hipmem):
+@pytest.mark.parametrize("off_in,off_out", [(0, 0), (8, 0), (0, 8)])
+def test_bytes_to_field_device(gpu, oracle, hipmem, off_in, off_out):
+    """lcpc_pos_bytes_to_field_device on 16-byte aligned buffers (the LDS-staged blocks of 2048
+    elements plus a ragged tail) and on buffers only 8-byte aligned (the API's requirement: the
+    per-thread path)."""
     import ctypes as C
     from lcpc_proof_of_storage_amd import _native as N
     rng = np.random.default_rng(2)
     n = 7 * 100000 + 3
     data = rng.integers(0, 256, n, dtype=np.uint8)
-    d_in = hipmem.to_device(data)
-    out = np.zeros((n + 6) // 7, np.uint64)
+    d_in = hipmem.to_device(np.concatenate([np.zeros(off_in, np.uint8), data]))
+    out = np.zeros((n + 6) // 7 + off_out // 8, np.uint64)
     d_out = hipmem.to_device(out)
     try:
-        assert N.load().lcpc_pos_bytes_to_field_device(C.c_void_p(d_in), n, C.c_void_p(d_out), None) == 0
-        assert np.array_equal(hipmem.to_host(d_out, out), oracle.pos_bytes_to_field(data.tobytes()))
+        assert N.load().lcpc_pos_bytes_to_field_device(C.c_void_p(d_in + off_in), n, C.c_void_p(d_out + off_out),
+                                                       None) == 0
+        got = hipmem.to_host(d_out, out)[off_out // 8:]
+        assert np.array_equal(got, oracle.pos_bytes_to_field(data.tobytes()))
     finally:
         hipmem.free(d_in)
         hipmem.free(d_out)
