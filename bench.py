@@ -58,7 +58,9 @@ def parse():
                          "commitments in flight are the faster single-GPU engine")
     ap.add_argument("--sharded-n1", type=int, default=1,
                     help="N = 1 replicas lines (ligero): also time the row-sharded engine on the one GPU "
-                         "(the N = 1 base of the sharded N > 1 lines) and report it as \"sharded_n1\"")
+                         "(the N = 1 base of the sharded N > 1 lines) and report it as \"sharded_n1\": "
+                         "1 in a fresh child process (as an N > 1 rank starts), 2 in this process after "
+                         "the replicas run, 0 off")
     ap.add_argument("--lag", type=int, default=0,
                     help="sharded driver: ticks between a row-combination gather and the next challenge "
                          "broadcast (0: the library's choice)")
@@ -716,10 +718,12 @@ def main():
         out = run_sharded(args, L, torch, dist, rank, world, device, backend, share)
     else:
         out = run_replicas(args, L, torch, dist, rank, world, device_idx, backend)
-        if world == 1 and args.code == "ligero" and args.sharded_n1:
+        if world == 1 and args.code == "ligero" and args.sharded_n1 == 2:
             # the row-sharded engine on this one GPU, like for like with the N > 1 lines
             # (--mode auto runs it there): same steps and warm-up, after the replicas' figures
             sharded_n1 = sharded_n1_figure(args, L, torch, device)
+        elif world == 1 and args.code == "ligero" and args.sharded_n1 == 1:
+            sharded_n1 = sharded_n1_child(args)
     if sharded_n1 is not None:
         out["sharded_n1"] = sharded_n1
     if rank == 0:
@@ -728,6 +732,40 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def sharded_n1_child(args):
+    """The sharded engine's one-GPU figure from a fresh child process running this script with
+    --mode sharded (same workload, steps and warm-up): the engine's streams and pools start as an
+    N > 1 rank's do, not after this process's replicas run left its stream pools in use (the
+    in-process figure, --sharded-n1 2, measured 9.1-9.4 against 10.1-10.4 G/s on one box)."""
+    import subprocess
+    drop = {"--mode": 1, "--sharded-n1": 1, "--cpu-baseline": 1, "--verify-reps": 1, "--timeline": 1}
+    argv, i = [], 0
+    src = sys.argv[1:]
+    while i < len(src):
+        a = src[i]
+        key = a.split("=", 1)[0]
+        if key in drop:
+            i += 1 if "=" in a else 1 + drop[key]
+            continue
+        argv.append(a)
+        i += 1
+    cmd = [sys.executable, os.path.abspath(__file__)] + argv + ["--mode", "sharded", "--sharded-n1", "0",
+                                                                 "--cpu-baseline", "off", "--verify-reps", "0"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    except subprocess.TimeoutExpired:
+        return {"error": "the child process timed out"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode or not lines:
+        return {"error": f"child exit {r.returncode}", "stderr_tail": r.stderr[-400:]}
+    d = json.loads(lines[-1])
+    return {"value": d["value"], "unit": d["unit"], "steps": d["steps"], "warmup": d["warmup"],
+            "ms_per_step": d["ms_per_step"], "scaling": "strong",
+            "engine": "lcpc_sharded_commit_prove_many, one rank (no exchanges): the N = 1 point of the "
+                      "--mode sharded (--gpus N > 1) curve, timed in a fresh child process",
+            "lag": args.lag or None, "root": d.get("root")}
 
 
 def sharded_n1_figure(args, L, torch, device):
@@ -833,6 +871,7 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
         mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row",
         leaf_compressions=leaf_compressions(n_rows, n_cols, B) if world == 1 else 0)
     out.update(roofline_objects(wl, iso, stats, args, traffic_rows_frac=nr / n_rows))
+    out["root"] = roots[0].hex()  # (every step commits the same polynomial)
 
     # the verifier (outside the timed region): the serial step's proof, verified again
     if rank == 0 and args.verify_reps > 0 and pf is not None:
