@@ -160,8 +160,10 @@ void run(const char *name, size_t n_rows, size_t n_cols, hipStream_t s) {
   float ms = tm.time([&]() { CK(leaf_hashes(F::ID, cw, n_rows, n_cols, n_cols, leaves, scratch, s, true)); }, reps);
   printf("%s library leaves total        %.4f ms (%.2f TB/s)\n", name, ms, bytes / ms / 1e9);
   ms = tm.time([&]() {
-    hipLaunchKernelGGL((k_leaf_chunks<F, true>), grid, dim3(256), 0, s, cw, n_rows, n_cols, n_cols, (size_t)1, cvs,
-                       leaves, n_chunks, (size_t)0, 0, n_chunks);
+    // (the library's grid: a block = 4 waves on 256 adjacent columns of one chunk)
+    hipLaunchKernelGGL((k_leaf_chunks<F, true>), dim3((unsigned)((n_cols + 255) / 256), (unsigned)n_chunks),
+                       dim3(256), 0, s, cw, n_rows, n_cols, n_cols, (size_t)1, cvs, leaves, n_chunks, (size_t)0, 0,
+                       n_chunks, (size_t)0);
   }, reps);
   printf("%s library k_leaf_chunks       %.4f ms (%.2f TB/s)\n", name, ms, bytes / ms / 1e9);
   dim3 gi((unsigned)((n_cols + 63) / 64), (unsigned)((n_full + 3) / 4));
