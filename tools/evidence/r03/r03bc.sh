@@ -1,5 +1,5 @@
 #!/bin/bash
 set -e
-bash tools/r03b.sh r03b
-bash tools/r03c.sh r03c
+bash tools/evidence/r03/r03b.sh r03b
+bash tools/evidence/r03/r03c.sh r03c
 echo all-ok
