@@ -14,6 +14,8 @@
 // the row-major codeword (no transpose).  Chunk chaining values of multi-chunk leaves go to a
 // [chunk][column] scratch (coalesced both ways) and a second kernel folds them with BLAKE3's
 // left-balanced tree (pairwise per level, odd node carried up, ROOT on the last parent).
+#include <cstdlib>
+
 #include "field.hpp"
 #include "kernels.hpp"
 #include "prof.hpp"
@@ -115,32 +117,20 @@ __device__ __forceinline__ size_t cv_slot(size_t col, int chunk, int chunk0, int
   return blk ? ((col / blk) * (size_t)(chunk_end - chunk0) + c) * blk + col % blk : c * n_cols + col;
 }
 
-// One thread per (column, chunk).  Message word w of a column: w < 8 is the zero prefix,
-// else word (w-8) % N of element row (w-8) / N.  N in {2, 4, 8} divides both 8 and 16, so
-// every 16-word block holds whole elements.  The launch covers chunks [chunk0, chunk_end) of
-// messages of n_rows rows; m holds rows [row0, ...) (a row shard: every row those chunks read
-// is present), and chaining values go to cvs[chunk - chunk0][col].
+// The chaining value of chunk `chunk` of one column's leaf message (column pointer colp, element
+// row r at colp + (r - row0) row_stride).  Message word w of a column: w < 8 is the zero prefix,
+// else word (w-8) % N of element row (w-8) / N.  N in {2, 4, 8} divides both 8 and 16, so every
+// 16-word block holds whole elements.  A one-chunk message gets ROOT (it is the leaf).
 template <class F, bool CANON>
-__global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict__ m,
-                                                     size_t n_rows, size_t n_cols,
-                                                     size_t row_stride, size_t col_stride,
-                                                     uint32_t *__restrict__ cvs,
-                                                     uint8_t *__restrict__ leaves, int n_chunks,
-                                                     size_t row0, int chunk0, int chunk_end, size_t blk) {
+__device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, size_t n_rows, size_t row_stride,
+                                            size_t row0, int chunk, int n_chunks, uint32_t cv[8]) {
   constexpr int N = F::N;
   static_assert(16 % N == 0 && 8 % N == 0, "element must tile a BLAKE3 block");
-  // a block = 4 waves on 256 adjacent columns of one chunk (every wave of a block does the same
-  // amount of work; a chunk per wave left the waves of chunks >= n_chunks idle)
-  const size_t col = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const int chunk = chunk0 + blockIdx.y;
-  if (col >= n_cols || chunk >= chunk_end) return;
   const size_t total_words = 8 + n_rows * N;
   const size_t w0 = (size_t)chunk * 256;
   const size_t cw = total_words - w0 < 256 ? total_words - w0 : 256;
   const int nb = (int)((cw + 15) / 16);
-  uint32_t cv[8];
   iv(cv);
-  const uint32_t *colp = m + col * col_stride * N;
   constexpr int EPB = 16 / N;  // elements per 64-byte block
   // element e of the block starting at word gw: stream word gw + e N - 8 (negative: prefix)
   auto fetch = [&](size_t gw, Fe<F> *raw) {
@@ -189,7 +179,6 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
         to_msg(eb, msg);
         compress(cv, msg, (uint64_t)chunk, 64u, b + 1 == 15 ? CHUNK_END : 0u);
       }
-      store8(cvs + cv_slot(col, chunk, chunk0, chunk_end, n_cols, blk) * 8, cv);
       return;
     }
   }
@@ -224,6 +213,25 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
 #pragma unroll
     for (int k = 0; k < EPB; k++) cur[k] = nxt[k];
   }
+}
+
+// One thread per (column, chunk) of a row-major matrix.  The launch covers chunks [chunk0,
+// chunk_end) of messages of n_rows rows; m holds rows [row0, ...) (a row shard: every row those
+// chunks read is present), and chaining values go to cvs[chunk - chunk0][col] (cv_slot).
+template <class F, bool CANON>
+__global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict__ m,
+                                                     size_t n_rows, size_t n_cols,
+                                                     size_t row_stride, size_t col_stride,
+                                                     uint32_t *__restrict__ cvs,
+                                                     uint8_t *__restrict__ leaves, int n_chunks,
+                                                     size_t row0, int chunk0, int chunk_end, size_t blk) {
+  // a block = 4 waves on 256 adjacent columns of one chunk (every wave of a block does the same
+  // amount of work; a chunk per wave left the waves of chunks >= n_chunks idle)
+  const size_t col = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int chunk = chunk0 + blockIdx.y;
+  if (col >= n_cols || chunk >= chunk_end) return;
+  uint32_t cv[8];
+  chunk_cv_rm<F, CANON>(m + col * col_stride * F::N, n_rows, row_stride, row0, chunk, n_chunks, cv);
   if (n_chunks == 1 && leaves) {
     store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
   } else {
