@@ -808,9 +808,11 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
     L.prof_reset()
     barrier()
     t0 = time.perf_counter()
+    c0, th0 = os.times(), cgroup_throttle()
     troots, _ = S["run"](args.steps)
     barrier()
     elapsed = time.perf_counter() - t0
+    c1, th1 = os.times(), cgroup_throttle()
     L.prof_enable(False)
     stats = L.prof_stats() if prof_timed else {}
     assert all(r == roots[0] for r in troots), "timed-region roots differ from the warm-up's"
@@ -860,6 +862,9 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
                     "what": "one commitment, serial: lcpc_sharded_commit_new_device and lcpc_sharded_prove "
                             "(host wall clock, median of the roofline steps)"},
     }
+    out["host_cpu"] = host_cpu_use(c0, c1, elapsed)
+    if th0 and th1:
+        out["host_cpu"]["cgroup_throttled"] = {k: th1[k] - th0[k] for k in th0 if k in th1}
     if stats:
         out["kernels_timed_region"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]}
                                        for k, v in stats.items()}

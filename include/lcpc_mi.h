@@ -502,9 +502,10 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
  * rank i % nranks, whose transcript is make_transcript(user, i, root_i) (the library frees it);
  * proofs[i] is set there and NULL elsewhere (proofs may be NULL: proofs are dropped), roots
  * (optional) gets every root on every rank.  Up to `depth` polynomials are in flight; the
- * exchanges of different polynomials go out in one fixed order on every rank (one RCCL group per
- * pipeline tick), `lag` ticks apart wherever the root rank absorbs a row combination into its
- * transcript (0: automatic). */
+ * exchanges of different polynomials go out in one fixed order on every rank (two RCCL groups per
+ * pipeline tick: the stages with no host wait, then the tensor and column-index broadcasts that
+ * wait on a transcript), `lag` ticks apart wherever the root rank absorbs a row combination into
+ * its transcript (0: automatic). */
 typedef lcpc_transcript *(*lcpc_make_transcript_fn)(void *user, size_t i, const uint8_t root[32]);
 lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *const *d_rows,
                                            size_t n_polys, size_t n_rows, const uint64_t *outer,
@@ -527,7 +528,8 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
  * rank count without a GPU.  These exchanges replace nothing in the reference (its rows never
  * leave one host, lcpc-2d/src/lib.rs:677-682, 736-815); stage numbers: 0 chaining values,
  * 1 subtrees, 2 + 2r / 3 + 2r round r's tensor broadcast / partial gather, 2 + 2 rounds column
- * indices, 3 + 2 rounds opened columns (rounds = max(n_degree_tests, 1)).  *n_out = the record
+ * indices, 3 + 2 rounds opened columns (rounds = max(n_degree_tests, 1)).  A record's `tick` is
+ * its exchange group: 2t + 0 / 2t + 1 for pipeline tick t's two groups.  *n_out = the record
  * count; LCPC_ERR_INVALID_ARG if it exceeds cap (out may be NULL with cap 0 to size). */
 typedef struct lcpc_p2p_record {
   uint32_t tick, pos, poly, stage;

@@ -2,11 +2,13 @@
 #include "prof.hpp"
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lcpc_mi.h"
@@ -24,6 +26,26 @@ bool on = false;
 std::vector<Rec> pending;
 std::vector<hipEvent_t> spare;
 std::map<std::string, std::pair<double, uint64_t>> totals;
+// LCPC_PROF_TIMELINE=<path>: every host phase as (name, start, end, thread), appended to <path> as
+// CSV (steady-clock ms, the clock rocprofv3's kernel timestamps use) when profiling is switched off
+struct Span {
+  const char *name;
+  double t0, t1;
+  size_t tid;
+};
+std::vector<Span> spans;
+const char *timeline_path() {
+  static const char *p = getenv("LCPC_PROF_TIMELINE");
+  return p && p[0] ? p : nullptr;
+}
+void flush_timeline() {  // caller holds mu
+  if (spans.empty() || !timeline_path()) return;
+  if (FILE *f = fopen(timeline_path(), "a")) {
+    for (auto &s : spans) fprintf(f, "%s,%.4f,%.4f,%zu\n", s.name, s.t0, s.t1, s.tid);
+    fclose(f);
+  }
+  spans.clear();
+}
 
 hipEvent_t get_event() {
   if (!spare.empty()) {
@@ -95,6 +117,8 @@ HostScope::~HostScope() {
   auto &t = totals[name_];
   t.first += dt;
   t.second += 1;
+  if (timeline_path())
+    spans.push_back(Span{name_, t0_, t0_ + dt, std::hash<std::thread::id>{}(std::this_thread::get_id()) % 100000});
 }
 
 }  // namespace prof
@@ -105,6 +129,7 @@ extern "C" {
 void lcpc_prof_enable(int enable) {
   std::lock_guard<std::mutex> lk(lcpc::prof::mu);
   lcpc::prof::on = enable != 0;
+  if (!enable) lcpc::prof::flush_timeline();
 }
 
 void lcpc_prof_reset(void) {

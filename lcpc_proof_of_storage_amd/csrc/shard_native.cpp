@@ -29,6 +29,7 @@
 #include <deque>
 #include <functional>
 #include <future>
+#include <optional>
 
 #include "host_internal.hpp"
 
@@ -760,7 +761,10 @@ void repr_order(int fid, uint8_t *h, size_t n, int wb) {
 // root, host: absorb round r's row combination(s) (lib.rs:1075-1077, 1096-1098) and draw the
 // next challenge: tensor r + 1 (:1056-1062) or, after the last round, the columns (:1101-1110)
 lcpc_status host_absorb(lcpc_sharded_commit *c, size_t r) {
-  HIP_TRY(hipEventSynchronize(c->ev_host));
+  {
+    prof::HostScope hs("host_absorb_wait");
+    HIP_TRY(hipEventSynchronize(c->ev_host));
+  }
   const size_t wb = c->wb, np = c->np, limbs = wb / 8;
   uint8_t *repr = c->h_repr.p;
   repr_order(c->fid, repr, (size_t)round_tensors(c, r) * np, (int)wb);
@@ -850,6 +854,7 @@ lcpc_status stage_paths(lcpc_sharded_commit *c) {
 
 // root, host: the LcEvalProof (:1117-1122); columns reassembled from the ranks' row pieces
 lcpc_status host_proof(lcpc_sharded_commit *c, lcpc_proof **out) {
+  prof::HostScope hs("host_final_proof");
   HIP_TRY(hipEventSynchronize(c->ev_host));
   if (c->me != c->root_rank) {
     if (out) *out = nullptr;
@@ -938,6 +943,16 @@ Xop stage_op(lcpc_sharded_commit *c, const Sched &sc, size_t s) {
   if (s == sc.s_cols) return op_cols_gather(c);
   const size_t r = (s - S_R0) / 2;
   return (s - S_R0) % 2 == 0 ? op_tensor_bcast(c, r) : op_partial_gather(c, r);
+}
+
+// A stage whose host work waits on the transcript rank: the tensor broadcasts (round 0: the
+// commitment root; later rounds: the previous round's absorb) and the column-index broadcast.  A
+// tick issues its other stages as one exchange group before these, so no polynomial's partial
+// gather and fold -- whose absorb is the next link of that polynomial's serial chain -- queues
+// behind another polynomial's transcript (with one group per tick, every lag-th polynomial's
+// absorbs chained through the drain: K = 20 at one rank lost 2-3 ms there).
+bool stage_waits(const Sched &sc, size_t s) {
+  return s == sc.s_idx || (s >= S_R0 && s < sc.s_idx && (s - S_R0) % 2 == 0);
 }
 
 const char *stage_name(const Sched &sc, size_t s) {
@@ -1306,6 +1321,8 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   if (proofs)
     for (size_t i = 0; i < n_polys; i++) proofs[i] = nullptr;
   if (n_polys == 0) return LCPC_OK;
+  prof::HostScope hs_all("many_total");
+  std::optional<prof::HostScope> hs_setup(std::in_place, "many_setup");
   std::lock_guard<std::mutex> lk(comm->mu);
   HIP_TRY(hipSetDevice(e->dev->id));
   const int G = comm->nranks, me = comm->rank;
@@ -1396,6 +1413,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     return n > 0 ? (size_t)n : (size_t)3;
   }();
   for (size_t k = 0; k < std::min(AHEAD, n_polys); k++) start(k);
+  hs_setup.reset();
   for (size_t t = 0; t < n_ticks; t++) {
     prof::HostScope hs_tick("tick_total");
     wd.mark(t, n_ticks, "the previous tick's launches");
@@ -1409,84 +1427,88 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
       if ((st = finals.front().second.get())) return fail_all(st);
       finals.pop_front();
     }
-    std::vector<Xop> ops;
-    std::vector<hipEvent_t> done;
-    std::vector<std::pair<size_t, size_t>> items;  // (poly, stage)
-    for (size_t s = 0; s < n_stages; s++) {
-      const size_t k = sc.poly(t, s, n_polys);
-      if (k == SIZE_MAX) continue;
-      {
-        prof::HostScope hs("tick_wait_launch");
-        wd.mark(t, n_ticks, "a polynomial's compute launches");
-        if ((st = settle(k))) return fail_all(st);
-      }
-      lcpc_sharded_commit *c = cs[k].get();
-      // the stage's host work before its exchange
-      if (s == S_IDX) {
-        if (c->me == c->root_rank) {
-          prof::HostScope hs("tick_wait_challenge");
-          wd.mark(t, n_ticks, "the root rank's transcript (column challenge)");
-          if ((st = c->next.get())) return fail_all(st);
-        }
-        if ((st = stage_idx_upload(c))) return fail_all(st);
-      } else if (s >= S_R0 && s < S_IDX && (s - S_R0) % 2 == 0) {
-        const size_t r = (s - S_R0) / 2;
+    // two exchange groups per tick: the stages with no host wait first, their compute submitted at
+    // once, then the stages that wait on a transcript (see stage_waits)
+    for (int pass = 0; pass < 2; pass++) {
+      std::vector<Xop> ops;
+      std::vector<hipEvent_t> done;
+      std::vector<std::pair<size_t, size_t>> items;  // (poly, stage)
+      for (size_t s = 0; s < n_stages; s++) {
+        const size_t k = sc.poly(t, s, n_polys);
+        if (k == SIZE_MAX || stage_waits(sc, s) != (pass == 1)) continue;
         {
-          if (r == 0) {
-            // the commit is complete (root on the host) and the transcript exists
-            {
-              prof::HostScope hs("tick_wait_root");
-              wd.mark(t, n_ticks, "the commitment root (subtree exchange)");
-              if ((st = finish_commit(c))) return fail_all(st);
-            }
-            if (roots) std::memcpy(roots + 32 * k, c->root, 32);
-            lcpc_transcript *tr = nullptr;
-            if (me == (int)(k % G)) {
-              prof::HostScope hs2("tick_make_transcript");
-              tr = make_transcript(user, k, c->root);
-              if (!tr) return fail_all(fail(LCPC_ERR_INVALID_ARG, "make_transcript returned NULL"));
-            }
-            prof::HostScope hs("tick_prove_init");
-            c->tr = tr;  // (the buffers: prove_alloc, with the subtree stage's launches)
-            c->own_tr = true;
-            if (me == c->root_rank && (st = challenge_first(c))) return fail_all(st);
-          } else if (c->me == c->root_rank) {
+          prof::HostScope hs("tick_wait_launch");
+          wd.mark(t, n_ticks, "a polynomial's compute launches");
+          if ((st = settle(k))) return fail_all(st);
+        }
+        lcpc_sharded_commit *c = cs[k].get();
+        // the stage's host work before its exchange
+        if (s == S_IDX) {
+          if (c->me == c->root_rank) {
             prof::HostScope hs("tick_wait_challenge");
-            wd.mark(t, n_ticks, "the root rank's transcript (challenge tensor)");
+            wd.mark(t, n_ticks, "the root rank's transcript (column challenge)");
             if ((st = c->next.get())) return fail_all(st);
           }
-          if ((st = stage_tensor_upload(c, r))) return fail_all(st);
+          if ((st = stage_idx_upload(c))) return fail_all(st);
+        } else if (s >= S_R0 && s < S_IDX && (s - S_R0) % 2 == 0) {
+          const size_t r = (s - S_R0) / 2;
+          {
+            if (r == 0) {
+              // the commit is complete (root on the host) and the transcript exists
+              {
+                prof::HostScope hs("tick_wait_root");
+                wd.mark(t, n_ticks, "the commitment root (subtree exchange)");
+                if ((st = finish_commit(c))) return fail_all(st);
+              }
+              if (roots) std::memcpy(roots + 32 * k, c->root, 32);
+              lcpc_transcript *tr = nullptr;
+              if (me == (int)(k % G)) {
+                prof::HostScope hs2("tick_make_transcript");
+                tr = make_transcript(user, k, c->root);
+                if (!tr) return fail_all(fail(LCPC_ERR_INVALID_ARG, "make_transcript returned NULL"));
+              }
+              prof::HostScope hs("tick_prove_init");
+              c->tr = tr;  // (the buffers: prove_alloc, with the subtree stage's launches)
+              c->own_tr = true;
+              if (me == c->root_rank && (st = challenge_first(c))) return fail_all(st);
+            } else if (c->me == c->root_rank) {
+              prof::HostScope hs("tick_wait_challenge");
+              wd.mark(t, n_ticks, "the root rank's transcript (challenge tensor)");
+              if ((st = c->next.get())) return fail_all(st);
+            }
+            if ((st = stage_tensor_upload(c, r))) return fail_all(st);
+          }
         }
+        ops.push_back(stage_op(c, sc, s));
+        done.push_back(c->ev_done);
+        items.emplace_back(k, s);
       }
-      ops.push_back(stage_op(c, sc, s));
-      done.push_back(c->ev_done);
-      items.emplace_back(k, s);
-    }
-    if (!ops.empty()) {
-      prof::HostScope hs("tick_run_group");
-      wd.mark(t, n_ticks, "issuing the exchange group", G > 1 ? describe_group(items, ops, sc, G, me) : std::string());
-      if ((st = run_group(comm, ops, done))) return fail_all(st);
-    }
-    // the compute each exchange feeds, on the polynomials' own streams (launch workers)
-    prof::HostScope hs_sub("tick_submit");
-    for (auto [k, s] : items) {
-      lcpc_sharded_commit *c = cs[k].get();
-      pending[k] = launch.submit(wrap([&pool, c, s = s, k = k, S_IDX, S_COLS, outer, G, e]() -> lcpc_status {
-        if (s == S_CV) return stage_post_cv(c);
-        if (s == S_SUB) {
-          const lcpc_status s2 = stage_post_subtrees(c);
-          return s2 ? s2 : prove_alloc(c, outer, (int)(k % G), e);
-        }
-        if (s == S_IDX) return stage_gather_cols(c);
-        if (s == S_COLS) return stage_paths(c);
-        const size_t r = (s - S_R0) / 2;
-        if ((s - S_R0) % 2 == 0) return stage_collapse(c, r);
-        const lcpc_status s2 = stage_fold(c, r);
-        if (s2) return s2;
-        if (c->me == c->root_rank) c->next = pool.submit([c, r] { return host_absorb(c, r); });
-        return LCPC_OK;
-      }));
-      if (s == S_COLS) to_finalize.push_back(k);
+      if (!ops.empty()) {
+        prof::HostScope hs("tick_run_group");
+        wd.mark(t, n_ticks, "issuing the exchange group", G > 1 ? describe_group(items, ops, sc, G, me) : std::string());
+        if ((st = run_group(comm, ops, done))) return fail_all(st);
+      }
+      // the compute each exchange feeds, on the polynomials' own streams (launch workers)
+      prof::HostScope hs_sub("tick_submit");
+      for (auto [k, s] : items) {
+        lcpc_sharded_commit *c = cs[k].get();
+        pending[k] = launch.submit(wrap([&pool, c, s = s, k = k, S_IDX, S_COLS, outer, G, e]() -> lcpc_status {
+          if (s == S_CV) return stage_post_cv(c);
+          if (s == S_SUB) {
+            const lcpc_status s2 = stage_post_subtrees(c);
+            return s2 ? s2 : prove_alloc(c, outer, (int)(k % G), e);
+          }
+          if (s == S_IDX) return stage_gather_cols(c);
+          if (s == S_COLS) return stage_paths(c);
+          const size_t r = (s - S_R0) / 2;
+          if ((s - S_R0) % 2 == 0) return stage_collapse(c, r);
+          const lcpc_status s2 = stage_fold(c, r);
+          if (s2) return s2;
+          if (c->me == c->root_rank) c->next = pool.submit([c, r] { return host_absorb(c, r); });
+          return LCPC_OK;
+        }));
+        if (s == S_COLS) to_finalize.push_back(k);
+      }
     }
     if (t + AHEAD < n_polys) start(t + AHEAD);
   }
@@ -1593,12 +1615,13 @@ lcpc_status lcpc_sharded_p2p_schedule(lcpc_field f, size_t n_rows, size_t n_per_
     prove_geom(cs[k].get(), n_degree_tests, n_col_opens, (int)(k % nranks));
   }
   size_t n = 0;
-  for (size_t t = 0; t < sc.n_ticks; t++) {
+  for (size_t grp = 0; grp < 2 * sc.n_ticks; grp++) {  // (the driver's two groups per tick)
+    const size_t t = grp / 2;
     std::vector<Xop> ops;
     std::vector<std::pair<size_t, size_t>> items;
     for (size_t s = 0; s < sc.n_stages; s++) {
       const size_t k = sc.poly(t, s, n_polys);
-      if (k == SIZE_MAX) continue;
+      if (k == SIZE_MAX || stage_waits(sc, s) != (grp % 2 == 1)) continue;
       ops.push_back(stage_op(cs[k].get(), sc, s));
       items.emplace_back(k, s);
     }
@@ -1606,7 +1629,7 @@ lcpc_status lcpc_sharded_p2p_schedule(lcpc_field f, size_t n_rows, size_t n_per_
     for (const P2p &x : p2p_plan(nranks, rank, ops)) {
       if (n < cap) {
         lcpc_p2p_record &r = out[n];
-        r.tick = (uint32_t)t;
+        r.tick = (uint32_t)grp;
         r.pos = pos;
         r.poly = (uint32_t)items[x.op].first;
         r.stage = (uint32_t)items[x.op].second;
