@@ -150,6 +150,9 @@ struct lcpc_comm {
   Device *dev = nullptr;
   hipStream_t cs = nullptr;  // the comm stream: every exchange, in issue order
   std::mutex mu;             // one sharded call at a time
+  // the pipelined driver's host threads (transcripts and proofs, compute launches, encodes),
+  // started on its first call and kept across calls: idle between calls, joined last
+  std::unique_ptr<TaskPool> pool, launch, encoder;
   ~lcpc_comm() {
     if (cs) {
       (void)hipStreamSynchronize(cs);
@@ -913,8 +916,11 @@ struct Sched {
 Sched make_sched(size_t ndt, int G, size_t lag, size_t n_polys) {
   Sched sc;
   // ~1.2 ms of absorption per round (cfg3) over ~1.05 ms / G per tick, plus the fold's trip to
-  // the host: lag 3 at one rank measured 10.8-11.0 G/s at K = 20 against 10.3-10.6 with lag 2
-  sc.lag = lag ? lag : 2 + (size_t)G;
+  // the host, plus slack.  One rank at K = 20 (profiles/r03_sharded_lag_sweep.json), two groups
+  // per tick: 10.0-10.7 G/s at lag 3, 10.7-10.8 at 4, 11.0-11.2 at 5 (four runs), 9.4-11.0 at 6;
+  // one group per tick: 9.6-9.9 at lag 2, 10.1-10.5 at 3, 10.7-10.9 at 4.  More hardware queues
+  // (GPU_MAX_HW_QUEUES 8, 16) were slower at every lag.
+  sc.lag = lag ? lag : std::max<size_t>(5, 2 + (size_t)G);
   sc.ndt = ndt;
   sc.rounds = std::max<size_t>(ndt, 1);
   sc.n_stages = 2 + 2 * sc.rounds + 2;
@@ -1335,14 +1341,18 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   // workers, one task per polynomial at a time (a task's launches precede that polynomial's next
   // exchange: the main thread settles it first), so the main thread's tick is the group plus the
   // waits; the root rank's transcript absorptions and the final proofs run on `pool`.
-  const size_t hw = std::max(2u, std::thread::hardware_concurrency());
-  TaskPool pool(std::min<size_t>(16, hw), e->dev->id);
-  TaskPool launch(std::min<size_t>(4, hw), e->dev->id);
-  // every polynomial's encode goes on one stream, issued in polynomial order by one thread: the
-  // encodes finish first come first (on streams of their own they ran side by side and each
-  // commitment's root arrived late), while the short exchange-side and prove kernels run on each
-  // polynomial's own (prove) stream
-  TaskPool encoder(1, e->dev->id);
+  // (every task of a call has finished when it returns, error paths included: fail_all)
+  if (!comm->pool) {
+    const size_t hw = std::max(2u, std::thread::hardware_concurrency());
+    comm->pool = std::make_unique<TaskPool>(std::min<size_t>(16, hw), e->dev->id);
+    comm->launch = std::make_unique<TaskPool>(std::min<size_t>(4, hw), e->dev->id);
+    // every polynomial's encode goes on one stream, issued in polynomial order by one thread:
+    // the encodes finish first come first (on streams of their own they ran side by side and
+    // each commitment's root arrived late), while the short exchange-side and prove kernels run
+    // on each polynomial's own (prove) stream
+    comm->encoder = std::make_unique<TaskPool>(1, e->dev->id);
+  }
+  TaskPool &pool = *comm->pool, &launch = *comm->launch, &encoder = *comm->encoder;
   hipStream_t bulk = e->dev->acquire_stream(shard_all_high());
   if (!bulk) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   struct BulkRelease {  // (destroyed after cs: returns the stream to the pool)
