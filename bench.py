@@ -105,8 +105,8 @@ def parse():
                          "times (s, from the start of the timed region) to this JSON file")
     ap.add_argument("--pipeline", type=int, default=0,
                     help="independent commitments in flight per GPU (host threads); the serial "
-                         "Merlin transcript of one overlaps the kernels of the others.  0: 16, or "
-                         "4 for --code pos (a 1 GiB request's 2.3 GiB codeword per slot: deeper "
+                         "Merlin transcript of one overlaps the kernels of the others.  0: 16, 20 for "
+                         "--code sdig, or 4 for --code pos (a 1 GiB request's 2.3 GiB codeword per slot: deeper "
                          "pipelines only contend for HBM)")
     args = ap.parse_args()
     if args.code in ("sdig", "encode"):
@@ -118,7 +118,9 @@ def parse():
     if args.commit_slots < 0:
         args.commit_slots = {"sdig": 2, "pos": 0}.get(args.code, 4)
     if args.pipeline <= 0:
-        args.pipeline = 4 if args.code == "pos" else 16
+        # sdig: 20, its proofs being 26 ms of host transcript each (K = 20: 5.6-6.05 against
+        # 5.1-5.3 G/s at 16, 4.5-4.9 at 24; tools/evidence/r03/workers_sweep.sh)
+        args.pipeline = {"pos": 4, "sdig": 20}.get(args.code, 16)
     return args
 
 
