@@ -69,6 +69,10 @@ def parse():
                          "max-over-ranks over gloo); prints the JSON line with value null")
     ap.add_argument("--log-len", type=int, default=None, help="log2 coefficients (24; 20 for --code encode)")
     ap.add_argument("--field", default="Ft127")
+    ap.add_argument("--rho", default="1/2",
+                    help="Ligero code rate (LigeroEncodingRho<F, U1, U2>, lcpc-ligero-pc/src/lib.rs:32-37): 1/2 "
+                         "is LigeroEncoding (the BASELINE metric, :189); 1/4 is the reference's commit_bench "
+                         "(lcpc-ligero-pc/src/bench.rs:43, the 2021 published commit timings)")
     ap.add_argument("--code", choices=["ligero", "sdig", "pos", "encode"], default="ligero",
                     help="ligero: R-S / NTT rows (the BASELINE metric, cfg3); sdig: Brakedown "
                          "SdigCode3 expander code, seed 0 (cfg4); pos: proof-of-storage request "
@@ -115,6 +119,8 @@ def parse():
         args.mode = "sharded" if args.gpus > 1 else "replicas"
     if args.log_len is None:
         args.log_len = 20 if args.code == "encode" else 24
+    num, den = (int(x) for x in args.rho.split("/"))
+    args.rho_t = (num, den)
     if args.commit_slots < 0:
         args.commit_slots = {"sdig": 2, "pos": 0}.get(args.code, 4)
     if args.pipeline <= 0:
@@ -219,6 +225,11 @@ class Workload:
         self.__dict__.update(kw)
 
 
+def rho_note(args):
+    """the metric name of a non-default rate (the BASELINE metric is rho = 1/2)"""
+    return "" if args.rho == "1/2" else f", rho={args.rho}"
+
+
 def ligero_or_sdig(args, L, torch, rank, local_rank):
     """cfg3 (Ligero, the BASELINE metric) and cfg4 (Brakedown SdigCode3, seed 0): commit + open
     of one polynomial (lcpc-2d/src/lib.rs:651-700, 1034-1123)."""
@@ -226,7 +237,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
     nl = L.limbs(fid)
     n = 1 << args.log_len
     sdig = args.code == "sdig"
-    enc = L.SdigEncoding.new(fid, n, 0) if sdig else L.LigeroEncoding.new(fid, n)
+    enc = L.SdigEncoding.new(fid, n, 0) if sdig else L.LigeroEncoding.new(fid, n, args.rho_t)
     n_rows, n_per_row, n_cols = enc.get_dims(n)
     nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
     # synthetic inputs (host RNG of the product library), then resident in HBM
@@ -282,7 +293,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
 
     def cpu_baseline(O):
         o_enc = (O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3) if sdig
-                 else O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt))
+                 else O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt, rho=args.rho_t))
         t1 = time.perf_counter()
         oc = O.Commit(o_enc, coeffs.reshape(-1))
         op = oc.prove(o_enc, outer.reshape(-1), O.standard_transcript(nco, oc.root()))
@@ -315,11 +326,11 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
 
     B = 8 * nl
     name = (f"Brakedown (SdigCode3, seed 0) commit+open, {args.field}, 2^{args.log_len} coeffs, " if sdig
-            else f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho=1/2, ")
+            else f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho={args.rho}, ")
     return Workload(
         units=n, unit="field-elements/s", bytes_per_unit=B,
         metric=("committed field-elements/s (commit+open), 2^24-coeff Brakedown (cfg4)" if sdig else
-                "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU"),
+                "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU" + rho_note(args)),
         dtype=f"u64x{nl} ({args.field} Montgomery limbs)",
         data=f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), resident in HBM",
         config={"workload": name + f"{n_rows}x{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, "
@@ -350,7 +361,7 @@ def encode_workload(args, L, torch, rank, local_rank):
     fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
     nl = L.limbs(fid)
     n = 1 << args.log_len
-    enc = L.LigeroEncoding.new(fid, n)
+    enc = L.LigeroEncoding.new(fid, n, args.rho_t)
     n_rows, n_per_row, n_cols = enc.get_dims(n)
     coeffs = L.field_random(fid, n_rows * n_per_row, replica_seed(rank))
     dev = f"cuda:{local_rank}"
@@ -456,6 +467,17 @@ def pos_workload(args, L, torch, rank, local_rank):
         return dt * n_bytes / len(sample), None, (f"commit + u^T Enc(M) of the first 1/16 of the file "
                                                   f"({len(sample)} B, {dt:.2f} s), scaled to the whole file")
 
+    def parity(O):
+        """one request of this workload (untimed) against the oracle's answer on the whole file"""
+        d_el = slots[0]
+        rc = lib.lcpc_pos_bytes_to_field_device(d_bytes.data_ptr(), n_bytes, d_el.data_ptr(), None)
+        if rc:
+            raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
+        c = L.LcCommit.commit_device(d_el.data_ptr(), n_rows * np_, enc)
+        ev = P.verifiable_polynomial_evaluation(c, left)
+        opened = c.open_columns(cols)
+        return pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, c.get_root(), ev, opened)
+
     return Workload(
         units=n_el, unit="field-elements/s", bytes_per_unit=8,
         metric="proof-of-storage server request: committed field-elements/s (pack+commit+eval+256-col open), "
@@ -465,7 +487,7 @@ def pos_workload(args, L, torch, rank, local_rank):
         config={"workload": f"PoS request on a {n_bytes}-byte file: {n_el} WriteableFt63 elements, default "
                             f"dims {n_rows}x{np_}->{nc}, u^T Enc(M) at a point, 256 opened columns",
                 "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd},
-        step=step, cpu_baseline=cpu_baseline,
+        step=step, cpu_baseline=cpu_baseline, parity=parity,
         enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)",
         algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
@@ -626,7 +648,7 @@ def ligero_sharded(args, L, torch, dist, rank, world, device, backend, share):
     fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
     nl = L.limbs(fid)
     n = 1 << args.log_len
-    enc = L.LigeroEncoding.new(fid, n)
+    enc = L.LigeroEncoding.new(fid, n, args.rho_t)
     n_rows, n_per_row, n_cols = enc.get_dims(n)
     nco, ndt = enc.get_n_col_opens(), enc.get_n_degree_tests()
     coeffs = L.field_random(fid, n, SEED)                    # one polynomial; rank g keeps its rows
@@ -689,6 +711,10 @@ def main():
     if args.plumbing_only:
         sys.exit(plumbing_check(args, rank, world))
     os.environ["LCPC_STREAM_MODE"] = args.stream_mode  # read when the library creates streams
+    # the sharded calls' watchdog (off in the library by default): a rank whose exchanges stop for
+    # two minutes reports the tick and its peers and exits, instead of holding the run until the
+    # driver's own limit
+    os.environ.setdefault("LCPC_SHARD_WATCHDOG_S", "120")
     import torch
 
     # LCPC_BENCH_BACKEND=gloo with LCPC_BENCH_SHARE_GPU=1 rehearses N ranks on one GPU (a
@@ -727,13 +753,21 @@ def main():
         elif world == 1 and args.code == "ligero" and args.sharded_n1 == 1:
             sharded_n1 = sharded_n1_child(args)
     if sharded_n1 is not None:
+        # the sharded engine commits the same polynomial (seed SEED) as replica 0: its root must
+        # be the replicas' and the oracle's
+        sharded_n1["root_equals_replicas"] = sharded_n1.get("root") == out.get("root")
         out["sharded_n1"] = sharded_n1
+        if "parity_ok" in out and sharded_n1.get("root") is not None:
+            out["parity_ok"] = bool(out["parity_ok"] and sharded_n1["root_equals_replicas"])
     if rank == 0:
         out["world_formed"] = formed
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and out.get("parity_ok") is False:
+        print("bench.py: the run's answers differ from the oracle's (see the parity_* keys)", file=sys.stderr)
+        sys.exit(4)
 
 
 def sharded_n1_child(args):
@@ -767,7 +801,7 @@ def sharded_n1_child(args):
             "ms_per_step": d["ms_per_step"], "scaling": "strong",
             "engine": "lcpc_sharded_commit_prove_many, one rank (no exchanges): the N = 1 point of the "
                       "--mode sharded (--gpus N > 1) curve, timed in a fresh child process",
-            "lag": args.lag or None, "root": d.get("root")}
+            "lag": args.lag or None, "root": d.get("root"), "steps_agree": d.get("steps_agree")}
 
 
 def sharded_n1_figure(args, L, torch, device):
@@ -817,7 +851,8 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
     c1, th1 = os.times(), cgroup_throttle()
     L.prof_enable(False)
     stats = L.prof_stats() if prof_timed else {}
-    assert all(r == roots[0] for r in troots), "timed-region roots differ from the warm-up's"
+    # recorded, not asserted: the line still prints, and main() exits non-zero on a mismatch
+    steps_agree = len(troots) == args.steps and all(r == roots[0] for r in list(troots) + list(roots))
     elapsed = max_over_ranks(dist, elapsed, "cpu" if backend == "gloo" else device)
 
     # one commitment's latency (serial, median of 3) and the roofline launches (HIP events on the
@@ -844,13 +879,13 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
     lat_p.sort()
     value = job_throughput(n, args.steps, 1, elapsed)
     out = {
-        "metric": "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU",
+        "metric": "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU" + rho_note(args),
         "value": value, "unit": "field-elements/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": f"u64x{B // 8} ({args.field} Montgomery limbs)",
         "data": f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x})), one polynomial, each rank's rows "
                 f"resident in its HBM",
-        "config": {"workload": f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho=1/2, {n_rows}x"
+        "config": {"workload": f"Ligero commit+open, {args.field}, 2^{args.log_len} coeffs, rho={args.rho}, {n_rows}x"
                                f"{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, BLAKE3 Merkle",
                    "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                    "n_col_opens": nco, "n_degree_tests": ndt,
@@ -879,6 +914,7 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
         leaf_compressions=leaf_compressions(n_rows, n_cols, B) if world == 1 else 0)
     out.update(roofline_objects(wl, iso, stats, args, traffic_rows_frac=nr / n_rows))
     out["root"] = roots[0].hex()  # (every step commits the same polynomial)
+    out["steps_agree"] = steps_agree
 
     # the verifier (outside the timed region): the serial step's proof, verified again
     if rank == 0 and args.verify_reps > 0 and pf is not None:
@@ -892,12 +928,14 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
     else:
         ev = None
 
-    # CPU baseline: the oracle (C restatement) on the same workload, rank 0 at N = 1
-    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    # CPU baseline and parity: the oracle (C restatement) on the same workload, on rank 0 at EVERY
+    # N (after the timed region), so that an N > 1 line carries its own proof of a right answer:
+    # every timed step's root, the kept warm-up proof and the verifier's value against the oracle's
+    want_cpu = args.cpu_baseline in ("on", "auto")
     if rank == 0 and want_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ffi as O  # checker / CPU baseline only
-        o_enc = O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
+        o_enc = O.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt, rho=args.rho_t)
         keep = {}
 
         def cpu_once(O_):
@@ -916,7 +954,11 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
                                "sample": f"{sample}: median of {len(runs)} runs after a warm-up on {cores} threads "
                                          f"({', '.join(f'{r:.3f}' for r in runs)} s)", "cores_basis": basis}
         out["parity_root_vs_oracle"] = oroot == roots[0]
+        out["parity_steps_vs_oracle"] = {"steps": len(troots) + len(roots),
+                                         "equal": sum(r == oroot for r in list(troots) + list(roots)),
+                                         "what": "every warm-up and timed step's root against the oracle's"}
         op = keep["op"]
+        out["parity_proof_vs_oracle"] = False
         if warm_proof is not None:
             out["parity_proof_vs_oracle"] = bool(
                 np.array_equal(warm_proof.p_eval.reshape(-1), op.p_eval)
@@ -929,12 +971,16 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
                                 O.standard_transcript(nco, keep["oc"].root()))
             out["verify"]["cpu_ms"] = 1e3 * (time.perf_counter() - t2)
             out["verify"]["parity_vs_oracle"] = bool(rc == 0 and np.array_equal(np.asarray(ev).reshape(-1), oev))
-        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto"):
+        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and world == 1):
             O.lib().of_set_threads(1)
             dt1, oroot1, sample1 = cpu_once(O)
             out["cpu_baseline_1core"] = {"value": n / dt1, "unit": "field-elements/s", "cores": 1, "kind": "port",
                                          "sample": f"{sample1}: one run on 1 thread ({dt1:.2f} s)"}
             out["parity_root_vs_oracle"] = out["parity_root_vs_oracle"] and oroot1 == roots[0]
+        ps = out["parity_steps_vs_oracle"]
+        out["parity_ok"] = bool(steps_agree and out["parity_root_vs_oracle"] and ps["equal"] == ps["steps"]
+                                and out["parity_proof_vs_oracle"]
+                                and out.get("verify", {}).get("parity_vs_oracle", True))
     return out
 
 
@@ -988,9 +1034,10 @@ def run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share):
     L.prof_enable(False)
     barrier()
     t0 = time.perf_counter()
+    troots = []
     for _ in range(args.steps):
         r_, _ = step()
-        assert r_ == root, "nondeterministic root across steps"
+        troots.append(r_)
     barrier()
     elapsed = max_over_ranks(dist, time.perf_counter() - t0, "cpu" if backend == "gloo" else device)
     iso = {}
@@ -1023,30 +1070,52 @@ def run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share):
                   mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass "
                             "twiddles per row", leaf_compressions=0)
     out.update(roofline_objects(wl, iso, {}, args, traffic_rows_frac=nr / n_rows))
-    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    out["steps_agree"] = all(r == root for r in troots)
+    want_cpu = args.cpu_baseline in ("on", "auto")
     if rank == 0:
-        # parity of this run's answers against the oracle on a bounded sample is the replicas
-        # line's job (bench.py --code pos); here the root and the request's digests are reported
         import hashlib
         ev, opened = res0
         out["answer_digests"] = {"root": root.hex(), "eval_sha256": hashlib.sha256(ev.tobytes()).hexdigest(),
                                  "cols_sha256": hashlib.sha256(b"".join(o.col.tobytes() for o in opened)).hexdigest()}
     if rank == 0 and want_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_ffi as O  # CPU baseline only
-        sample = host[: n_bytes // 16]
-        el = O.pos_bytes_to_field(sample.tobytes())
+        import oracle_ffi as O  # CPU baseline and parity only
         o_enc = O.Encoding.ligero(0, np_, nc)
         cores, basis = available_cores()
         O.lib().of_set_threads(cores)
+        # timed sample: the first 1/16 of the file, scaled to the whole
+        sample = host[: n_bytes // 16]
+        el = O.pos_bytes_to_field(sample.tobytes())
         t1 = time.perf_counter()
         oc = O.Commit(o_enc, el)
         O.collapse(0, oc.comm, O.pos_side_vectors(0, x.reshape(-1), oc.n_rows, nc)[0], oc.n_rows, nc)
         dt = (time.perf_counter() - t1) * 16
+        del oc
         out["cpu_baseline"] = {"value": n_el / dt, "unit": "field-elements/s", "cores": cores, "kind": "port",
                                "sample": f"commit + u^T Enc(M) of the first 1/16 of the file, scaled to the whole "
                                          f"file ({dt / 16:.2f} s)", "cores_basis": basis}
+        out.update(pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, root, ev, opened))
+        out["parity_ok"] = bool(out["steps_agree"] and out["parity_root_vs_oracle"]
+                                and out["parity_eval_vs_oracle"] and out["parity_cols_vs_oracle"])
     return out
+
+
+def pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, root, ev, opened):
+    """The oracle's answer to the same proof-of-storage request on the WHOLE file (untimed): the
+    root, u^T Enc(M) and the opened columns with their Merkle paths (lcpc_online.rs:80-239,
+    454-484), against this run's answer."""
+    oc = O.Commit(O.Encoding.ligero(0, np_, nc), O.pos_bytes_to_field(host.tobytes()))
+    m = oc.comm.reshape(n_rows, nc)
+    ohash = bytes(oc.hashes)
+    return {
+        "parity_root_vs_oracle": root == oc.root(),
+        "parity_eval_vs_oracle": bool(np.array_equal(np.asarray(ev).reshape(-1),
+                                                     O.collapse(0, oc.comm, left.reshape(-1), n_rows, nc))),
+        "parity_cols_vs_oracle": bool(
+            all(np.array_equal(o.col.reshape(-1), m[:, c]) for c, o in zip(cols, opened))
+            and all(O.verify_path(ohash[32 * c:32 * c + 32], c, b"".join(o.path), oc.root())
+                    for c, o in zip(cols, opened))),
+        "parity_what": "the oracle's commit + u^T Enc(M) + columns and paths of the whole file, untimed"}
 
 
 # ---------------------------------------------------------------- the replica engine
@@ -1118,7 +1187,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     if errors:
         raise errors[0]
     root = roots[-1] if roots else None
-    assert all(r == root for r in roots), "nondeterministic root across steps"
+    steps_agree = len(roots) == args.steps and all(r == root for r in roots)
     barrier()
     elapsed = time.perf_counter() - t0
     c1, th1 = os.times(), cgroup_throttle()
@@ -1166,7 +1235,10 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
         vms, gev = wl.verify_bench(args.verify_reps)
         out["verify"] = {"ms": vms, "reps": args.verify_reps,
                          "what": "LcEvalProof::verify of one proof of this workload (host + GPU, serial)"}
-    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    if root is not None:
+        out["root"] = root.hex()
+    out["steps_agree"] = steps_agree
+    want_cpu = args.cpu_baseline in ("on", "auto")  # rank 0's polynomial, at every N
     if rank == 0 and want_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ffi as O  # checker / CPU baseline only
@@ -1184,7 +1256,8 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
             out["parity_vs_oracle"] = bool(oroot)
         elif oroot is not None:
             out["parity_root_vs_oracle"] = oroot == root if root is not None else None
-        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and args.code == "ligero"):
+        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and args.code == "ligero"
+                                               and world == 1):
             O.lib().of_set_threads(1)
             cpu1_s, oroot1, sample1 = wl.cpu_baseline(O)
             out["cpu_baseline_1core"] = {"value": wl.units / cpu1_s, "unit": wl.unit, "cores": 1, "kind": "port",
@@ -1197,6 +1270,14 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
         out["verify"]["parity_vs_oracle"] = bool(all(a for _, a, _ in cv) and gev is not None and
                                                  np.array_equal(np.asarray(cv[-1][2]).reshape(-1),
                                                                 np.asarray(gev).reshape(-1)))
+    if rank == 0 and want_cpu and getattr(wl, "parity", None):
+        out.update(wl.parity(O))
+    if rank == 0 and want_cpu:
+        flags = [out[k] for k in ("parity_root_vs_oracle", "parity_vs_oracle", "parity_eval_vs_oracle",
+                                  "parity_cols_vs_oracle") if k in out]
+        if "parity_vs_oracle" in out.get("verify", {}):
+            flags.append(out["verify"]["parity_vs_oracle"])
+        out["parity_ok"] = bool(steps_agree and flags and all(f is True for f in flags))
     return out
 
 

@@ -25,6 +25,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <array>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -153,11 +154,15 @@ struct lcpc_comm {
   // the pipelined driver's host threads (transcripts and proofs, compute launches, encodes),
   // started on its first call and kept across calls: idle between calls, joined last
   std::unique_ptr<TaskPool> pool, launch, encoder;
+  // the per-(polynomial, stage) events of finished polynomials, for reuse (ev_take / ev_give)
+  std::mutex ev_mu;
+  std::vector<hipEvent_t> ev_free;
   ~lcpc_comm() {
     if (cs) {
       (void)hipStreamSynchronize(cs);
       (void)hipStreamDestroy(cs);
     }
+    for (hipEvent_t e : ev_free) (void)hipEventDestroy(e);
     if (nc) rccl().CommDestroy(nc);
   }
 };
@@ -361,6 +366,16 @@ struct HostBuf {
 }  // namespace
 
 // ---------------------------------------------------------------- one polynomial's shard state
+// stages of one polynomial: 0 chaining values, 1 subtrees, 2 + 2r / 3 + 2r round r's tensor
+// broadcast / partial gather, then the column indices and the column gather (make_sched); the
+// proof-of-storage request's two gathers take the last two slots
+constexpr size_t kMaxStages = 64;
+enum EvKind { EV_READY = 0, EV_DONE = 1, EV_HOST = 2 };
+constexpr size_t kPosEvalStage = kMaxStages - 2, kPosColsStage = kMaxStages - 1;
+enum { S_CV = 0, S_SUB = 1, S_R0 = 2 };
+constexpr size_t st_bcast(size_t r) { return S_R0 + 2 * r; }
+constexpr size_t st_gather(size_t r) { return S_R0 + 2 * r + 1; }
+
 struct lcpc_sharded_commit {
   const lcpc_encoding *e = nullptr;
   lcpc_comm *comm = nullptr;
@@ -373,12 +388,21 @@ struct lcpc_sharded_commit {
                                   // pipelined driver's polynomials: encodes finish first come first)
   bool own_s = true;              // s is this polynomial's own (released with it)
   hipStream_t sp = nullptr;       // its exchange-side and prove stream (short kernels, beside the encodes)
-  hipEvent_t ev_ready = nullptr;  // send data of the next exchange written
-  hipEvent_t ev_done = nullptr;   // the last exchange completed (comm stream)
-  hipEvent_t ev_host = nullptr;   // device -> host copies of the last stage landed
+  // One event per (stage, edge), recorded at most once per call: EV_READY = the stage's send data
+  // written (producer stream -> comm stream), EV_DONE = the stage's exchange completed (comm
+  // stream -> consumer stream), EV_HOST = the stage's device -> host copies landed.  No event is
+  // re-recorded while a wait on an earlier record of it may still be queued (the pattern the
+  // round-3 eight-rank wrong-root failure pointed at; DESIGN.md §6, "Hand-offs").  Created when a
+  // call first needs a stage (ev_need), returned to the communicator's free list with the
+  // polynomial once every wait on them has retired (ev_quiet), destroyed otherwise.
+  std::array<hipEvent_t, 3 * kMaxStages> ev{};
+  bool ev_quiet = true;  // no exchange of this polynomial is outstanding on the comm stream
   DBuf coeffs, comm_rows, hashes;  // kept for prove
   DBuf cv_send, cv_recv, sub, subs, sdig_tmp;  // commit scratch
   uint8_t root[32] = {0};
+  const void *d_rows = nullptr;  // the caller's rows (LCPC_SHARD_DEBUG's recomputation)
+  uint64_t rows_fnv = 0;         // (LCPC_SHARD_DEBUG) their digest when the encode was issued
+  size_t poly = 0;               // index in a pipelined call (LCPC_SHARD_DEBUG)
   // prove state
   int root_rank = 0;
   size_t ndt = 0, nco = 0, rounds = 0;
@@ -392,9 +416,17 @@ struct lcpc_sharded_commit {
     if (s && own_s) (void)hipStreamSynchronize(s);
     if (sp && sp != s) (void)hipStreamSynchronize(sp);
     if (own_tr) delete tr;
-    if (ev_ready) (void)hipEventDestroy(ev_ready);
-    if (ev_done) (void)hipEventDestroy(ev_done);
-    if (ev_host) (void)hipEventDestroy(ev_host);
+    std::vector<hipEvent_t> mine;
+    for (hipEvent_t &x : ev)
+      if (x) mine.push_back(x), x = nullptr;
+    if (!mine.empty()) {
+      if (comm && ev_quiet) {
+        std::lock_guard<std::mutex> lk(comm->ev_mu);
+        comm->ev_free.insert(comm->ev_free.end(), mine.begin(), mine.end());
+      } else {
+        for (hipEvent_t x : mine) (void)hipEventDestroy(x);  // (HIP keeps a queued wait's marker alive)
+      }
+    }
     // DBufs drain s in their destructors (declared after s, destroyed before it is released)
   }
 };
@@ -413,12 +445,21 @@ namespace {
 // one-rank K = 20 rate on one box: 3 (default) every stream of the driver high priority, 10.1-10.3
 // G/s; 1 every stream normal priority, 8.5-9.0; 0 the prove work on the encode stream, 9.5-10.2;
 // 2 the old mixed priorities, 10.1-11.1 (unsafe).
+std::atomic<int> g_prio_override{-1};  // set once a multi-rank communicator rejects mode 2
 int shard_prove_stream_mode() {
   static const int v = [] {
     const char *e = getenv("LCPC_SHARD_PRIO");
     return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 3;
   }();
-  return v;
+  const int o = g_prio_override.load(std::memory_order_relaxed);
+  return o >= 0 ? o : v;
+}
+// mode 2 across ranks only for A/B runs that ask for it (LCPC_SHARD_PRIO_AB=1): otherwise a
+// multi-rank communicator falls back to mode 3 with a warning (check_shardable)
+bool shard_mode2_allowed(int nranks) {
+  if (shard_prove_stream_mode() != 2 || nranks <= 1) return true;
+  const char *e = getenv("LCPC_SHARD_PRIO_AB");
+  return e && e[0] == '1';
 }
 bool shard_prio_streams() { return shard_prove_stream_mode() != 0; }
 // (3: every stream of the driver -- encode, exchange, prove -- at high priority)
@@ -493,6 +534,8 @@ void prove_geom(lcpc_sharded_commit *c, size_t ndt, size_t nco, int root_rank) {
 
 // bulk: a stream the caller owns for the encode (the pipelined driver's shared one), or null for
 // a stream of this commitment's own
+lcpc_status ev_need(lcpc_sharded_commit *c, size_t s0, size_t s1);
+
 lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, ShardPtr &out,
                        hipStream_t bulk = nullptr) {
   ShardPtr c(new lcpc_sharded_commit());
@@ -506,11 +549,8 @@ lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, S
   if (!c->s) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   c->sp = shard_prio_streams() ? c->dev->acquire_stream(shard_prove_high()) : c->s;
   if (!c->sp) return fail(LCPC_ERR_DEVICE, "no HIP stream");
-  HIP_TRY(hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&c->ev_host, hipEventDisableTiming));
   out = std::move(c);
-  return LCPC_OK;
+  return ev_need(out.get(), 0, 2);  // (the commit's stages: chaining values, subtrees)
 }
 
 // DBuf allocations drain the polynomial's stream (not the caller's lease) when released: the
@@ -525,9 +565,34 @@ hipError_t salloc_on(lcpc_sharded_commit *c, DBuf &b, size_t bytes, hipStream_t 
 hipError_t salloc(lcpc_sharded_commit *c, DBuf &b, size_t bytes) { return salloc_on(c, b, bytes, c->s); }
 hipError_t salloc_p(lcpc_sharded_commit *c, DBuf &b, size_t bytes) { return salloc_on(c, b, bytes, c->sp); }
 
+// ---- per-(stage, edge) events
+// the event of stage s's edge `k` (created by ev_need before the call's first use)
+hipEvent_t EV(const lcpc_sharded_commit *c, EvKind k, size_t s) { return c->ev[3 * s + k]; }
+
+// make sure the three events of stages [s0, s1) exist (from the communicator's free list first)
+lcpc_status ev_need(lcpc_sharded_commit *c, size_t s0, size_t s1) {
+  if (s1 > kMaxStages) return fail(LCPC_ERR_UNSUPPORTED, "row shards: too many prove stages");
+  for (size_t i = 3 * s0; i < 3 * s1; i++) {
+    if (c->ev[i]) continue;
+    {
+      std::lock_guard<std::mutex> lk(c->comm->ev_mu);
+      if (!c->comm->ev_free.empty()) {
+        c->ev[i] = c->comm->ev_free.back();
+        c->comm->ev_free.pop_back();
+        continue;
+      }
+    }
+    HIP_TRY(hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming));
+  }
+  return LCPC_OK;
+}
+
 // ---- commit
 // encode this rank's rows (the first NTT pass writes the commitment's own coefficient copy),
 // chaining values of its chunks of every column, laid out [dest rank][chunk][block col]
+bool shard_debug();
+uint64_t debug_fnv_device(const void *d, size_t n);
+
 lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
   const Part &pm = c->part[c->me];
   const size_t nch = pm.c_hi - pm.c_lo, wb = c->wb;
@@ -536,6 +601,8 @@ lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
   HIP_TRY(salloc(c, c->cv_send, nch * c->np2 * 32 + 16));
   if (c->G > 1) HIP_TRY(salloc(c, c->cv_recv, c->n_chunks * c->B * 32 + 16));  // (one rank: cv_send itself)
   if (c->nr && !d_rows) return fail(LCPC_ERR_INVALID_ARG, "null rows");
+  c->d_rows = d_rows;
+  if (shard_debug() && c->nr) c->rows_fnv = debug_fnv_device(d_rows, c->nr * c->np * c->wb);
   if (c->nr && c->sdig) {
     // Brakedown rows (lcpc-brakedown-pc/src/encode.rs:36-94, independent per row): this rank's
     // rows transposed to the element-major shard [n_cols][nr] as canonical values (one pass also
@@ -554,7 +621,7 @@ lcpc_status stage_pre_commit(lcpc_sharded_commit *c, const void *d_rows) {
     HIP_TRY(leaf_chunk_cvs(c->fid, c->comm_rows.as<uint32_t>(), pm.r_lo, c->n_rows, c->nc, c->sdig ? 1 : c->nc,
                            pm.c_lo, pm.c_hi, c->cv_send.as<uint32_t>(), c->s, true, c->B,
                            c->sdig ? c->nr : 1));
-  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  HIP_TRY(hipEventRecord(EV(c, EV_READY, S_CV), c->s));
   return LCPC_OK;
 }
 
@@ -566,7 +633,7 @@ Xop op_cv_exchange(lcpc_sharded_commit *c) {
   op.sb.assign(c->G, nch_me * c->B * 32);
   op.rb.resize(c->G);
   for (int k = 0; k < c->G; k++) op.rb[k] = (c->part[k].c_hi - c->part[k].c_lo) * c->B * 32;
-  op.ready = c->ev_ready;
+  op.ready = EV(c, EV_READY, S_CV);
   op.s = c->sp;  // (one rank: where the post stage waits for the encode)
   return op;
 }
@@ -574,7 +641,7 @@ Xop op_cv_exchange(lcpc_sharded_commit *c) {
 // leaves of my column block from all chunks' chaining values, and the block's subtree (the
 // commit's short latency-critical kernels go on the prove stream, ahead of bulk encodes)
 lcpc_status stage_post_cv(lcpc_sharded_commit *c) {
-  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, EV(c, EV_DONE, S_CV), 0));
   HIP_TRY(salloc_p(c, c->sub, (2 * c->B - 1) * 32));
   uint32_t *cvs = (c->G > 1 ? c->cv_recv : c->cv_send).as<uint32_t>();
   HIP_TRY(leaves_from_cvs(cvs, c->B, (int)c->n_chunks, c->sub.as<uint8_t>(), c->sp));
@@ -583,7 +650,7 @@ lcpc_status stage_post_cv(lcpc_sharded_commit *c) {
   if (valid < c->B) HIP_TRY(hipMemsetAsync(c->sub.as<uint8_t>() + valid * 32, 0, (c->B - valid) * 32, c->sp));
   if (c->B > 1) HIP_TRY(merkle_tree(c->sub.as<uint8_t>(), c->B, c->sp));
   if (c->G > 1) HIP_TRY(salloc_p(c, c->subs, (size_t)c->G * (2 * c->B - 1) * 32));  // (one rank: sub itself)
-  HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
+  HIP_TRY(hipEventRecord(EV(c, EV_READY, S_SUB), c->sp));
   return LCPC_OK;
 }
 
@@ -592,14 +659,14 @@ Xop op_subtree_exchange(lcpc_sharded_commit *c) {
   op.send = c->sub.as<uint8_t>();
   op.recv = (c->G > 1 ? c->subs : c->sub).as<uint8_t>();
   op.bytes = (2 * c->B - 1) * 32;
-  op.ready = c->ev_ready;
+  op.ready = EV(c, EV_READY, S_SUB);
   op.s = c->sp;
   return op;
 }
 
 // every rank: the whole tree [leaves | level 1 | ... | root] from the G subtrees + top levels
 lcpc_status stage_post_subtrees(lcpc_sharded_commit *c) {
-  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, EV(c, EV_DONE, S_SUB), 0));
   const size_t nc = c->np2, B = c->B, G = c->G;  // (the tree's leaf count)
   HIP_TRY(salloc_p(c, c->hashes, (2 * nc - 1) * 32));
   uint8_t *h = c->hashes.as<uint8_t>();
@@ -608,15 +675,103 @@ lcpc_status stage_post_subtrees(lcpc_sharded_commit *c) {
   lcpc_status st = c->h_root.get(c->dev, 32);
   if (st) return st;
   HIP_TRY(d2h(c->h_root.p, h + (2 * nc - 2) * 32, 32, c->sp));
-  HIP_TRY(hipEventRecord(c->ev_host, c->sp));
+  HIP_TRY(hipEventRecord(EV(c, EV_HOST, S_SUB), c->sp));
   return LCPC_OK;
+}
+
+// LCPC_SHARD_DEBUG=1 (diagnostic runs only): once a commitment's root is on the host, recompute
+// this rank's encode and chunk chaining values from its rows on a private stream and print, per
+// (rank, polynomial), whether the codeword shard and the sent chaining values match, with the
+// first words of this rank's subtree root and of every gathered subtree: localises a wrong root
+// to the encode, the chaining values, the exchange, or the subtree stage.
+bool shard_debug() {
+  static const bool v = [] {
+    const char *e = getenv("LCPC_SHARD_DEBUG");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+uint64_t debug_fnv(const uint8_t *p, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 1099511628211ull;
+  return h;
+}
+
+uint64_t debug_fnv_device(const void *d, size_t n) {
+  std::vector<uint8_t> h(n);
+  if (n) (void)hipMemcpy(h.data(), d, n, hipMemcpyDeviceToHost);
+  return debug_fnv(h.data(), n);
+}
+
+void debug_commit(lcpc_sharded_commit *c) {
+  if (c->sdig || c->G == 1) return;
+  auto fetch = [](const void *d, size_t n) {
+    std::vector<uint8_t> h(n);
+    if (n) (void)hipMemcpy(h.data(), d, n, hipMemcpyDeviceToHost);
+    return h;
+  };
+  const Part &pm = c->part[c->me];
+  const size_t nch = pm.c_hi - pm.c_lo, wb = c->wb;
+  const size_t cvb = nch * c->np2 * 32;
+  hipStream_t ds = nullptr;
+  (void)hipStreamCreateWithFlags(&ds, hipStreamNonBlocking);
+  void *tc = nullptr, *tk = nullptr, *tv = nullptr;
+  (void)hipMalloc(&tc, c->nr * c->nc * wb + 16);
+  (void)hipMalloc(&tk, c->nr * c->np * wb + 16);
+  (void)hipMalloc(&tv, cvb + 16);
+  if (c->nr)
+    (void)ntt_rows(c->e->plan, (const uint32_t *)c->d_rows, c->np, c->np, (uint32_t *)tc, c->nc, c->nr, ds,
+                   (uint32_t *)tk, c->np, true);
+  if (nch)
+    (void)leaf_chunk_cvs(c->fid, (const uint32_t *)tc, pm.r_lo, c->n_rows, c->nc, c->nc, pm.c_lo, pm.c_hi,
+                         (uint32_t *)tv, ds, true, c->B, 1);
+  (void)hipStreamSynchronize(ds);
+  const auto rows = fetch(c->comm_rows.p, c->nr * c->nc * wb), rows2 = fetch(tc, c->nr * c->nc * wb);
+  // a second recomputation, and the input rows' digest against the one taken at issue time
+  if (c->nr) {
+    (void)hipMemsetAsync(tc, 0, c->nr * c->nc * wb, ds);
+    (void)ntt_rows(c->e->plan, (const uint32_t *)c->d_rows, c->np, c->np, (uint32_t *)tc, c->nc, c->nr, ds,
+                   (uint32_t *)tk, c->np, true);
+    (void)hipStreamSynchronize(ds);
+  }
+  const auto rows3 = fetch(tc, c->nr * c->nc * wb);
+  const bool input_same = !c->nr || debug_fnv_device(c->d_rows, c->nr * c->np * wb) == c->rows_fnv;
+  const auto cvs = fetch(c->cv_send.p, cvb), cvs2 = fetch(tv, cvb);
+  const auto sub = fetch(c->sub.p, (2 * c->B - 1) * 32);
+  const auto subs = fetch(c->subs.p, (size_t)c->G * (2 * c->B - 1) * 32);
+  std::string per_dest;
+  for (int q = 0; q < c->G; q++) {
+    const size_t o = (size_t)q * nch * c->B * 32, n = nch * c->B * 32;
+    per_dest += std::memcmp(cvs.data() + o, cvs2.data() + o, n) ? "X" : ".";
+  }
+  auto w4 = [](const uint8_t *p) {
+    char b[9];
+    snprintf(b, sizeof b, "%02x%02x%02x%02x", p[0], p[1], p[2], p[3]);
+    return std::string(b);
+  };
+  std::string gathered;
+  for (int q = 0; q < c->G; q++) gathered += " " + w4(subs.data() + ((size_t)q * (2 * c->B - 1) + 2 * c->B - 2) * 32);
+  fprintf(stderr,
+          "liblcpc_mi dbg: rank %d poly %zu rows %s cv_send %s (per dest %s) recompute2 %s input %s sub %s gathered%s "
+          "root %s\n",
+          c->me, c->poly, rows == rows2 ? "ok" : "DIFF", cvs == cvs2 ? "ok" : "DIFF", per_dest.c_str(),
+          rows3 == rows2 ? "same" : "DIFFERS", input_same ? "unchanged" : "CHANGED",
+          w4(sub.data() + (2 * c->B - 2) * 32).c_str(), gathered.c_str(), w4(c->root).c_str());
+  fflush(stderr);
+  (void)hipFree(tc);
+  (void)hipFree(tk);
+  (void)hipFree(tv);
+  (void)hipStreamDestroy(ds);
 }
 
 // commit scratch no longer needed once the root is known
 lcpc_status finish_commit(lcpc_sharded_commit *c) {
-  HIP_TRY(hipEventSynchronize(c->ev_host));
+  HIP_TRY(hipEventSynchronize(EV(c, EV_HOST, S_SUB)));
+  c->ev_quiet = true;  // (every exchange of the commit precedes it)
   std::memcpy(c->root, c->h_root.p, 32);
-  // every use of the commit scratch precedes ev_host on the stream: no drain on release
+  if (shard_debug()) debug_commit(c);
+  // every use of the commit scratch precedes the subtree stage's EV_HOST: no drain on release
   for (DBuf *b : {&c->cv_send, &c->cv_recv, &c->sub, &c->subs, &c->sdig_tmp}) b->settle();
   c->sdig_tmp.reset();
   c->cv_send.reset();
@@ -633,6 +788,7 @@ lcpc_status prove_alloc(lcpc_sharded_commit *c, const uint64_t *outer, int root_
   prove_geom(c, pe->n_degree_tests, pe->n_col_opens, root_rank);
   const size_t wb = c->wb, np = c->np;
   lcpc_status st;
+  if ((st = ev_need(c, S_R0, S_R0 + 2 * c->rounds + 2))) return st;
   HIP_TRY(salloc_p(c, c->bt, c->n_rows * wb));
   HIP_TRY(salloc_p(c, c->tens, 2 * std::max<size_t>(c->nr, 1) * wb));
   HIP_TRY(salloc_p(c, c->part_d, 2 * np * wb));
@@ -707,7 +863,7 @@ lcpc_status stage_tensor_upload(lcpc_sharded_commit *c, size_t r) {
 
 // partial row combinations over my rows: [t_r slice | outer slice] (round 0) or t_r slice
 lcpc_status stage_collapse(lcpc_sharded_commit *c, size_t r) {
-  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, EV(c, EV_DONE, st_bcast(r)), 0));
   const size_t wb = c->wb, np = c->np, nr = c->nr;
   const int nt = round_tensors(c, r);
   const bool eval_only = c->ndt == 0;  // round 0 = the evaluation tensor alone
@@ -723,7 +879,7 @@ lcpc_status stage_collapse(lcpc_sharded_commit *c, size_t r) {
     HIP_TRY(collapse_rows(c->fid, c->coeffs.as<uint32_t>(), nr, np, tens, nt, c->part_d.as<uint32_t>(), c->scratch.p,
                           c->sp));
   }
-  HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
+  HIP_TRY(hipEventRecord(EV(c, EV_READY, st_gather(r)), c->sp));
   return LCPC_OK;
 }
 
@@ -736,7 +892,7 @@ Xop op_partial_gather(lcpc_sharded_commit *c, size_t r) {
   op.rb.assign(c->G, 0);
   op.sb[c->root_rank] = bytes;
   if (c->me == c->root_rank) op.rb.assign(c->G, bytes);
-  op.ready = c->ev_ready;
+  op.ready = EV(c, EV_READY, st_gather(r));
   op.s = c->sp;
   return op;
 }
@@ -745,14 +901,14 @@ Xop op_partial_gather(lcpc_sharded_commit *c, size_t r) {
 // transcript) to the host
 lcpc_status stage_fold(lcpc_sharded_commit *c, size_t r) {
   if (c->me != c->root_rank) return LCPC_OK;
-  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, EV(c, EV_DONE, st_gather(r)), 0));
   const size_t wb = c->wb, np = c->np;
   const size_t len = (size_t)round_tensors(c, r) * np;
   HIP_TRY(collapse_fold_rows(c->fid, c->allpart.as<uint32_t>(), c->G, len, c->sum.as<uint32_t>(), c->sp));
   HIP_TRY(convert(c->fid, c->sum.as<uint32_t>(), c->canon.as<uint32_t>(), len, false, c->sp));
   HIP_TRY(d2h(c->h_sum.p, c->sum.p, len * wb, c->sp));
   HIP_TRY(d2h(c->h_repr.p, c->canon.p, len * wb, c->sp));
-  HIP_TRY(hipEventRecord(c->ev_host, c->sp));
+  HIP_TRY(hipEventRecord(EV(c, EV_HOST, st_gather(r)), c->sp));
   return LCPC_OK;
 }
 
@@ -766,7 +922,7 @@ void repr_order(int fid, uint8_t *h, size_t n, int wb) {
 lcpc_status host_absorb(lcpc_sharded_commit *c, size_t r) {
   {
     prof::HostScope hs("host_absorb_wait");
-    HIP_TRY(hipEventSynchronize(c->ev_host));
+    HIP_TRY(hipEventSynchronize(EV(c, EV_HOST, st_gather(r))));
   }
   const size_t wb = c->wb, np = c->np, limbs = wb / 8;
   uint8_t *repr = c->h_repr.p;
@@ -814,12 +970,15 @@ lcpc_status stage_idx_upload(lcpc_sharded_commit *c) {
 }
 
 // my rows of the opened columns (open_column, :818-855): [col][my rows], Montgomery
+size_t st_idx(const lcpc_sharded_commit *c) { return S_R0 + 2 * c->rounds; }
+size_t st_cols(const lcpc_sharded_commit *c) { return S_R0 + 2 * c->rounds + 1; }
+
 lcpc_status stage_gather_cols(lcpc_sharded_commit *c) {
-  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, EV(c, EV_DONE, st_idx(c)), 0));
   if (c->nco && c->nr)
     HIP_TRY(gather_columns(c->fid, c->comm_rows.as<uint32_t>(), c->nr, c->nc, c->didx.as<uint64_t>(), c->nco,
                            c->mycols.as<uint32_t>(), c->sp, c->sdig, true));
-  HIP_TRY(hipEventRecord(c->ev_ready, c->sp));
+  HIP_TRY(hipEventRecord(EV(c, EV_READY, st_cols(c)), c->sp));
   return LCPC_OK;
 }
 
@@ -832,16 +991,16 @@ Xop op_cols_gather(lcpc_sharded_commit *c) {
   op.sb[c->root_rank] = c->nco * c->nr * c->wb;
   if (c->me == c->root_rank)
     for (int k = 0; k < c->G; k++) op.rb[k] = c->nco * (c->part[k].r_hi - c->part[k].r_lo) * c->wb;
-  op.ready = c->ev_ready;
+  op.ready = EV(c, EV_READY, st_cols(c));
   op.s = c->sp;
   return op;
 }
 
 // root: Merkle paths off the whole tree, everything to the host
 lcpc_status stage_paths(lcpc_sharded_commit *c) {
-  HIP_TRY(hipStreamWaitEvent(c->sp, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->sp, EV(c, EV_DONE, st_cols(c)), 0));
   if (c->me != c->root_rank) {
-    HIP_TRY(hipEventRecord(c->ev_host, c->sp));
+    HIP_TRY(hipEventRecord(EV(c, EV_HOST, st_cols(c)), c->sp));
     return LCPC_OK;
   }
   const size_t pl = log2_np2(c->nc);
@@ -851,14 +1010,15 @@ lcpc_status stage_paths(lcpc_sharded_commit *c) {
     HIP_TRY(d2h(c->h_cols.p, c->allcols.p, c->nco * c->n_rows * c->wb, c->sp));
     if (pl) HIP_TRY(d2h(c->h_paths.p, c->dpaths.p, c->nco * pl * 32, c->sp));
   }
-  HIP_TRY(hipEventRecord(c->ev_host, c->sp));
+  HIP_TRY(hipEventRecord(EV(c, EV_HOST, st_cols(c)), c->sp));
   return LCPC_OK;
 }
 
 // root, host: the LcEvalProof (:1117-1122); columns reassembled from the ranks' row pieces
 lcpc_status host_proof(lcpc_sharded_commit *c, lcpc_proof **out) {
   prof::HostScope hs("host_final_proof");
-  HIP_TRY(hipEventSynchronize(c->ev_host));
+  HIP_TRY(hipEventSynchronize(EV(c, EV_HOST, st_cols(c))));
+  c->ev_quiet = true;  // (every exchange of the proof precedes it)
   if (c->me != c->root_rank) {
     if (out) *out = nullptr;
     return LCPC_OK;
@@ -903,7 +1063,6 @@ void prove_release(lcpc_sharded_commit *c) {
 // column gather.  Stage s of polynomial k goes out in tick k + off[s]; off[] leaves `lag` ticks
 // wherever the root rank absorbs one row combination before the next exchange needs its
 // challenge.  Every rank computes the same schedule, so the exchange groups match.
-enum { S_CV = 0, S_SUB = 1, S_R0 = 2 };
 struct Sched {
   size_t ndt = 0, rounds = 1, n_stages = 0, s_idx = 0, s_cols = 0, n_ticks = 0, lag = 1;
   std::vector<size_t> off;
@@ -973,13 +1132,15 @@ const char *stage_name(const Sched &sc, size_t s) {
 // A sharded call whose exchanges never complete (a peer that issued a different group, a dead
 // rank) would block forever in a stream or event wait.  The watchdog thread watches a progress
 // mark the calling thread moves at every tick and wait; when it has not moved for
-// LCPC_SHARD_WATCHDOG_S seconds (default 120; 0 disables) it prints the tick, the stage and the
-// peers on stderr and ends the process with status 75 (no re-exec, no further GPU call).
+// LCPC_SHARD_WATCHDOG_S seconds it prints the tick, the stage and the peers on stderr and ends the
+// process with status 75 (no re-exec, no further GPU call).  Off unless that variable is set (a
+// library must not end its host process by default: a peer may legitimately reach an exchange
+// late); bench.py and the tests set it.
 class Watchdog {
  public:
   Watchdog(int G, int me) : G_(G), me_(me) {
     const char *v = getenv("LCPC_SHARD_WATCHDOG_S");
-    limit_ = v ? atof(v) : 120.0;
+    limit_ = v ? atof(v) : 0.0;
     if (limit_ > 0) th_ = std::thread([this] { run(); });
   }
   ~Watchdog() {
@@ -990,6 +1151,7 @@ class Watchdog {
     cv_.notify_all();
     if (th_.joinable()) th_.join();
   }
+  bool enabled() const { return limit_ > 0; }
   // what the calling thread is about to wait for
   void mark(size_t tick, size_t n_ticks, const char *what, const std::string &group = std::string()) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -1018,7 +1180,7 @@ class Watchdog {
     }
   }
   int G_, me_;
-  double limit_ = 120;
+  double limit_ = 0;
   std::thread th_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -1042,16 +1204,18 @@ std::string describe_group(const std::vector<std::pair<size_t, size_t>> &items, 
   return g.empty() ? "-" : g;
 }
 
-lcpc_status one_group(lcpc_sharded_commit *c, Xop op, Watchdog *wd = nullptr, size_t step = 0,
+// one exchange of stage `stage` as its own group (the serial entry points)
+lcpc_status one_group(lcpc_sharded_commit *c, Xop op, size_t stage, Watchdog *wd = nullptr, size_t step = 0,
                       const char *what = "") {
   std::vector<Xop> ops{std::move(op)};
   if (wd) wd->mark(step, 0, what);
-  return run_group(c->comm, ops, {c->ev_done});
+  c->ev_quiet = false;
+  return run_group(c->comm, ops, {EV(c, EV_DONE, stage)});
 }
 
 // a gather of per-rank byte counts to one rank (an all-to-all with only the root receiving)
 Xop gather_to_root(const lcpc_sharded_commit *c, const uint8_t *send, uint8_t *recv, int root,
-                   const std::vector<size_t> &bytes_of_rank) {
+                   const std::vector<size_t> &bytes_of_rank, size_t stage) {
   Xop op{Xop::ALL_TO_ALL};
   op.send = send;
   op.recv = c->me == root ? recv : nullptr;
@@ -1059,7 +1223,7 @@ Xop gather_to_root(const lcpc_sharded_commit *c, const uint8_t *send, uint8_t *r
   op.rb.assign(c->G, 0);
   op.sb[root] = bytes_of_rank[c->me];
   if (c->me == root) op.rb = bytes_of_rank;
-  op.ready = c->ev_ready;
+  op.ready = EV(c, EV_READY, stage);
   op.s = c->s;
   return op;
 }
@@ -1083,6 +1247,12 @@ static lcpc_status comm_common(lcpc_comm *c) {
   lcpc_status st;
   c->dev = current_device(&st);
   if (!c->dev) return st;
+  if (!shard_mode2_allowed(c->nranks)) {
+    fprintf(stderr, "liblcpc_mi: LCPC_SHARD_PRIO=2 (mixed stream priorities) across %d ranks is an A/B mode "
+                    "(set LCPC_SHARD_PRIO_AB=1); using mode 3 (every stream of the driver at high priority)\n",
+            c->nranks);
+    g_prio_override.store(3);
+  }
   HIP_TRY(hipSetDevice(c->dev->id));
   if (shard_all_high()) {
     int lo = 0, hi = 0;
@@ -1150,9 +1320,9 @@ lcpc_status lcpc_sharded_commit_new_device(const lcpc_encoding *e, const void *d
   if ((st = shard_init(e, comm, n_rows, c))) return st;
   Watchdog wd(comm->nranks, comm->rank);
   if ((st = stage_pre_commit(c.get(), d_rows))) return st;
-  if ((st = one_group(c.get(), op_cv_exchange(c.get()), &wd, 0, "chaining-value all-to-all"))) return st;
+  if ((st = one_group(c.get(), op_cv_exchange(c.get()), S_CV, &wd, 0, "chaining-value all-to-all"))) return st;
   if ((st = stage_post_cv(c.get()))) return st;
-  if ((st = one_group(c.get(), op_subtree_exchange(c.get()), &wd, 1, "subtree all-gather"))) return st;
+  if ((st = one_group(c.get(), op_subtree_exchange(c.get()), S_SUB, &wd, 1, "subtree all-gather"))) return st;
   if ((st = stage_post_subtrees(c.get()))) return st;
   wd.mark(2, 0, "the commitment root");
   if ((st = finish_commit(c.get()))) return st;
@@ -1200,17 +1370,18 @@ lcpc_status lcpc_sharded_prove(lcpc_sharded_commit *c, const uint64_t *outer, si
   if (c->me == root && (st = challenge_first(c))) return st;
   for (size_t r = 0; r < c->rounds; r++) {
     if ((st = stage_tensor_upload(c, r))) return st;
-    if ((st = one_group(c, op_tensor_bcast(c, r), &wd, 2 * r, "challenge-tensor broadcast"))) return st;
+    if ((st = one_group(c, op_tensor_bcast(c, r), st_bcast(r), &wd, 2 * r, "challenge-tensor broadcast"))) return st;
     if ((st = stage_collapse(c, r))) return st;
-    if ((st = one_group(c, op_partial_gather(c, r), &wd, 2 * r + 1, "partial-combination gather"))) return st;
+    if ((st = one_group(c, op_partial_gather(c, r), st_gather(r), &wd, 2 * r + 1, "partial-combination gather")))
+      return st;
     if ((st = stage_fold(c, r))) return st;
     wd.mark(2 * r + 1, 0, "the folded row combination");
     if (c->me == root && (st = host_absorb(c, r))) return st;
   }
   if ((st = stage_idx_upload(c))) return st;
-  if ((st = one_group(c, op_idx_bcast(c), &wd, 2 * c->rounds, "column-index broadcast"))) return st;
+  if ((st = one_group(c, op_idx_bcast(c), st_idx(c), &wd, 2 * c->rounds, "column-index broadcast"))) return st;
   if ((st = stage_gather_cols(c))) return st;
-  if ((st = one_group(c, op_cols_gather(c), &wd, 2 * c->rounds + 1, "opened-column gather"))) return st;
+  if ((st = one_group(c, op_cols_gather(c), st_cols(c), &wd, 2 * c->rounds + 1, "opened-column gather"))) return st;
   if ((st = stage_paths(c))) return st;
   wd.mark(2 * c->rounds + 2, 0, "the opened columns and paths");
   return host_proof(c, out);
@@ -1240,6 +1411,20 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
   lcpc_status st;
   DBuf tens, part, scratch, all, sum, didx, mycols, allcols, dpaths;
   HostBuf h_left, h_idx;
+  if ((st = ev_need(c, kPosEvalStage, kPosColsStage + 1))) return st;
+  // (declared after the buffers, so destroyed first) on an early return once a gather is on the
+  // comm stream, RCCL may still read `part` / `mycols` or write `all` / `allcols`: drain the comm
+  // stream before the buffers go back to the pool
+  struct CommDrain {
+    lcpc_sharded_commit *c;
+    ~CommDrain() {
+      if (!c->ev_quiet) {
+        (void)hipStreamSynchronize(c->comm->cs);
+        (void)hipStreamSynchronize(c->s);
+        c->ev_quiet = true;
+      }
+    }
+  } comm_drain{c};
   // this rank's partial u^T Enc(M) over its rows.  The codeword holds canonical values (ntt_rows
   // canon_out), so the Montgomery products sum_r u_r R * m_rj R^-1 come out canonical.
   HIP_TRY(salloc(c, part, nc * wb));
@@ -1254,11 +1439,11 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
   } else {
     HIP_TRY(hipMemsetAsync(part.p, 0, nc * wb, c->s));
   }
-  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  HIP_TRY(hipEventRecord(EV(c, EV_READY, kPosEvalStage), c->s));
   if (am_root) HIP_TRY(salloc(c, all, (size_t)c->G * nc * wb));
   if ((st = one_group(c, gather_to_root(c, part.as<uint8_t>(), all.as<uint8_t>(), root,
-                                        std::vector<size_t>(c->G, nc * wb)),
-                      &wd, 0, "partial u^T Enc(M) gather")))
+                                        std::vector<size_t>(c->G, nc * wb), kPosEvalStage),
+                      kPosEvalStage, &wd, 0, "partial u^T Enc(M) gather")))
     return st;
   // my rows of the requested columns
   if (n_open) {
@@ -1267,7 +1452,7 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
     HIP_TRY(salloc(c, didx, n_open * 8));
     HIP_TRY(h2d(didx.p, h_idx.p, n_open * 8, c->s));
   }
-  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->s, EV(c, EV_DONE, kPosEvalStage), 0));
   HIP_TRY(salloc(c, mycols, std::max<size_t>(n_open * nr, 1) * wb));
   if (n_open && nr)
     HIP_TRY(gather_columns(c->fid, c->comm_rows.as<uint32_t>(), nr, nc, didx.as<uint64_t>(), n_open,
@@ -1279,13 +1464,14 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
     HIP_TRY(convert(c->fid, sum.as<uint32_t>(), sum.as<uint32_t>(), nc, true, c->s));
     HIP_TRY(salloc(c, allcols, std::max<size_t>(n_open * c->n_rows, 1) * wb));
   }
-  HIP_TRY(hipEventRecord(c->ev_ready, c->s));
+  HIP_TRY(hipEventRecord(EV(c, EV_READY, kPosColsStage), c->s));
   std::vector<size_t> col_bytes(c->G);
   for (int k = 0; k < c->G; k++) col_bytes[k] = n_open * (c->part[k].r_hi - c->part[k].r_lo) * wb;
-  if ((st = one_group(c, gather_to_root(c, mycols.as<uint8_t>(), allcols.as<uint8_t>(), root, col_bytes), &wd, 1,
-                      "requested-column gather")))
+  if ((st = one_group(c, gather_to_root(c, mycols.as<uint8_t>(), allcols.as<uint8_t>(), root, col_bytes,
+                                        kPosColsStage),
+                      kPosColsStage, &wd, 1, "requested-column gather")))
     return st;
-  HIP_TRY(hipStreamWaitEvent(c->s, c->ev_done, 0));
+  HIP_TRY(hipStreamWaitEvent(c->s, EV(c, EV_DONE, kPosColsStage), 0));
   if (am_root) {
     const size_t pl = log2_np2(nc);
     HIP_TRY(salloc(c, dpaths, std::max<size_t>(n_open * pl, 1) * 32));
@@ -1299,6 +1485,7 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
     if (paths_out && n_open && pl) HIP_TRY(d2h_staged(paths_out, dpaths.p, n_open * pl * 32, c->s));
     wd.mark(2, 0, "the request's results");
     HIP_TRY(hipStreamSynchronize(c->s));
+    c->ev_quiet = true;
     if (cols_out) {
       const uint8_t *src = h_cols.data();
       uint8_t *dst = (uint8_t *)cols_out;
@@ -1311,6 +1498,7 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
   } else {
     wd.mark(2, 0, "the request's exchanges");
     HIP_TRY(hipStreamSynchronize(c->s));
+    c->ev_quiet = true;
   }
   return LCPC_OK;
 }
@@ -1411,6 +1599,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     pending[k] = encoder.submit(wrap([&, k]() -> lcpc_status {
       lcpc_status s2 = shard_init(e, comm, n_rows, cs[k], bulk);
       if (s2) return s2;
+      cs[k]->poly = k;
       return stage_pre_commit(cs[k].get(), d_rows[k]);
     }));
   };
@@ -1490,12 +1679,15 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
           }
         }
         ops.push_back(stage_op(c, sc, s));
-        done.push_back(c->ev_done);
+        done.push_back(EV(c, EV_DONE, s));
+        c->ev_quiet = false;
         items.emplace_back(k, s);
       }
       if (!ops.empty()) {
         prof::HostScope hs("tick_run_group");
-        wd.mark(t, n_ticks, "issuing the exchange group", G > 1 ? describe_group(items, ops, sc, G, me) : std::string());
+        // (the group's text only feeds the watchdog's message: not built when it is off)
+        wd.mark(t, n_ticks, "issuing the exchange group",
+                G > 1 && wd.enabled() ? describe_group(items, ops, sc, G, me) : std::string());
         if ((st = run_group(comm, ops, done))) return fail_all(st);
       }
       // the compute each exchange feeds, on the polynomials' own streams (launch workers)
@@ -1595,12 +1787,11 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
   if (!st) st = take(rdsz, rpsz, root_depth);
   for (void *p : blocks) dev->release(p);
   for (void *p : pins) dev->pinned_put(p);
-  // two streams per polynomial in flight (commit, prove)
+  // the streams lcpc_sharded_commit_prove_many acquires: one shared (bulk) encode stream, and a
+  // prove stream per polynomial in flight
   std::vector<hipStream_t> lo, hi;
-  for (size_t k = 0; k < depth; k++) {
-    lo.push_back(dev->acquire_stream(shard_all_high()));
-    if (shard_prio_streams()) hi.push_back(dev->acquire_stream(shard_prove_high()));
-  }
+  lo.push_back(dev->acquire_stream(shard_all_high()));
+  for (size_t k = 0; k < depth && shard_prio_streams(); k++) hi.push_back(dev->acquire_stream(shard_prove_high()));
   for (hipStream_t x : lo)
     if (x) dev->release_stream(x, shard_all_high());
   for (hipStream_t x : hi)

@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+# the sharded calls' watchdog is off in the library by default; the tests (and the processes they
+# spawn, which inherit the environment) turn it on so a stuck exchange ends with a message
+os.environ.setdefault("LCPC_SHARD_WATCHDOG_S", "120")
 
 
 def pytest_configure(config):

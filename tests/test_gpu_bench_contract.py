@@ -56,6 +56,7 @@ def test_bench_ligero_sharded_small(gpu):
     assert d["scaling"] == "strong" and d["parity_proof_vs_oracle"] is True
     assert d["latency"]["commit_ms"] > 0 and d["latency"]["prove_ms"] > 0
     assert "traffic_source" in d["roofline"] and d["world_formed"] == 1
+    assert d["parity_ok"] is True and d["steps_agree"] is True
 
 
 def test_bench_ligero_default_small(gpu):
@@ -66,25 +67,50 @@ def test_bench_ligero_default_small(gpu):
     assert d["scaling"] == "weak" and d["parity_root_vs_oracle"] is True and d["pipeline"] == 4
     assert d["verify"]["parity_vs_oracle"] is True
     assert d["latency"]["commit_ms"] > 0 and d["world_formed"] == 1
+    assert d["parity_ok"] is True and d["sharded_n1"]["root_equals_replicas"] is True
+
+
+def _bench_ranks(world, extra_env, *args, timeout=280):
+    env = dict(os.environ, LCPC_BENCH_BACKEND="gloo", LCPC_BENCH_SHARE_GPU="1", **extra_env)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), *args], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _check_self_checking(d, world):
+    """an N > 1 line carries its own evidence of a right answer: the oracle's root against every
+    warm-up and timed step, the kept proof, the verifier's value and a cpu_baseline"""
+    assert d["n_gpus"] == world and d["world_formed"] == world and d["scaling"] == "strong"
+    assert d["parity_root_vs_oracle"] is True and d["parity_proof_vs_oracle"] is True
+    ps = d["parity_steps_vs_oracle"]
+    assert ps["steps"] == d["steps"] + d["warmup"] and ps["equal"] == ps["steps"]
+    assert d["steps_agree"] is True and d["parity_ok"] is True
+    assert d["verify"]["parity_vs_oracle"] is True
+    _check_cpu(d)
 
 
 @pytest.mark.timeout(300)
 def test_bench_sharded_two_ranks_one_gpu(gpu):
     """`bench.py --gpus 2` spawns two ranks; on a one-GPU box they share the GPU and exchange over
     host-staged gloo collectives (RCCL refuses two ranks on one device)."""
-    env = dict(os.environ, LCPC_BENCH_BACKEND="gloo", LCPC_BENCH_SHARE_GPU="1")
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
-        env.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup",
-                        "2", "--log-len", "16", "--verify-reps", "1", "--cpu-baseline", "on"], cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=280)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
-    d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["world_formed"] == 2 and d["scaling"] == "strong"
-    assert d["parity_root_vs_oracle"] is True and d["parity_proof_vs_oracle"] is True
+    d = _bench_ranks(2, {}, "--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1")
+    _check_self_checking(d, 2)
     assert "gloo" in d["config"]["exchanges"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_sharded_two_ranks_rccl_one_gpu(gpu):
+    """the same line through the library's RCCL communicator (per-rank NCCL_HOSTID: RCCL's socket
+    transport over loopback), with the default cpu_baseline setting: every N > 1 line self-checks"""
+    d = _bench_ranks(2, {"LCPC_BENCH_RCCL_SAME_GPU": "1"}, "--steps", "4", "--warmup", "2", "--log-len", "16",
+                     "--verify-reps", "1")
+    _check_self_checking(d, 2)
+    assert "RCCL" in d["config"]["exchanges"]
 
 
 def test_bench_encode_small(gpu):
@@ -105,3 +131,5 @@ def test_bench_pos_small(gpu):
     d = _bench("--code", "pos", "--steps", "2", "--warmup", "2", "--pos-bytes", str(1 << 20))
     _check_common(d, 2)
     _check_cpu(d)
+    assert d["parity_root_vs_oracle"] and d["parity_eval_vs_oracle"] and d["parity_cols_vs_oracle"]
+    assert d["parity_ok"] is True
