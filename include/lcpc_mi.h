@@ -63,7 +63,7 @@ typedef enum lcpc_status {
 typedef enum lcpc_field {
   LCPC_FT63 = 0,      /* lcpc-test-fields/src/lib.rs:18-22; PoS WriteableFt63 (same p) */
   LCPC_FT127 = 1,     /* lcpc-test-fields/src/lib.rs:41-45 */
-  LCPC_FT191 = 2,     /* lcpc-test-fields/src/lib.rs:53-57 (no row shards: 24-byte elements) */
+  LCPC_FT191 = 2,     /* lcpc-test-fields/src/lib.rs:53-57 (24-byte elements: row shards cut at chunks 2 mod 3) */
   LCPC_FT255 = 3,     /* lcpc-test-fields/src/lib.rs:65-69 */
   LCPC_FT253_192 = 4  /* proof-of-storage/src/fields/ft253_192.rs:6-10 (big-endian repr) */
 } lcpc_field;

@@ -737,6 +737,22 @@ void debug_commit(lcpc_sharded_commit *c) {
   }
   const auto rows3 = fetch(tc, c->nr * c->nc * wb);
   const bool input_same = !c->nr || debug_fnv_device(c->d_rows, c->nr * c->np * wb) == c->rows_fnv;
+  // where the production codeword differs: element count, rows touched, first / last (row, col)
+  std::string where;
+  if (rows != rows2) {
+    size_t cnt = 0, first = SIZE_MAX, last = 0, nrows_hit = 0, prev_row = SIZE_MAX;
+    for (size_t i = 0; i < c->nr * c->nc; i++)
+      if (std::memcmp(rows.data() + i * wb, rows2.data() + i * wb, wb)) {
+        cnt++;
+        first = std::min(first, i);
+        last = i;
+        if (i / c->nc != prev_row) nrows_hit++, prev_row = i / c->nc;
+      }
+    char b[200];
+    snprintf(b, sizeof b, " [%zu elements differ in %zu rows, first (%zu,%zu) last (%zu,%zu)]", cnt, nrows_hit,
+             first / c->nc, first % c->nc, last / c->nc, last % c->nc);
+    where = b;
+  }
   const auto cvs = fetch(c->cv_send.p, cvb), cvs2 = fetch(tv, cvb);
   const auto sub = fetch(c->sub.p, (2 * c->B - 1) * 32);
   const auto subs = fetch(c->subs.p, (size_t)c->G * (2 * c->B - 1) * 32);
@@ -753,9 +769,9 @@ void debug_commit(lcpc_sharded_commit *c) {
   std::string gathered;
   for (int q = 0; q < c->G; q++) gathered += " " + w4(subs.data() + ((size_t)q * (2 * c->B - 1) + 2 * c->B - 2) * 32);
   fprintf(stderr,
-          "liblcpc_mi dbg: rank %d poly %zu rows %s cv_send %s (per dest %s) recompute2 %s input %s sub %s gathered%s "
-          "root %s\n",
-          c->me, c->poly, rows == rows2 ? "ok" : "DIFF", cvs == cvs2 ? "ok" : "DIFF", per_dest.c_str(),
+          "liblcpc_mi dbg: rank %d poly %zu rows %s%s cv_send %s (per dest %s) recompute2 %s input %s sub %s "
+          "gathered%s root %s\n",
+          c->me, c->poly, rows == rows2 ? "ok" : "DIFF", where.c_str(), cvs == cvs2 ? "ok" : "DIFF", per_dest.c_str(),
           rows3 == rows2 ? "same" : "DIFFERS", input_same ? "unchanged" : "CHANGED",
           w4(sub.data() + (2 * c->B - 2) * 32).c_str(), gathered.c_str(), w4(c->root).c_str());
   fflush(stderr);
