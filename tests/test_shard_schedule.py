@@ -147,3 +147,41 @@ def test_row_cuts_fall_on_chunk_and_element_boundaries(fid, wb, n_rows, G):
     for r0, _ in rows[1:]:
         if 0 < r0 < n_rows:
             assert (32 + r0 * wb) % 1024 == 0, (r0, wb)
+
+
+def test_model_offsets_match_the_library_schedule():
+    """tools/shard_model.py's tick offsets (the basis of DESIGN §6's expected N = 1/2/4/8 table)
+    are the library's: polynomial k's stage s is in tick k + off[s] of lcpc_sharded_p2p_schedule"""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import shard_model
+    for G in (2, 4, 8):
+        off = shard_model.offsets(2, G)
+        recs = schedule(FT127, 512, 32768, 65536, 2, 309, G, 0, 20)
+        for k in (0, 7, 19):
+            ticks = {}
+            for grp, _pos, poly, stage, *_ in recs:
+                if poly == k:
+                    ticks.setdefault(stage, grp // 2)
+            assert ticks == {s: k + off[s] for s in range(len(off))}, (G, k, ticks, off)
+
+
+def test_ticks_per_proof_bounded_at_eight_ranks():
+    """G = 8, cfg3, the driver's K = 20: a polynomial's exchanges span 6 + 3 lag ticks from its
+    chaining values to its opened columns (lag = 10: 36), the whole run K + 36 ticks, and lag ticks
+    of the steady state still cover one transcript absorption (else every round would stall)"""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import shard_model
+    G, K = 8, 20
+    recs = schedule(FT127, 512, 32768, 65536, 2, 309, G, 0, K)
+    span = {}
+    for grp, _pos, poly, _stage, *_ in recs:
+        lo, hi = span.get(poly, (grp // 2, grp // 2))
+        span[poly] = (min(lo, grp // 2), max(hi, grp // 2))
+    assert len(span) == K and all(hi - lo <= 36 for lo, hi in span.values())
+    assert max(hi for _, hi in span.values()) + 1 <= K + 36
+    p = shard_model.predict(G, K)
+    assert p["ticks"] == K + 36 and p["lag_covers_absorb"]

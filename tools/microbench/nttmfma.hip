@@ -105,6 +105,9 @@ __device__ __forceinline__ void reduce_p(uint32_t x[4]) {  // x < 2p -> x mod p
 }
 
 // one wave = 32 vectors of 16 elements ([vec][i] canonical 16-byte elements); reps stages
+// MODE 0: the stage; 1: the matrix-core part alone (the next digits are a cheap mix of the
+// accumulators); 2: the VALU part alone (the accumulators are a cheap mix of the digits)
+template <int MODE>
 __global__ __launch_bounds__(256) void k_stage(const uint4 *__restrict__ in, uint4 *__restrict__ out,
                                                const uint4 *__restrict__ ht, int reps, size_t nvec) {
   __shared__ uint4 sh[64 * 64];  // the 64 A fragments (64 KB)
@@ -125,10 +128,39 @@ __global__ __launch_bounds__(256) void k_stage(const uint4 *__restrict__ in, uin
 #pragma unroll
     for (int p = 0; p < 8; p++) {
       v16i acc = {0};
+      if constexpr (MODE == 3) {
+        // two output pairs per pass: two independent accumulation chains interleaved
+        if (p & 1) continue;
+        v16i acc2 = {0};
 #pragma unroll
-      for (int ks = 0; ks < 8; ks++) {
-        const uint4 a = sh[(p * 8 + ks) * 64 + lane];
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(v4i{(int)a.x, (int)a.y, (int)a.z, (int)a.w}, B[ks], acc, 0, 0, 0);
+        for (int ks = 0; ks < 8; ks++) {
+          const uint4 a = sh[(p * 8 + ks) * 64 + lane];
+          const uint4 a2 = sh[((p + 1) * 8 + ks) * 64 + lane];
+          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(v4i{(int)a.x, (int)a.y, (int)a.z, (int)a.w}, B[ks], acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(v4i{(int)a2.x, (int)a2.y, (int)a2.z, (int)a2.w}, B[ks], acc2, 0, 0, 0);
+        }
+        uint32_t y[4], y2[4];
+        recombine(acc, y);
+        recombine(acc2, y2);
+        Bn[p] = digits(y);
+        Bn[p + 1] = digits(y2);
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
+      if constexpr (MODE == 2) {
+#pragma unroll
+        for (int u = 0; u < 16; u++) acc[u] = B[u & 7][u >> 3] ^ (p * 0x1010101 + u);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 8; ks++) {
+          const uint4 a = sh[(p * 8 + ks) * 64 + lane];
+          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(v4i{(int)a.x, (int)a.y, (int)a.z, (int)a.w}, B[ks], acc, 0, 0, 0);
+        }
+      }
+      if constexpr (MODE == 1) {
+        Bn[p] = v4i{acc[0] ^ acc[4], acc[1] ^ acc[8], acc[2] ^ acc[12], acc[3] ^ acc[15]};
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
       }
       uint32_t y[4];
       recombine(acc, y);
@@ -197,7 +229,7 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(din, hin.data(), nvec * 256, hipMemcpyHostToDevice));
   CK(hipMemcpy(dht, ht.data(), ht.size(), hipMemcpyHostToDevice));
   const unsigned blocks = (unsigned)((nvec + 127) / 128);
-  hipLaunchKernelGGL(k_stage, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
+  hipLaunchKernelGGL(k_stage<0>, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -205,7 +237,7 @@ int main(int argc, char **argv) {
   const int iters = 10;
   CK(hipEventRecord(e0));
   for (int it = 0; it < iters; it++)
-    hipLaunchKernelGGL(k_stage, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
+    hipLaunchKernelGGL(k_stage<0>, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0;
@@ -214,13 +246,35 @@ int main(int argc, char **argv) {
   // the same launch with reps = 0 (load + digits + store only) to subtract the memory part
   CK(hipEventRecord(e0));
   for (int it = 0; it < iters; it++)
-    hipLaunchKernelGGL(k_stage, dim3(blocks), dim3(256), 0, 0, din, dout, dht, 1, nvec);
+    hipLaunchKernelGGL(k_stage<0>, dim3(blocks), dim3(256), 0, 0, din, dout, dht, 1, nvec);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms1 = 0;
   CK(hipEventElapsedTime(&ms1, e0, e1));
   ms1 /= iters;
-  hipLaunchKernelGGL(k_stage, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
+  float msm[3] = {ms, 0, 0};
+  float ms3 = 0;
+  for (int md = 1; md <= 3; md++) {
+    CK(hipEventRecord(e0));
+    for (int it = 0; it < iters; it++) {
+      if (md == 1) hipLaunchKernelGGL(k_stage<1>, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
+      else if (md == 2) hipLaunchKernelGGL(k_stage<2>, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
+      else hipLaunchKernelGGL(k_stage<3>, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
+    }
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float& dst = md == 3 ? ms3 : msm[md];
+    CK(hipEventElapsedTime(&dst, e0, e1));
+    dst /= iters;
+  }
+  {
+    const double el = (double)nvec * 16;
+    auto cyc = [&](float m) { return (m - ms1) * 1e-3 / (reps - 1) / el * 2.4e9 * 1024; };
+    printf("nttmfma split: whole stage %.2f, matrix cores alone %.2f, VALU alone %.2f, two interleaved chains %.2f "
+           "SIMD-cycles per element (nominal)\n",
+           cyc(msm[0]), cyc(msm[1]), cyc(msm[2]), cyc(ms3));
+  }
+  hipLaunchKernelGGL(k_stage<0>, dim3(blocks), dim3(256), 0, 0, din, dout, dht, reps, nvec);
   CK(hipDeviceSynchronize());
   std::vector<uint32_t> hout(nvec * 16 * 4);
   CK(hipMemcpy(hout.data(), dout, nvec * 256, hipMemcpyDeviceToHost));
