@@ -73,10 +73,14 @@ def parse():
                     help="Ligero code rate (LigeroEncodingRho<F, U1, U2>, lcpc-ligero-pc/src/lib.rs:32-37): 1/2 "
                          "is LigeroEncoding (the BASELINE metric, :189); 1/4 is the reference's commit_bench "
                          "(lcpc-ligero-pc/src/bench.rs:43, the 2021 published commit timings)")
-    ap.add_argument("--code", choices=["ligero", "sdig", "pos", "encode"], default="ligero",
+    ap.add_argument("--code", choices=["ligero", "sdig", "pos", "encode", "sdig-encode"], default="ligero",
                     help="ligero: R-S / NTT rows (the BASELINE metric, cfg3); sdig: Brakedown "
                          "SdigCode3 expander code, seed 0 (cfg4); pos: proof-of-storage request "
-                         "on a resident file (cfg5); encode: the Ligero R-S encode alone (cfg2)")
+                         "on a resident file (cfg5); encode: the Ligero R-S encode alone (cfg2); "
+                         "sdig-encode: the Brakedown encode alone (cfg4's rows, LcEncoding::encode)")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="sdig-encode: commitments' rows per encode call (72 rows each at 2^24): the "
+                         "expander levels gather batch x 72-row runs per nonzero")
     ap.add_argument("--pos-bytes", type=int, default=1 << 30, help="file size for --code pos")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -113,12 +117,14 @@ def parse():
                          "--code sdig, or 4 for --code pos (a 1 GiB request's 2.3 GiB codeword per slot: deeper "
                          "pipelines only contend for HBM)")
     args = ap.parse_args()
-    if args.code in ("sdig", "encode"):
+    if args.code in ("sdig", "encode", "sdig-encode"):
         args.mode = "replicas"  # cfg2 / cfg4 run as independent steps per rank
     if args.mode == "auto":
         args.mode = "sharded" if args.gpus > 1 else "replicas"
     if args.log_len is None:
         args.log_len = 20 if args.code == "encode" else 24
+    if args.code == "sdig-encode" and args.pipeline <= 0:
+        args.pipeline = 4
     num, den = (int(x) for x in args.rho.split("/"))
     args.rho_t = (num, den)
     if args.commit_slots < 0:
@@ -411,6 +417,68 @@ def encode_workload(args, L, torch, rank, local_rank):
         traffic_key=(n, args.field, "encode"),
         mul_count=n_rows * ntt_muls(n_cols),
         mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row")
+
+
+def sdig_encode_workload(args, L, torch, rank, local_rank):
+    """cfg4's encode alone: LcEncoding::encode of SdigEncodingS (lcpc-brakedown-pc/src/lib.rs:150-153
+    -> encode.rs:36-94) on every row of `batch` 2^24-coefficient commitments in one call (row-major
+    device rows in and out; the library runs the expander levels on the element-major transpose)."""
+    fid = {"Ft63": L.FT63, "Ft127": L.FT127, "Ft255": L.FT255}[args.field]
+    nl = L.limbs(fid)
+    n = 1 << args.log_len
+    enc = L.SdigEncoding.new(fid, n, 0)
+    n_rows1, n_per_row, n_cols = enc.get_dims(n)
+    k = max(1, args.batch)
+    n_rows = n_rows1 * k
+    coeffs = L.field_random(fid, n_rows * n_per_row, replica_seed(rank))
+    dev = f"cuda:{local_rank}"
+    d_src = torch.from_numpy(coeffs.view(np.int64)).to(dev)
+    dst = [torch.empty(n_rows * n_cols * nl, dtype=torch.int64, device=dev) for _ in range(max(1, args.pipeline))]
+    torch.cuda.synchronize()
+
+    def step(slot):
+        enc.encode_rows_device(d_src.data_ptr(), n_per_row, n_per_row, dst[slot].data_ptr(), n_cols, n_rows)
+        return None
+
+    def cpu_baseline(O):
+        # bounded sample: the oracle's encode (encode.rs:36-94) on rows of this workload, one
+        # thread, until about 10 s; then the GPU's rows against those
+        o_enc = O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3)
+        rows = coeffs.reshape(n_rows, n_per_row * nl)
+        outs, t1 = [], time.perf_counter()
+        while len(outs) < n_rows and (time.perf_counter() - t1 < 10.0 or not outs):
+            x = np.zeros(n_cols * nl, np.uint64)
+            x[:n_per_row * nl] = rows[len(outs)]
+            outs.append(o_enc.encode(x))
+        dt = (time.perf_counter() - t1) / len(outs) * n_rows
+        step(0)
+        torch.cuda.synchronize()
+        got = dst[0].cpu().numpy().view(np.uint64).reshape(n_rows, n_cols * nl)
+        ok = all(np.array_equal(got[r], outs[r]) for r in range(len(outs)))
+        return dt, ok, (f"the oracle's encode of the first {len(outs)} of the {n_rows} rows on one thread "
+                        f"({time.perf_counter() - t1:.1f} s), scaled to all rows; those rows compared")
+
+    B = 8 * nl
+    nnz = enc.matrix_nnz
+    return Workload(
+        units=n_rows * n_per_row, unit="field-elements/s", bytes_per_unit=B,
+        metric=f"encoded field-elements/s (Brakedown SdigCode3 encode), 2^{args.log_len}-coeff {args.field} (cfg4)",
+        dtype=f"u64x{nl} ({args.field} Montgomery limbs)",
+        data=f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), resident in HBM",
+        config={"workload": f"Brakedown SdigCode3 (seed 0) encode, {args.field}, {k} x 2^{args.log_len} coeffs per "
+                            f"call, {n_rows}x{n_per_row}->{n_cols}",
+                "field": args.field, "len": n, "batch": k, "n_rows": n_rows, "n_per_row": n_per_row,
+                "n_cols": n_cols, "matrix_nnz": nnz},
+        step=step, cpu_baseline=cpu_baseline, cpu_cores=1, root_is_parity=True, cpu_reps_ok=False,
+        enc_kernels=("transpose", "sdig_encode"),
+        enc_kernel_desc=(f"sdig_encode = transpose to element-major + 13 SpMM / Reed-Solomon levels + transpose "
+                         f"back (one call, all {n_rows} rows)"),
+        # SURVEY §8(d): read the coefficients, write the codeword, stream the code matrices once
+        algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B + nnz * (B + 4),
+        gather_bytes=(n_rows * nnz * B + n_rows * (n_cols - n_per_row) * B + nnz * 20
+                      + 3 * n_rows * n_per_row * B + 2 * n_rows * n_cols * B),
+        traffic_key=(n, args.field, f"sdig-encode-b{k}"),
+        mul_count=n_rows * nnz, mul_model="one product per nonzero per row")
 
 
 def pos_workload(args, L, torch, rank, local_rank):
@@ -1122,7 +1190,8 @@ def pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, root, ev, opened):
 def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     """Independent commitments per rank (cfg3 replicas, cfg4 Brakedown, cfg5 PoS, cfg2 encode),
     kept in flight on host threads over the library's pooled streams."""
-    wl = {"pos": pos_workload, "encode": encode_workload}.get(args.code, ligero_or_sdig)(
+    wl = {"pos": pos_workload, "encode": encode_workload, "sdig-encode": sdig_encode_workload}.get(
+        args.code, ligero_or_sdig)(
         args, L, torch, rank, device_idx)
     torch.cuda.synchronize()
     prof = not args.no_prof

@@ -245,9 +245,20 @@ __global__ __launch_bounds__(256) void k_transpose(const uint32_t *__restrict__ 
   }
 }
 
-// rows per wave of k_spmm_mfma: chunks of at most 8 tiles (128 rows), as few 16-row tiles as cover R
+// rows per wave of k_spmm_mfma: chunks of at most LCPC_SDIG_TILES (default 8, at most 10) tiles of
+// 16 rows, as few tiles as cover R.  More tiles per wave amortise a 4-nonzero group's A-fragment
+// work over more rows (two commitments' 144 rows in one wave with 9) at the cost of registers.
+inline int mfma_max_tiles() {
+  static const int v = [] {
+    const char *e = std::getenv("LCPC_SDIG_TILES");
+    const int t = e ? std::atoi(e) : 8;
+    return t < 1 ? 8 : (t > 10 ? 10 : t);
+  }();
+  return v;
+}
 inline void mfma_tiling(size_t R, int &tiles, unsigned &chunks) {
-  chunks = (unsigned)((R + 127) / 128);
+  const size_t per = 16 * (size_t)mfma_max_tiles();
+  chunks = (unsigned)((R + per - 1) / per);
   tiles = (int)((R + 16 * chunks - 1) / (16 * chunks));
 }
 
@@ -277,7 +288,9 @@ hipError_t spmm(const SdigPlan &p, const CsrDev &M, const uint32_t *x, uint32_t 
         case 5: launch_spmm_mfma<F, 5>(M, x, y, R, b0, nb, chunks, s); break;
         case 6: launch_spmm_mfma<F, 6>(M, x, y, R, b0, nb, chunks, s); break;
         case 7: launch_spmm_mfma<F, 7>(M, x, y, R, b0, nb, chunks, s); break;
-        default: launch_spmm_mfma<F, 8>(M, x, y, R, b0, nb, chunks, s); break;
+        case 8: launch_spmm_mfma<F, 8>(M, x, y, R, b0, nb, chunks, s); break;
+        case 9: launch_spmm_mfma<F, 9>(M, x, y, R, b0, nb, chunks, s); break;
+        default: launch_spmm_mfma<F, 10>(M, x, y, R, b0, nb, chunks, s); break;
       }
       return hipGetLastError();
     }
