@@ -214,6 +214,27 @@ def ntt_muls(n):
     return (n // 2) * max(lg - 2, 0) + n
 
 
+ROW1_DEFAULT = "0"  # csrc/ntt_row1.hpp ROW1_DEFAULT
+
+
+def row1_active(n):
+    """the one-pass Ft63 row kernel (csrc/ntt_row1.hpp) encodes rate-1/2 2^15-point rows unless
+    LCPC_NTT_ROW1=0 selects the four-step pair"""
+    return n == 1 << 15 and os.environ.get("LCPC_NTT_ROW1", ROW1_DEFAULT)[:1] != "0"
+
+
+def pos_ntt_muls(n):
+    """(products per row, model) of the Ft63 encode at the PoS dims: the one-pass kernel does
+    stage 0 (16384, the sum branch's R^-1 scaling by a reduction counted as half a product),
+    stages 1-9 (16384 each) and round 3's 49 nontrivial products per thread; the four-step pair
+    ntt_muls(n)"""
+    if row1_active(n):
+        return (n // 2) * 10 + 1024 * 49 + n // 4, ("one-pass 2^15 DIF (ntt_row1): stages 0-9 all products, "
+                                                    "stages 10-14 the 49 nontrivial per thread, + n/2 half-cost "
+                                                    "R^-1 reductions")
+    return ntt_muls(n), "four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row"
+
+
 def leaf_compressions(n_rows, n_cols, elem_bytes):
     """BLAKE3 compressions of the column leaves (lcpc-2d/src/lib.rs:736-775): each leaf message
     is 32 zero bytes + n_rows elements, one compression per 64-byte block (the last one of a
@@ -556,13 +577,13 @@ def pos_workload(args, L, torch, rank, local_rank):
                             f"dims {n_rows}x{np_}->{nc}, u^T Enc(M) at a point, 256 opened columns",
                 "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd},
         step=step, cpu_baseline=cpu_baseline, parity=parity,
-        enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
-        enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)",
+        enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small", "ntt_row1"),
+        enc_kernel_desc=(f"ntt_encode = ntt_row1 (one launch per commit, all {n_rows} rows)" if row1_active(nc) else
+                         f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
         algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
         leaf_compressions=leaf_compressions(n_rows, nc, 8),
-        traffic_key=(n_el, "Ft63", "pos"),
-        mul_count=n_rows * ntt_muls(nc),
-        mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass twiddles per row")
+        traffic_key=(n_el, "Ft63", "pos-row1" if row1_active(nc) else "pos"),
+        mul_count=n_rows * pos_ntt_muls(nc)[0], mul_model=pos_ntt_muls(nc)[1])
 
 
 # ---------------------------------------------------------------- launch, cores, shared output
@@ -1131,12 +1152,14 @@ def run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share):
                    "exchanges": comm_kind, "rows_on_rank0": nr},
         "mb_per_s": n_bytes * args.steps / elapsed / 1e6,
     }
-    wl = Workload(algo_bytes=nr * np_ * 8 + nr * nc * 8, enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
-                  enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, this rank's "
-                                  f"{nr} rows)",
-                  traffic_key=(n_el, "Ft63", "pos"), mul_count=nr * ntt_muls(nc),
-                  mul_model="four-step fft_io: (n/2)(log2 n - 2) general-twiddle butterflies + n inter-pass "
-                            "twiddles per row", leaf_compressions=0)
+    wl = Workload(algo_bytes=nr * np_ * 8 + nr * nc * 8,
+                  enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small", "ntt_row1"),
+                  enc_kernel_desc=(f"ntt_encode = ntt_row1 (one launch per commit, this rank's {nr} rows)"
+                                   if row1_active(nc) else
+                                   f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, this rank's "
+                                   f"{nr} rows)"),
+                  traffic_key=(n_el, "Ft63", "pos-row1" if row1_active(nc) else "pos"),
+                  mul_count=nr * pos_ntt_muls(nc)[0], mul_model=pos_ntt_muls(nc)[1], leaf_compressions=0)
     out.update(roofline_objects(wl, iso, {}, args, traffic_rows_frac=nr / n_rows))
     out["steps_agree"] = all(r == root for r in troots)
     want_cpu = args.cpu_baseline in ("on", "auto")

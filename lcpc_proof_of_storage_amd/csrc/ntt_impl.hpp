@@ -22,8 +22,11 @@
 #pragma once
 #include "field.hpp"
 #include "kernels.hpp"
+#include "ntt_row1.hpp"
 #include "ntt_v2.hpp"
 #include "prof.hpp"
+
+#include <cstdlib>
 
 namespace lcpc {
 namespace ntt_detail {
@@ -160,6 +163,13 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
   }
   constexpr int R = Shape<F>::R, E = Shape<F>::E;
   const bool halfz = 2 * nv <= ((size_t)1 << p.log_n);
+  if constexpr (F::ID == 0) {
+    // PoS default dims: the one-pass row kernel (ntt_row1.hpp) when LCPC_NTT_ROW1 selects it
+    // (ROW1_DEFAULT otherwise; 0 = the four-step pair)
+    const char *r1 = std::getenv("LCPC_NTT_ROW1");
+    if (p.log_n == ntt_row1::LOG_N && halfz && (r1 ? r1[0] != '0' : ntt_row1::ROW1_DEFAULT))
+      return ntt_row1::launch<F>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, canon);
+  }
   constexpr int HI = F::N >= 8 ? 11 : 12;  // LDS budget of 32-byte fields
   auto pass_a = [&]<int L, int CW>() {
     constexpr int T = L + CW - R;

@@ -1,0 +1,226 @@
+// ntt_row1.hpp -- the 2^15-point Ft63 row encode in ONE pass (the proof-of-storage default
+// dims: 16384 coefficients -> 32768 per row, 9363 rows per 1 GiB file; lcpc_online.rs:80-239
+// commits them through LigeroEncodingRho::encode, lcpc-ligero-pc/src/lib.rs:162-164).
+// Same contract as ntt_impl.hpp (fffft::fft_io, out[bitrev(j)] = sum_i in[i] w^(ij)), rate-1/2
+// rows only (n_valid <= n / 2).
+//
+// One 1024-thread workgroup per row. The row (256 KiB) stays in registers, 32 elements per
+// thread, and the 15 radix-2 DIF stages run as three radix-32 rounds over the index bits
+// i = (hi << 10) | (mid << 5) | lo:
+//   round 1: stages 0-4   (bits 14-10)  thread (mid, lo) holds hi  = 0..31
+//   round 2: stages 5-9   (bits 9-5)    thread (hi, lo)  holds mid = 0..31
+//   round 3: stages 10-14 (bits 4-0)    thread (hi, mid) holds lo  = 0..31
+// Rounds exchange through one 128 KiB LDS buffer in two halves. The half is a bit that the
+// writer's and the reader's thread numbering put at the SAME thread-id bit >= 6 (lo's top bit at
+// bit 9 for exchange 1, hi's top bit at bit 8 for exchange 2), so each half is written and read
+// back by the same 8 waves and no thread ever holds more than its own 32 elements. The output
+// goes through LDS once more so the stores are contiguous 16-byte vectors.
+//
+// Against the four-step pair (k_pass_a + k_pass_b) at the PoS dims: no intermediate round trip
+// (2 x 2.45 GB of HBM per 1 GiB request) and no inter-pass twiddle products; round 3's twiddles
+// are w^(1024 k) with k known at compile time, so its trivial products drop out.
+// CANON: the row is scaled by R^-1 on the way in -- the sum branch of the (HALFZ) first stage by
+// a Montgomery reduction, the product branch through the canonical-word twiddle table -- so the
+// Montgomery words written out are the canonical values (the ntt_rows canon_out contract).
+#pragma once
+#include "field.hpp"
+#include "kernels.hpp"
+#include "prof.hpp"
+
+namespace lcpc {
+namespace ntt_row1 {
+
+constexpr int LOG_N = 15;
+constexpr bool ROW1_DEFAULT = false;  // (until measured against the four-step pair)
+
+// element (hi, mid, lo & 15) of the half lo >> 4 (exchange 1); the XOR spreads a ds_read's lanes
+// (16 values of hi) over 16 bank pairs
+__device__ __forceinline__ int x1_at(int hi, int mid, int l4) { return (((hi << 5) | mid) << 4) | (l4 ^ (hi & 15)); }
+// element (hi & 15, mid, lo) of the half hi >> 4 (exchange 2)
+__device__ __forceinline__ int x2_at(int hi, int mid, int lo) {
+  return ((hi & 15) << 10) | (mid << 5) | (lo ^ (hi & 15));
+}
+
+template <class F>
+__device__ __forceinline__ void bfly(Fe<F> &a, Fe<F> &b, const Fe<F> &w) {
+  const Fe<F> s = fe_add_2p<F>(a, b);
+  b = fe_mul_lazy<F>(fe_sub_2p<F>(a, b), w);
+  a = s;
+}
+template <class F>
+__device__ __forceinline__ void bfly1(Fe<F> &a, Fe<F> &b) {  // twiddle 1
+  const Fe<F> s = fe_add_2p<F>(a, b);
+  b = fe_sub_2p<F>(a, b);
+  a = s;
+}
+template <class F>
+__device__ __forceinline__ Fe<F> lds_ld(const uint2 *t, int i) {
+  const uint2 q = t[i];
+  Fe<F> r;
+  r.v[0] = q.x;
+  r.v[1] = q.y;
+  return r;
+}
+template <class F>
+__device__ __forceinline__ void lds_st(uint2 *t, int i, const Fe<F> &x) {
+  t[i] = make_uint2(x.v[0], x.v[1]);
+}
+
+// one DIF stage over the 32 register elements: pairs (j, j + HS), twiddle index tw_at(jm)
+template <class F, int HS, class TwAt>
+__device__ __forceinline__ void reg_stage(Fe<F> *x, TwAt &&tw_at) {
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    if (j & HS) continue;
+    bfly<F>(x[j], x[j + HS], tw_at(j & (HS - 1)));
+  }
+}
+// round 3's stage S (10..14): twiddle w^(jm << S) = wtab[jm << (S - 5)], 1 for jm = 0
+template <class F, int S>
+__device__ __forceinline__ void lo_stage(Fe<F> *x, const uint2 *wtab) {
+  constexpr int HS = 16 >> (S - 10);
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    if (j & HS) continue;
+    const int jm = j & (HS - 1);
+    if (jm == 0)
+      bfly1<F>(x[j], x[j + HS]);
+    else
+      bfly<F>(x[j], x[j + HS], lds_ld<F>(wtab, jm << (S - 5)));
+  }
+}
+
+// tw: w^e (Montgomery, e < n); tw0: the first stage's table (canonical words when CANON)
+template <class F, bool CANON, bool COPY>
+__global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__ src, size_t src_stride,
+                                                    size_t n_valid, uint32_t *__restrict__ dst, size_t dst_stride,
+                                                    const uint32_t *__restrict__ tw,
+                                                    const uint32_t *__restrict__ tw0,
+                                                    uint32_t *__restrict__ copy, size_t copy_stride) {
+  static_assert(F::N == 2, "8-byte fields");
+  __shared__ __align__(16) uint2 xbuf[16384];  // half a row
+  __shared__ uint2 wtab[512];                   // w^(32 k)
+  const int tid = threadIdx.x;
+  const size_t row = blockIdx.x;
+  if (tid < 512) wtab[tid] = reinterpret_cast<const uint2 *>(tw)[32 * tid];
+  const uint32_t *in = src + row * src_stride * 2;
+  Fe<F> x[32];
+
+  // ---- round 1: thread (mid, lo), lo's top bit at thread-id bit 9
+  {
+    const int lo = ((tid >> 9) << 4) | (tid & 15), mid = (tid >> 4) & 31;
+    const int tl = (mid << 5) | lo;
+#pragma unroll
+    for (int h = 0; h < 16; h++) {
+      const int pos = (h << 10) | tl;
+      Fe<F> a = fe_zero<F>();
+      if ((size_t)pos < n_valid) {
+        a = fe_load<F>(in, pos);
+        if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
+      }
+      // stage 0 with x[h + 16] = 0: (a, a w^e)
+      x[h + 16] = fe_mul_lazy<F>(a, fe_load<F>(tw0, pos));
+      if constexpr (CANON)
+        x[h] = fe_from_mont<F>(a);
+      else
+        x[h] = a;
+    }
+    reg_stage<F, 8>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 1); });
+    reg_stage<F, 4>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 2); });
+    reg_stage<F, 2>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 3); });
+    reg_stage<F, 1>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 4); });
+    // ---- exchange 1: (mid, lo) -> (hi, lo), halves by lo >> 4
+    const int lo2 = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi2 = (((tid >> 8) & 1) << 4) | (tid & 15);
+    auto xchg = [&](int ph) {
+      if ((tid >> 9) == ph) {
+#pragma unroll
+        for (int h = 0; h < 32; h++) lds_st<F>(xbuf, x1_at(h, mid, lo & 15), x[h]);
+      }
+      __syncthreads();
+      if ((tid >> 9) == ph) {
+#pragma unroll
+        for (int m = 0; m < 32; m++) x[m] = lds_ld<F>(xbuf, x1_at(hi2, m, lo2 & 15));
+      }
+      __syncthreads();
+    };
+    xchg(0);
+    xchg(1);
+  }
+  // ---- round 2: thread (hi, lo) holds mid = 0..31; twiddles w^(((jm << 5) | lo) << s)
+  {
+    const int lo = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
+    reg_stage<F, 16>(x, [&](int jm) { return lds_ld<F>(wtab, (jm << 5) | lo); });
+    reg_stage<F, 8>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 1); });
+    reg_stage<F, 4>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 2); });
+    reg_stage<F, 2>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 3); });
+    reg_stage<F, 1>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 4); });
+    // ---- exchange 2: (hi, lo) -> (hi, mid), halves by hi >> 4 (thread-id bit 8 in both)
+    const int mid3 = ((tid >> 9) << 4) | ((tid >> 4) & 15);
+    auto xchg = [&](int ph) {
+      if (((tid >> 8) & 1) == ph) {
+#pragma unroll
+        for (int m = 0; m < 32; m++) lds_st<F>(xbuf, x2_at(hi, m, lo), x[m]);
+      }
+      __syncthreads();
+      if (((tid >> 8) & 1) == ph) {
+#pragma unroll
+        for (int l = 0; l < 32; l++) x[l] = lds_ld<F>(xbuf, x2_at(hi, mid3, l));
+      }
+      __syncthreads();
+    };
+    xchg(0);
+    xchg(1);
+  }
+  // ---- round 3: thread (hi, mid) holds lo = 0..31; twiddles w^(jm << s) = wtab[jm << (s - 5)]
+  {
+    const int mid = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
+    lo_stage<F, 10>(x, wtab);
+    lo_stage<F, 11>(x, wtab);
+    lo_stage<F, 12>(x, wtab);
+    lo_stage<F, 13>(x, wtab);
+    lo_stage<F, 14>(x, wtab);
+    // ---- out: through LDS in halves (hi >> 4), 16-byte units u = ((hi & 15) << 9) | (mid << 4) | (lo >> 1)
+    //      stored at u ^ (hi & 7): a ds_write's 64 lanes land on 8 distinct 16-byte bank slots
+    uint4 *ubuf = reinterpret_cast<uint4 *>(xbuf);
+    uint4 *out = reinterpret_cast<uint4 *>(dst + row * dst_stride * 2);
+    auto store_half = [&](int ph) {
+      if (((tid >> 8) & 1) == ph) {
+#pragma unroll
+        for (int lp = 0; lp < 16; lp++) {
+          const Fe<F> a = fe_reduce_2p<F>(x[2 * lp]), b = fe_reduce_2p<F>(x[2 * lp + 1]);
+          const int u = ((hi & 15) << 9) | (mid << 4) | lp;
+          ubuf[u ^ (hi & 7)] = make_uint4(a.v[0], a.v[1], b.v[0], b.v[1]);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int u = (k << 10) | tid;
+        out[(ph << 13) | u] = ubuf[u ^ ((u >> 9) & 7)];
+      }
+    };
+    store_half(0);
+    __syncthreads();
+    store_half(1);
+  }
+}
+
+template <class F>
+hipError_t launch(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
+                  size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
+  const uint32_t *tw0 = canon ? p.d_tw_canon : p.d_tw;
+  prof::Scope ps("ntt_row1", s);
+  const dim3 g((unsigned)n_rows), b(1024);
+  if (canon && cp)
+    hipLaunchKernelGGL((k_row_ntt15<F, true, true>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
+  else if (canon)
+    hipLaunchKernelGGL((k_row_ntt15<F, true, false>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
+  else if (cp)
+    hipLaunchKernelGGL((k_row_ntt15<F, false, true>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
+  else
+    hipLaunchKernelGGL((k_row_ntt15<F, false, false>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
+  return hipGetLastError();
+}
+
+}  // namespace ntt_row1
+}  // namespace lcpc

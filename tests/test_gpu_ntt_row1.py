@@ -1,0 +1,98 @@
+"""GPU parity of the one-pass Ft63 row encode (csrc/ntt_row1.hpp) at the proof-of-storage
+default dims (2^15-point rows, rate 1/2: 16384 coefficients -> 32768), against the oracle's
+fft_io and commit (lcpc-ligero-pc/src/lib.rs:162-164, lcpc-2d/src/lib.rs:651-700), and against
+the four-step pair it replaces (LCPC_NTT_ROW1=0)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def row1_on():
+    """the one-pass kernel for every call of these tests unless four_step() says otherwise"""
+    old = os.environ.get("LCPC_NTT_ROW1")
+    os.environ["LCPC_NTT_ROW1"] = "1"
+    yield
+    if old is None:
+        del os.environ["LCPC_NTT_ROW1"]
+    else:
+        os.environ["LCPC_NTT_ROW1"] = old
+
+NP, NC = 16384, 32768
+
+
+def rand_elems(oracle, n, seed):
+    return oracle.ChaCha(seed_u64=seed).field_random(0, n)
+
+
+class four_step:
+    """LCPC_NTT_ROW1=0 for the duration (the library reads it at every launch)"""
+
+    def __enter__(self):
+        self.old = os.environ.get("LCPC_NTT_ROW1")
+        os.environ["LCPC_NTT_ROW1"] = "0"
+
+    def __exit__(self, *a):
+        if self.old is None:
+            del os.environ["LCPC_NTT_ROW1"]
+        else:
+            os.environ["LCPC_NTT_ROW1"] = self.old
+
+
+def test_row1_encode_rows_match_fffft(gpu, oracle):
+    """batched rows (Montgomery output, no coefficient copy) against fft_io row by row"""
+    enc = gpu.RsEncoding.new(0, NP, NC, 4, 1)
+    rows = np.zeros((5, NC), np.uint64)
+    rows[:, :NP] = rand_elems(oracle, 5 * NP, 61).reshape(5, NP)
+    got = enc.encode_rows(rows.copy()).reshape(5, NC)
+    for r in range(5):
+        assert np.array_equal(got[r], oracle.fft_io(0, rows[r])), r
+    with four_step():
+        got4 = enc.encode_rows(rows.copy()).reshape(5, NC)
+    assert np.array_equal(got, got4)
+
+
+@pytest.mark.parametrize("pattern", ["max", "alternating", "one", "impulse_last"])
+def test_row1_extreme_values(gpu, oracle, pattern):
+    """p - 1 everywhere, alternating 0 / p - 1, a single 1 and a single p - 1 at the last valid
+    coefficient: the [0, 2p) butterflies at their carry / borrow boundaries"""
+    pm1 = oracle.modulus(0) - 1
+    row = np.zeros(NC, np.uint64)
+    if pattern == "max":
+        row[:NP] = pm1
+    elif pattern == "alternating":
+        row[1:NP:2] = pm1
+    elif pattern == "one":
+        row[0] = 1
+    else:
+        row[NP - 1] = pm1
+    enc = gpu.RsEncoding.new(0, NP, NC, 4, 1)
+    got = row.copy()
+    enc.encode(got)
+    assert np.array_equal(got, oracle.fft_io(0, row))
+
+
+@pytest.mark.parametrize("length", [37 * NP, 37 * NP + 5, 3 * NP - 1, 1000])
+def test_row1_commit_device_matches_oracle(gpu, oracle, hipmem, length):
+    """the commit path (canonical output + the commitment's coefficient copy), full and ragged
+    last rows, against the oracle's coefficient matrix, codeword, hashes and root"""
+    coeffs = rand_elems(oracle, length, 17)
+    g_enc = gpu.RsEncoding.new(0, NP, NC, 16, 2)
+    o_enc = oracle.Encoding.ligero(0, NP, NC, 16, 2)
+    d = hipmem.to_device(coeffs)
+    try:
+        g = gpu.LcCommit.commit_device(d, length, g_enc)
+        o = oracle.Commit(o_enc, coeffs)
+        assert np.array_equal(g.coeffs.reshape(-1), o.coeffs)
+        assert np.array_equal(g.comm.reshape(-1), o.comm)
+        assert g.hashes == o.hashes
+        assert g.get_root() == o.root()
+        with four_step():
+            g4 = gpu.LcCommit.commit_device(d, length, g_enc)
+        assert g4.get_root() == g.get_root()
+        del g, g4
+    finally:
+        hipmem.free(d)

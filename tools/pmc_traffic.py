@@ -23,7 +23,7 @@ KERNELS = {"ntt_pass_a": "k_pass_a", "ntt_pass_b": "k_pass_b", "leaf_chunks": "k
            # Brakedown (--code sdig): the transpose into element-major form, the SpMM levels
            # (matrix-core or VALU kernel) and the Reed-Solomon base
            "transpose": "k_transpose", "spmm": "k_spmm", "reed_solomon": "k_reed_solomon",
-           "pos_pack7": "k_pack7"}
+           "pos_pack7": "k_pack7", "ntt_row1": "k_row_ntt15"}
 SDIG_ENCODE = ("transpose", "spmm", "reed_solomon")
 
 
@@ -65,8 +65,10 @@ def main():
         n_enc = nf["transpose"]
         enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in SDIG_ENCODE) / n_enc
     else:
-        n_enc = nf["pos_pack7"] if a.code == "pos" else nf["leaf_chunks"]
-        enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in ("ntt_pass_a", "ntt_pass_b")) / n_enc
+        # (pos-row1: the one-pass Ft63 row kernel, whose 8-byte loads arrive as 128-byte runs; the
+        # x2 read correction is checked by its read figure against the input's size)
+        n_enc = nf["pos_pack7"] if a.code.startswith("pos") else nf["leaf_chunks"]
+        enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in ("ntt_pass_a", "ntt_pass_b", "ntt_row1")) / n_enc
     for k in kern:
         kern[k]["hbm_bytes_per_step"] = (2.0 * ftot[k] + wtot.get(k, 0.0)) / n_enc
     out = {
