@@ -21,6 +21,7 @@ def row1_on():
     else:
         os.environ["LCPC_NTT_ROW1"] = old
 
+
 NP, NC = 16384, 32768
 
 
