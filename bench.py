@@ -82,6 +82,9 @@ def parse():
                     help="sdig-encode: commitments' rows per encode call (72 rows each at 2^24): the "
                          "expander levels gather batch x 72-row runs per nonzero")
     ap.add_argument("--pos-bytes", type=int, default=1 << 30, help="file size for --code pos")
+    ap.add_argument("--pos-commit", choices=["bytes", "elements"], default="bytes",
+                    help="--code pos: commit the file image in one call (lcpc_pos_commit_bytes_device) or pack "
+                         "it to elements first (lcpc_pos_bytes_to_field_device + lcpc_commit_new_device)")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every core this process may use (affinity and cgroup quota)")
@@ -519,7 +522,8 @@ def pos_workload(args, L, torch, rank, local_rank):
     # element buffers of whole-row capacity whose tail past n_el stays zero: commit pads the last
     # row with zeros (lcpc-2d/src/lib.rs:665-674), so committing the n_rows x n_per_row buffer is
     # the same commitment, and the ragged row needs no separate one-row encode
-    slots = [torch.zeros(n_rows * np_, dtype=torch.int64, device=dev) for _ in range(max(1, args.pipeline))]
+    slots = ([torch.zeros(n_rows * np_, dtype=torch.int64, device=dev) for _ in range(max(1, args.pipeline))]
+             if args.pos_commit == "elements" else [])
     x = L.field_random(L.FT63, 1, 1337)
     left, _ = P.form_side_vectors_for_polynomial_evaluation_from_point(x, n_rows, nc)
     cols = P.get_column_indicies_from_random_seed(1337, 256, nc)
@@ -528,15 +532,20 @@ def pos_workload(args, L, torch, rank, local_rank):
 
     gate = threading.Semaphore(args.commit_slots) if args.commit_slots > 0 else None
 
-    def step(slot):
+    def commit(slot):
+        if args.pos_commit == "bytes":  # lcpc_pos_commit_bytes_device: the file image in one call
+            return L.LcCommit.commit_pos_bytes_device(d_bytes.data_ptr(), n_bytes, enc)
         d_el = slots[slot]
+        rc = lib.lcpc_pos_bytes_to_field_device(d_bytes.data_ptr(), n_bytes, d_el.data_ptr(), None)
+        if rc:
+            raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
+        return L.LcCommit.commit_device(d_el.data_ptr(), n_rows * np_, enc)
+
+    def step(slot):
         if gate is not None:
             gate.acquire()
         try:
-            rc = lib.lcpc_pos_bytes_to_field_device(d_bytes.data_ptr(), n_bytes, d_el.data_ptr(), None)
-            if rc:
-                raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
-            c = L.LcCommit.commit_device(d_el.data_ptr(), n_rows * np_, enc)
+            c = commit(slot)
         finally:
             if gate is not None:
                 gate.release()
@@ -558,11 +567,7 @@ def pos_workload(args, L, torch, rank, local_rank):
 
     def parity(O):
         """one request of this workload (untimed) against the oracle's answer on the whole file"""
-        d_el = slots[0]
-        rc = lib.lcpc_pos_bytes_to_field_device(d_bytes.data_ptr(), n_bytes, d_el.data_ptr(), None)
-        if rc:
-            raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
-        c = L.LcCommit.commit_device(d_el.data_ptr(), n_rows * np_, enc)
+        c = commit(0)
         ev = P.verifiable_polynomial_evaluation(c, left)
         opened = c.open_columns(cols)
         return pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, c.get_root(), ev, opened)
@@ -575,7 +580,9 @@ def pos_workload(args, L, torch, rank, local_rank):
         data=f"synthetic: {n_bytes} random bytes (numpy default_rng(1 + rank)), resident in HBM",
         config={"workload": f"PoS request on a {n_bytes}-byte file: {n_el} WriteableFt63 elements, default "
                             f"dims {n_rows}x{np_}->{nc}, u^T Enc(M) at a point, 256 opened columns",
-                "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd},
+                "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd,
+                "commit_call": ("lcpc_pos_commit_bytes_device (file image in one call)" if args.pos_commit == "bytes"
+                                else "lcpc_pos_bytes_to_field_device + lcpc_commit_new_device")},
         step=step, cpu_baseline=cpu_baseline, parity=parity,
         enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small", "ntt_row1"),
         enc_kernel_desc=(f"ntt_encode = ntt_row1 (one launch per commit, all {n_rows} rows)" if row1_active(nc) else

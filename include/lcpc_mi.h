@@ -262,6 +262,14 @@ lcpc_status lcpc_pos_bytes_to_field(const uint8_t *bytes, size_t n_bytes, uint64
 /* same on device buffers (8-byte aligned); asynchronous on `stream` (NULL: synchronous) */
 lcpc_status lcpc_pos_bytes_to_field_device(const void *d_bytes, size_t n_bytes, void *d_out,
                                            void *stream);
+/* The server's commitment to a file image in device memory: DataField::from_byte_vec then
+ * LcCommit::commit (lcpc_online.rs:80-239, networking/server.rs:670-730), the same commitment as
+ * lcpc_pos_bytes_to_field_device + lcpc_commit_new_device on ceil(n_bytes / 7) elements.  At the
+ * default PoS dims (2^14 -> 2^15 Ft63 rows, 16-byte-aligned image) the bytes are unpacked inside
+ * the one-pass encode (no element image in HBM); elsewhere they are packed first.  The image must
+ * be 8-byte aligned; WriteableFt63 (LCPC_FT63) encodings only. */
+lcpc_status lcpc_pos_commit_bytes_device(const lcpc_encoding *e, const void *d_bytes, size_t n_bytes,
+                                         lcpc_commit **out);
 /* DataField::field_vec_to_byte_vec truncated to expected_len (data_field.rs:57-62,
  * fields.rs:115-121) */
 lcpc_status lcpc_pos_field_to_bytes(const uint64_t *elems, size_t n, uint8_t *out,

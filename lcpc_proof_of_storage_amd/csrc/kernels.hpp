@@ -47,6 +47,14 @@ void ntt_plan_free(NttPlan &p);
 hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
                     uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s,
                     uint32_t *copy = nullptr, size_t copy_stride = 0, bool canon_out = false);
+// The proof-of-storage file image encoded straight into a commitment (ntt_row1.hpp BYTES): row r
+// = WriteableFt63 elements [n_per_row r, n_per_row (r + 1)) of the n_bytes-byte image, 7 bytes per
+// element (zero padded); canonical output, the coefficient matrix written to copy.  Only at the
+// one-pass kernel's shape (ntt_rows_pos_bytes_ok), 16-byte-aligned bytes.
+bool ntt_rows_pos_bytes_ok(const NttPlan &p, size_t n_per_row);
+bool ntt_row1_default();  // whether the one-pass kernel is on when LCPC_NTT_ROW1 is unset
+hipError_t ntt_rows_pos_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst,
+                              size_t dst_stride, size_t n_rows, hipStream_t s, uint32_t *copy, size_t copy_stride);
 
 // ------------------------------------------------------------------ BLAKE3 / Merkle
 // leaf[j] = BLAKE3(32 zero bytes || repr(m[0][j]) || ... || repr(m[n_rows-1][j]))

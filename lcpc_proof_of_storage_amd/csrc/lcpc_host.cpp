@@ -83,8 +83,11 @@ lcpc_status make_sdig_encoding(int fid, int code, size_t n_per_row, size_t want_
   return LCPC_OK;
 }
 
+// src_bytes != 0: d_src is a device proof-of-storage file image of src_bytes bytes, 7 per
+// WriteableFt63 element (len = ceil(src_bytes / 7)), packed as DataField::from_byte_vec does
+// (fields/data_field.rs:38-46) -- at the PoS default dims straight into the one-pass encode
 lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is_host, size_t len,
-                          lcpc_commit **out) {
+                          lcpc_commit **out, size_t src_bytes = 0) {
   prof::HostScope hs_total("host_commit_total");
   if (!e || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   const size_t np = e->n_per_row, nc = e->n_cols;
@@ -113,6 +116,20 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
     }
   }
   const int fid = e->fid, wb = field_bytes(fid);
+  DBuf packed;  // bytes off the fused path: the element image (at function scope: no block-exit drain)
+  const uint8_t *src_b = nullptr;
+  if (src_bytes) {
+    if (fid != LCPC_FT63 || src_is_host) return fail(LCPC_ERR_INVALID_ARG, "file image: device WriteableFt63 only");
+    const char *r1 = std::getenv("LCPC_NTT_ROW1");
+    const bool row1 = r1 ? r1[0] != '0' : ntt_row1_default();
+    if (e->kind != KIND_SDIG && row1 && ntt_rows_pos_bytes_ok(e->plan, np) && !((uintptr_t)d_src & 15)) {
+      src_b = (const uint8_t *)d_src;
+    } else {
+      HIP_TRY(packed.alloc(dev, len * 8));
+      HIP_TRY(pos_pack7((const uint8_t *)d_src, src_bytes, packed.as<uint64_t>(), s));
+      d_src = packed.p;
+    }
+  }
   auto c = std::make_unique<lcpc_commit>();
   c->fid = fid;
   c->dev = dev;
@@ -154,6 +171,10 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
     HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb, hipMemcpyHostToDevice, s));
     if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
     HIP_TRY(ntt_rows(e->plan, (const uint32_t *)cf, np, np, (uint32_t *)cm, nc, n_rows, s, nullptr, 0, true));
+  } else if (src_b) {
+    // the file image, unpacked inside the encode, which also writes the coefficient matrix
+    c->canon = true;
+    HIP_TRY(ntt_rows_pos_bytes(e->plan, src_b, src_bytes, (uint32_t *)cm, nc, n_rows, s, (uint32_t *)cf, np));
   } else {
     // full rows are encoded straight from the caller's buffer; the first NTT pass writes the
     // commitment's own coefficient copy as it reads them (no separate D2D copy)
@@ -192,6 +213,7 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
     // this commit's work is complete: its scratch needs no drain of the shared stream
     tmp.settle();
     scratch.settle();
+    packed.settle();
   } else {
     HIP_TRY(hipStreamSynchronize(s));
   }
@@ -522,6 +544,13 @@ lcpc_status lcpc_commit_new_device(const lcpc_encoding *e, const void *d_coeffs,
                                    lcpc_commit **out) {
   if (!d_coeffs) return fail(LCPC_ERR_INVALID_ARG, "null coeffs");
   return commit_device(e, d_coeffs, false, len, out);
+}
+
+lcpc_status lcpc_pos_commit_bytes_device(const lcpc_encoding *e, const void *d_bytes, size_t n_bytes,
+                                         lcpc_commit **out) {
+  if (!d_bytes || !n_bytes) return fail(LCPC_ERR_INVALID_ARG, "null or empty file image");
+  if ((uintptr_t)d_bytes & 7) return fail(LCPC_ERR_INVALID_ARG, "device file image must be 8-byte aligned");
+  return commit_device(e, d_bytes, false, (n_bytes + 6) / 7, out, n_bytes);  // 7 data bytes per element
 }
 
 void lcpc_commit_free(lcpc_commit *c) {

@@ -6,6 +6,18 @@ hipError_t ntt_rows_ft63(const NttPlan &p, const uint32_t *src, size_t ss, size_
                       size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
   return ntt_detail::ntt_rows_t<Ft63>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, canon);
 }
+bool ntt_row1_default() { return ntt_row1::ROW1_DEFAULT; }
+bool ntt_rows_pos_bytes_ok(const NttPlan &p, size_t n_per_row) {
+  return p.fid == 0 && p.log_n == ntt_row1::LOG_N && n_per_row == ((size_t)1 << (ntt_row1::LOG_N - 1)) &&
+         p.d_tw_canon;
+}
+hipError_t ntt_rows_pos_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst,
+                              size_t dst_stride, size_t n_rows, hipStream_t s, uint32_t *copy, size_t copy_stride) {
+  if (!ntt_rows_pos_bytes_ok(p, (size_t)1 << (ntt_row1::LOG_N - 1)) || ((uintptr_t)bytes & 15) || !copy)
+    return hipErrorInvalidValue;
+  if (n_rows == 0) return hipSuccess;
+  return ntt_row1::launch_bytes<Ft63>(p, bytes, n_bytes, dst, dst_stride, n_rows, s, copy, copy_stride);
+}
 hipError_t ntt_tw_table_ft63(uint32_t *tw, int log_n, bool inverse, hipStream_t s) {
   const size_t n = (size_t)1 << log_n;
   hipLaunchKernelGGL((ntt_detail::k_tw_table<Ft63>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0,

@@ -90,8 +90,13 @@ __device__ __forceinline__ void lo_stage(Fe<F> *x, const uint2 *wtab) {
   }
 }
 
-// tw: w^e (Montgomery, e < n); tw0: the first stage's table (canonical words when CANON)
-template <class F, bool CANON, bool COPY>
+// tw: w^e (Montgomery, e < n); tw0: the first stage's table (canonical words when CANON).
+// BYTES: src is a proof-of-storage file image of n_valid bytes, 7 little-endian bytes per element
+// (DataField::from_byte_vec for WriteableFt63, fields/data_field.rs:38-46: the element's raw u64
+// limb, zero-padded), row r = elements [16384 r, 16384 (r + 1)); the row's 112 KiB are staged in
+// the exchange buffer with coalesced 16-byte loads and each thread unpacks its 16 elements from
+// there -- k_pack7 fused into the encode (no element image written and read back).
+template <class F, bool CANON, bool COPY, bool BYTES = false>
 __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__ src, size_t src_stride,
                                                     size_t n_valid, uint32_t *__restrict__ dst, size_t dst_stride,
                                                     const uint32_t *__restrict__ tw,
@@ -110,11 +115,36 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
   {
     const int lo = ((tid >> 9) << 4) | (tid & 15), mid = (tid >> 4) & 31;
     const int tl = (mid << 5) | lo;
+    if constexpr (BYTES) {
+      constexpr int ROW_BYTES = 7 << 14, ROW_U4 = ROW_BYTES / 16;
+      const size_t row0 = row * (size_t)ROW_BYTES;
+      const uint8_t *rb = reinterpret_cast<const uint8_t *>(src) + row0;
+      uint4 *sb = reinterpret_cast<uint4 *>(xbuf);
+      for (int i = tid; i < ROW_U4; i += 1024) {
+        const size_t b = row0 + 16 * (size_t)i;
+        if (b + 16 <= n_valid) {
+          sb[i] = reinterpret_cast<const uint4 *>(rb)[i];
+        } else {  // the file's last bytes: zero padded
+          uint32_t w[4] = {0, 0, 0, 0};
+          for (int k = 0; k < 16; k++)
+            if (b + k < n_valid) w[k >> 2] |= (uint32_t)rb[16 * i + k] << (8 * (k & 3));
+          sb[i] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+      __syncthreads();
+    }
 #pragma unroll
     for (int h = 0; h < 16; h++) {
       const int pos = (h << 10) | tl;
       Fe<F> a = fe_zero<F>();
-      if ((size_t)pos < n_valid) {
+      if constexpr (BYTES) {
+        const uint32_t *sw = reinterpret_cast<const uint32_t *>(xbuf);
+        const int b = 7 * pos, d = b >> 2, sh = b & 3;
+        const uint32_t d0 = sw[d], d1 = sw[d + 1], d2 = sw[d + 2];  // (d + 2 < 32768: inside xbuf)
+        a.v[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        a.v[1] = __builtin_amdgcn_alignbyte(d2, d1, sh) & 0xffffffu;
+        if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
+      } else if ((size_t)pos < n_valid) {
         a = fe_load<F>(in, pos);
         if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
       }
@@ -125,6 +155,7 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
       else
         x[h] = a;
     }
+    if constexpr (BYTES) __syncthreads();  // every row byte unpacked before exchange 1 reuses xbuf
     reg_stage<F, 8>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 1); });
     reg_stage<F, 4>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 2); });
     reg_stage<F, 2>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 3); });
@@ -219,6 +250,16 @@ hipError_t launch(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, u
     hipLaunchKernelGGL((k_row_ntt15<F, false, true>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
   else
     hipLaunchKernelGGL((k_row_ntt15<F, false, false>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
+  return hipGetLastError();
+}
+
+// the proof-of-storage commit from the file image (BYTES above): canonical output, coefficient copy
+template <class F>
+hipError_t launch_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst, size_t ds,
+                        size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
+  prof::Scope ps("ntt_row1", s);
+  hipLaunchKernelGGL((k_row_ntt15<F, true, true, true>), dim3((unsigned)n_rows), dim3(1024), 0, s,
+                     reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds, p.d_tw, p.d_tw_canon, cp, cs);
   return hipGetLastError();
 }
 

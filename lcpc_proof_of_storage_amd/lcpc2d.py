@@ -383,6 +383,15 @@ class LcCommit:
         _raise(N.load().lcpc_commit_new_device(enc._h, d_coeffs, length, C.byref(h)))
         return cls(h.value, enc.field)
 
+    @classmethod
+    def commit_pos_bytes_device(cls, d_bytes: int, n_bytes: int, enc: LcEncoding) -> "LcCommit":
+        """the proof-of-storage server's commitment to a file image in device memory:
+        DataField::from_byte_vec + LcCommit::commit (lcpc_online.rs:80-239), one call
+        (lcpc_pos_commit_bytes_device; WriteableFt63 encodings only)"""
+        h = C.c_void_p()
+        _raise(N.load().lcpc_pos_commit_bytes_device(enc._h, d_bytes, n_bytes, C.byref(h)))
+        return cls(h.value, enc.field)
+
     def get_root(self) -> bytes:
         out = (C.c_uint8 * 32)()
         _raise(N.load().lcpc_commit_get_root(self._h, C.cast(out, N.u8p)))

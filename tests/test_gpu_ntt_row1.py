@@ -97,3 +97,50 @@ def test_row1_commit_device_matches_oracle(gpu, oracle, hipmem, length):
         del g, g4
     finally:
         hipmem.free(d)
+
+
+@pytest.mark.parametrize("row1", ["1", "0"])
+@pytest.mark.parametrize("dims,n_bytes", [
+    ((NP, NC), 7 * NP * 5),            # whole rows, one-pass fused unpack
+    ((NP, NC), 7 * NP * 5 + 1001),     # a partial last row, a partial last element
+    ((NP, NC), 13),                    # two elements, one row
+    ((100, 256), 7 * 100 * 3 + 5),     # other dims: packed first
+])
+def test_pos_commit_bytes_device(gpu, oracle, hipmem, row1, dims, n_bytes):
+    """lcpc_pos_commit_bytes_device == DataField::from_byte_vec + LcCommit::commit (the oracle's
+    pos_bytes_to_field + Commit), and == the two-call device path"""
+    os.environ["LCPC_NTT_ROW1"] = row1
+    np_, nc = dims
+    data = np.random.default_rng(n_bytes).integers(0, 256, n_bytes, dtype=np.uint8)
+    data[-1] = 0xff
+    el = oracle.pos_bytes_to_field(data.tobytes())
+    g_enc = gpu.RsEncoding.new(0, np_, nc, 16, 2)
+    o_enc = oracle.Encoding.ligero(0, np_, nc, 16, 2)
+    d = hipmem.to_device(np.concatenate([data, np.zeros((-n_bytes) % 8, np.uint8)]).view(np.uint64))
+    de = hipmem.to_device(el)
+    try:
+        g = gpu.LcCommit.commit_pos_bytes_device(d, n_bytes, g_enc)
+        o = oracle.Commit(o_enc, el)
+        assert np.array_equal(g.coeffs.reshape(-1), o.coeffs)
+        assert np.array_equal(g.comm.reshape(-1), o.comm)
+        assert g.get_root() == o.root()
+        assert gpu.LcCommit.commit_device(de, el.size, g_enc).get_root() == g.get_root()
+        del g
+    finally:
+        hipmem.free(d)
+        hipmem.free(de)
+
+
+def test_pos_commit_bytes_device_rejects(gpu, hipmem):
+    d = hipmem.to_device(np.zeros(16, np.uint64))
+    try:
+        enc127 = gpu.RsEncoding.new(1, 64, 128, 4, 1)
+        with pytest.raises(Exception):
+            gpu.LcCommit.commit_pos_bytes_device(d, 64, enc127)       # not WriteableFt63
+        enc = gpu.RsEncoding.new(0, 64, 128, 4, 1)
+        with pytest.raises(Exception):
+            gpu.LcCommit.commit_pos_bytes_device(d + 1, 64, enc)      # misaligned
+        with pytest.raises(Exception):
+            gpu.LcCommit.commit_pos_bytes_device(d, 0, enc)           # empty
+    finally:
+        hipmem.free(d)
