@@ -27,11 +27,13 @@
 #include "kernels.hpp"
 #include "prof.hpp"
 
+#include <cstdlib>
+
 namespace lcpc {
 namespace ntt_row1 {
 
 constexpr int LOG_N = 15;
-constexpr bool ROW1_DEFAULT = false;  // (until measured against the four-step pair)
+constexpr int ROW1_DEFAULT = 0;  // LCPC_NTT_ROW1 unset: the four-step pair (until measured)
 
 // element (hi, mid, lo & 15) of the half lo >> 4 (exchange 1); the XOR spreads a ds_read's lanes
 // (16 values of hi) over 16 bank pairs
@@ -96,171 +98,251 @@ __device__ __forceinline__ void lo_stage(Fe<F> *x, const uint2 *wtab) {
 // limb, zero-padded), row r = elements [16384 r, 16384 (r + 1)); the row's 112 KiB are staged in
 // the exchange buffer with coalesced 16-byte loads and each thread unpacks its 16 elements from
 // there -- k_pack7 fused into the encode (no element image written and read back).
-template <class F, bool CANON, bool COPY, bool BYTES = false>
+// PERSIST: one workgroup per CU walks rows blockIdx.x, + gridDim.x, ...; the next row's input goes
+// into the exchange buffer by LDS-DMA (global_load_lds_dwordx4) while round 3 computes, and the
+// outputs are stored straight from registers (16-byte stores, a lane's 32 outputs contiguous), so
+// the buffer is free for the prefetch -- a row's HBM load no longer waits between two rows.
+constexpr int ROW_BYTES = 7 << 14;  // one row of the file image
+
+__device__ __forceinline__ void glds16(const void *g, void *l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                   (__attribute__((address_space(3))) void *)l, 16, 0, 0);
+}
+
+// a whole row's input into xbuf by LDS-DMA (PERSIST rows are whole: every 16-byte piece in bounds)
+template <bool BYTES>
+__device__ __forceinline__ void stage_row(const uint32_t *src, size_t src_stride, size_t row, uint2 *xbuf, int tid) {
+  uint4 *sb = reinterpret_cast<uint4 *>(xbuf) + (tid & ~63);
+  const uint4 *g = BYTES ? reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(src) + row * (size_t)ROW_BYTES)
+                         : reinterpret_cast<const uint4 *>(src + row * src_stride * 2);
+  g += tid;
+  constexpr int PIECES = BYTES ? ROW_BYTES / 16 / 1024 : 8;
+#pragma unroll
+  for (int i = 0; i < PIECES; i++) glds16(g + i * 1024, sb + i * 1024);
+}
+
+template <class F, bool CANON, bool COPY, bool BYTES, bool PERSIST>
 __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__ src, size_t src_stride,
                                                     size_t n_valid, uint32_t *__restrict__ dst, size_t dst_stride,
                                                     const uint32_t *__restrict__ tw,
                                                     const uint32_t *__restrict__ tw0,
-                                                    uint32_t *__restrict__ copy, size_t copy_stride) {
+                                                    uint32_t *__restrict__ copy, size_t copy_stride, size_t n_rows,
+                                                    size_t row_base) {
   static_assert(F::N == 2, "8-byte fields");
   __shared__ __align__(16) uint2 xbuf[16384];  // half a row
   __shared__ uint2 wtab[512];                   // w^(32 k)
   const int tid = threadIdx.x;
-  const size_t row = blockIdx.x;
+  size_t row = row_base + blockIdx.x;
   if (tid < 512) wtab[tid] = reinterpret_cast<const uint2 *>(tw)[32 * tid];
-  const uint32_t *in = src + row * src_stride * 2;
+  if constexpr (PERSIST) {
+    stage_row<BYTES>(src, src_stride, row, xbuf, tid);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
   Fe<F> x[32];
-
-  // ---- round 1: thread (mid, lo), lo's top bit at thread-id bit 9
-  {
-    const int lo = ((tid >> 9) << 4) | (tid & 15), mid = (tid >> 4) & 31;
-    const int tl = (mid << 5) | lo;
-    if constexpr (BYTES) {
-      constexpr int ROW_BYTES = 7 << 14, ROW_U4 = ROW_BYTES / 16;
-      const size_t row0 = row * (size_t)ROW_BYTES;
-      const uint8_t *rb = reinterpret_cast<const uint8_t *>(src) + row0;
-      uint4 *sb = reinterpret_cast<uint4 *>(xbuf);
-      for (int i = tid; i < ROW_U4; i += 1024) {
-        const size_t b = row0 + 16 * (size_t)i;
-        if (b + 16 <= n_valid) {
-          sb[i] = reinterpret_cast<const uint4 *>(rb)[i];
-        } else {  // the file's last bytes: zero padded
-          uint32_t w[4] = {0, 0, 0, 0};
-          for (int k = 0; k < 16; k++)
-            if (b + k < n_valid) w[k >> 2] |= (uint32_t)rb[16 * i + k] << (8 * (k & 3));
-          sb[i] = make_uint4(w[0], w[1], w[2], w[3]);
+  for (;;) {
+    // (PERSIST: tid through an opaque zero, so that the row-independent twiddle loads and LDS
+    // addresses are recomputed per row, not hoisted out of the loop into ~100 live registers)
+    int z = 0;
+    if constexpr (PERSIST) asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    const int tid = threadIdx.x + z;
+    // ---- round 1: thread (mid, lo), lo's top bit at thread-id bit 9
+    {
+      const int lo = ((tid >> 9) << 4) | (tid & 15), mid = (tid >> 4) & 31;
+      const int tl = (mid << 5) | lo;
+      if constexpr (BYTES && !PERSIST) {
+        const size_t row0 = row * (size_t)ROW_BYTES;
+        const uint8_t *rb = reinterpret_cast<const uint8_t *>(src) + row0;
+        uint4 *sb = reinterpret_cast<uint4 *>(xbuf);
+        for (int i = tid; i < ROW_BYTES / 16; i += 1024) {
+          const size_t b = row0 + 16 * (size_t)i;
+          if (b + 16 <= n_valid) {
+            sb[i] = reinterpret_cast<const uint4 *>(rb)[i];
+          } else {  // the file's last bytes: zero padded
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (int k = 0; k < 16; k++)
+              if (b + k < n_valid) w[k >> 2] |= (uint32_t)rb[16 * i + k] << (8 * (k & 3));
+            sb[i] = make_uint4(w[0], w[1], w[2], w[3]);
+          }
         }
       }
-      __syncthreads();
+      if constexpr (BYTES || PERSIST) __syncthreads();  // the staged row (every wave's part) is in
+      const uint32_t *in = src + row * src_stride * 2;
+#pragma unroll
+      for (int h = 0; h < 16; h++) {
+        const int pos = (h << 10) | tl;
+        Fe<F> a = fe_zero<F>();
+        if constexpr (BYTES) {
+          const uint32_t *sw = reinterpret_cast<const uint32_t *>(xbuf);
+          const int b = 7 * pos, d = b >> 2, sh = b & 3;
+          const uint32_t d0 = sw[d], d1 = sw[d + 1], d2 = sw[d + 2];  // (d + 2 < 32768: inside xbuf)
+          a.v[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+          a.v[1] = __builtin_amdgcn_alignbyte(d2, d1, sh) & 0xffffffu;
+          if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
+        } else if constexpr (PERSIST) {
+          a = lds_ld<F>(xbuf, pos);  // (whole rows: n_valid = 16384)
+          if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
+        } else if ((size_t)pos < n_valid) {
+          a = fe_load<F>(in, pos);
+          if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
+        }
+        // stage 0 with x[h + 16] = 0: (a, a w^e)
+        x[h + 16] = fe_mul_lazy<F>(a, fe_load<F>(tw0, pos));
+        if constexpr (CANON)
+          x[h] = fe_from_mont<F>(a);
+        else
+          x[h] = a;
+      }
+      if constexpr (BYTES || PERSIST) __syncthreads();  // every input read before exchange 1 reuses xbuf
+      reg_stage<F, 8>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 1); });
+      reg_stage<F, 4>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 2); });
+      reg_stage<F, 2>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 3); });
+      reg_stage<F, 1>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 4); });
+      // ---- exchange 1: (mid, lo) -> (hi, lo), halves by lo >> 4
+      const int lo2 = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi2 = (((tid >> 8) & 1) << 4) | (tid & 15);
+      auto xchg = [&](int ph) {
+        if ((tid >> 9) == ph) {
+#pragma unroll
+          for (int h = 0; h < 32; h++) lds_st<F>(xbuf, x1_at(h, mid, lo & 15), x[h]);
+        }
+        __syncthreads();
+        if ((tid >> 9) == ph) {
+#pragma unroll
+          for (int m = 0; m < 32; m++) x[m] = lds_ld<F>(xbuf, x1_at(hi2, m, lo2 & 15));
+        }
+        __syncthreads();
+      };
+      xchg(0);
+      xchg(1);
     }
+    // ---- round 2: thread (hi, lo) holds mid = 0..31; twiddles w^(((jm << 5) | lo) << s)
+    {
+      const int lo = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
+      reg_stage<F, 16>(x, [&](int jm) { return lds_ld<F>(wtab, (jm << 5) | lo); });
+      reg_stage<F, 8>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 1); });
+      reg_stage<F, 4>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 2); });
+      reg_stage<F, 2>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 3); });
+      reg_stage<F, 1>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 4); });
+      // ---- exchange 2: (hi, lo) -> (hi, mid), halves by hi >> 4 (thread-id bit 8 in both)
+      const int mid3 = ((tid >> 9) << 4) | ((tid >> 4) & 15);
+      auto xchg = [&](int ph) {
+        if (((tid >> 8) & 1) == ph) {
 #pragma unroll
-    for (int h = 0; h < 16; h++) {
-      const int pos = (h << 10) | tl;
-      Fe<F> a = fe_zero<F>();
-      if constexpr (BYTES) {
-        const uint32_t *sw = reinterpret_cast<const uint32_t *>(xbuf);
-        const int b = 7 * pos, d = b >> 2, sh = b & 3;
-        const uint32_t d0 = sw[d], d1 = sw[d + 1], d2 = sw[d + 2];  // (d + 2 < 32768: inside xbuf)
-        a.v[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
-        a.v[1] = __builtin_amdgcn_alignbyte(d2, d1, sh) & 0xffffffu;
-        if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
-      } else if ((size_t)pos < n_valid) {
-        a = fe_load<F>(in, pos);
-        if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
-      }
-      // stage 0 with x[h + 16] = 0: (a, a w^e)
-      x[h + 16] = fe_mul_lazy<F>(a, fe_load<F>(tw0, pos));
-      if constexpr (CANON)
-        x[h] = fe_from_mont<F>(a);
-      else
-        x[h] = a;
+          for (int m = 0; m < 32; m++) lds_st<F>(xbuf, x2_at(hi, m, lo), x[m]);
+        }
+        __syncthreads();
+        if (((tid >> 8) & 1) == ph) {
+#pragma unroll
+          for (int l = 0; l < 32; l++) x[l] = lds_ld<F>(xbuf, x2_at(hi, mid3, l));
+        }
+        __syncthreads();
+      };
+      xchg(0);
+      xchg(1);
     }
-    if constexpr (BYTES) __syncthreads();  // every row byte unpacked before exchange 1 reuses xbuf
-    reg_stage<F, 8>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 1); });
-    reg_stage<F, 4>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 2); });
-    reg_stage<F, 2>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 3); });
-    reg_stage<F, 1>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 4); });
-    // ---- exchange 1: (mid, lo) -> (hi, lo), halves by lo >> 4
-    const int lo2 = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi2 = (((tid >> 8) & 1) << 4) | (tid & 15);
-    auto xchg = [&](int ph) {
-      if ((tid >> 9) == ph) {
-#pragma unroll
-        for (int h = 0; h < 32; h++) lds_st<F>(xbuf, x1_at(h, mid, lo & 15), x[h]);
-      }
-      __syncthreads();
-      if ((tid >> 9) == ph) {
-#pragma unroll
-        for (int m = 0; m < 32; m++) x[m] = lds_ld<F>(xbuf, x1_at(hi2, m, lo2 & 15));
-      }
-      __syncthreads();
-    };
-    xchg(0);
-    xchg(1);
-  }
-  // ---- round 2: thread (hi, lo) holds mid = 0..31; twiddles w^(((jm << 5) | lo) << s)
-  {
-    const int lo = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
-    reg_stage<F, 16>(x, [&](int jm) { return lds_ld<F>(wtab, (jm << 5) | lo); });
-    reg_stage<F, 8>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 1); });
-    reg_stage<F, 4>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 2); });
-    reg_stage<F, 2>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 3); });
-    reg_stage<F, 1>(x, [&](int jm) { return lds_ld<F>(wtab, ((jm << 5) | lo) << 4); });
-    // ---- exchange 2: (hi, lo) -> (hi, mid), halves by hi >> 4 (thread-id bit 8 in both)
-    const int mid3 = ((tid >> 9) << 4) | ((tid >> 4) & 15);
-    auto xchg = [&](int ph) {
-      if (((tid >> 8) & 1) == ph) {
-#pragma unroll
-        for (int m = 0; m < 32; m++) lds_st<F>(xbuf, x2_at(hi, m, lo), x[m]);
-      }
-      __syncthreads();
-      if (((tid >> 8) & 1) == ph) {
-#pragma unroll
-        for (int l = 0; l < 32; l++) x[l] = lds_ld<F>(xbuf, x2_at(hi, mid3, l));
-      }
-      __syncthreads();
-    };
-    xchg(0);
-    xchg(1);
-  }
-  // ---- round 3: thread (hi, mid) holds lo = 0..31; twiddles w^(jm << s) = wtab[jm << (s - 5)]
-  {
+    // ---- round 3: thread (hi, mid) holds lo = 0..31; twiddles w^(jm << s) = wtab[jm << (s - 5)]
     const int mid = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
+    const size_t next = row + gridDim.x;
+    if constexpr (PERSIST) {
+      if (next < n_rows) stage_row<BYTES>(src, src_stride, next, xbuf, tid);
+      asm volatile("" ::: "memory");  // issue the prefetch here, before round 3 (not sunk past it)
+    }
     lo_stage<F, 10>(x, wtab);
     lo_stage<F, 11>(x, wtab);
     lo_stage<F, 12>(x, wtab);
     lo_stage<F, 13>(x, wtab);
     lo_stage<F, 14>(x, wtab);
-    // ---- out: through LDS in halves (hi >> 4), 16-byte units u = ((hi & 15) << 9) | (mid << 4) | (lo >> 1)
-    //      stored at u ^ (hi & 7): a ds_write's 64 lanes land on 8 distinct 16-byte bank slots
-    uint4 *ubuf = reinterpret_cast<uint4 *>(xbuf);
-    uint4 *out = reinterpret_cast<uint4 *>(dst + row * dst_stride * 2);
-    auto store_half = [&](int ph) {
-      if (((tid >> 8) & 1) == ph) {
+    if constexpr (PERSIST) {
+      // the prefetch has landed (every wave's part: the barrier at the next row's top)
+      __builtin_amdgcn_s_waitcnt(0);
+      uint4 *out = reinterpret_cast<uint4 *>(dst + row * dst_stride * 2) + (((hi << 10) | (mid << 5)) >> 1);
 #pragma unroll
-        for (int lp = 0; lp < 16; lp++) {
-          const Fe<F> a = fe_reduce_2p<F>(x[2 * lp]), b = fe_reduce_2p<F>(x[2 * lp + 1]);
-          const int u = ((hi & 15) << 9) | (mid << 4) | lp;
-          ubuf[u ^ (hi & 7)] = make_uint4(a.v[0], a.v[1], b.v[0], b.v[1]);
+      for (int lp = 0; lp < 16; lp++) {
+        const Fe<F> a = fe_reduce_2p<F>(x[2 * lp]), b = fe_reduce_2p<F>(x[2 * lp + 1]);
+        out[lp] = make_uint4(a.v[0], a.v[1], b.v[0], b.v[1]);
+      }
+      row = next;
+      if (row >= n_rows) break;
+    } else {
+      // ---- out: through LDS in halves (hi >> 4), 16-byte units u = ((hi & 15) << 9) | (mid << 4) | (lo >> 1)
+      //      stored at u ^ (hi & 7): a ds_write's 64 lanes land on 8 distinct 16-byte bank slots
+      uint4 *ubuf = reinterpret_cast<uint4 *>(xbuf);
+      uint4 *out = reinterpret_cast<uint4 *>(dst + row * dst_stride * 2);
+      auto store_half = [&](int ph) {
+        if (((tid >> 8) & 1) == ph) {
+#pragma unroll
+          for (int lp = 0; lp < 16; lp++) {
+            const Fe<F> a = fe_reduce_2p<F>(x[2 * lp]), b = fe_reduce_2p<F>(x[2 * lp + 1]);
+            const int u = ((hi & 15) << 9) | (mid << 4) | lp;
+            ubuf[u ^ (hi & 7)] = make_uint4(a.v[0], a.v[1], b.v[0], b.v[1]);
+          }
         }
-      }
-      __syncthreads();
+        __syncthreads();
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int u = (k << 10) | tid;
-        out[(ph << 13) | u] = ubuf[u ^ ((u >> 9) & 7)];
-      }
-    };
-    store_half(0);
-    __syncthreads();
-    store_half(1);
+        for (int k = 0; k < 8; k++) {
+          const int u = (k << 10) | tid;
+          out[(ph << 13) | u] = ubuf[u ^ ((u >> 9) & 7)];
+        }
+      };
+      store_half(0);
+      __syncthreads();
+      store_half(1);
+      break;
+    }
   }
+}
+
+// LCPC_NTT_ROW1: 0 = the four-step pair, 1 = one workgroup per row, 2 = persistent workgroups with
+// the next row prefetched; unset = ROW1_DEFAULT
+inline int row1_mode() {
+  const char *r1 = std::getenv("LCPC_NTT_ROW1");
+  return r1 ? r1[0] - '0' : ROW1_DEFAULT;
+}
+
+inline unsigned persist_grid(size_t n_rows) {
+  static int n_cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return (unsigned)(n_rows < (size_t)n_cu ? n_rows : (size_t)n_cu);
+}
+
+template <class F, bool CANON, bool COPY, bool BYTES>
+hipError_t launch_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
+                    size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, size_t n_persist) {
+  // rows [0, n_persist): persistent workgroups (whole rows); the rest one workgroup per row
+  const uint32_t *tw0 = CANON ? p.d_tw_canon : p.d_tw;
+  prof::Scope ps("ntt_row1", s);
+  if (n_persist)
+    hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, true>), dim3(persist_grid(n_persist)), dim3(1024), 0, s,
+                       src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs, n_persist, (size_t)0);
+  if (n_rows > n_persist)
+    hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, false>), dim3((unsigned)(n_rows - n_persist)), dim3(1024),
+                       0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs, n_rows, n_persist);
+  return hipGetLastError();
 }
 
 template <class F>
 hipError_t launch(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                   size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
-  const uint32_t *tw0 = canon ? p.d_tw_canon : p.d_tw;
-  prof::Scope ps("ntt_row1", s);
-  const dim3 g((unsigned)n_rows), b(1024);
-  if (canon && cp)
-    hipLaunchKernelGGL((k_row_ntt15<F, true, true>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
-  else if (canon)
-    hipLaunchKernelGGL((k_row_ntt15<F, true, false>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
-  else if (cp)
-    hipLaunchKernelGGL((k_row_ntt15<F, false, true>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
-  else
-    hipLaunchKernelGGL((k_row_ntt15<F, false, false>), g, b, 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs);
-  return hipGetLastError();
+  // the LDS-DMA prefetch moves whole rows of 16-byte pieces
+  const bool persist = row1_mode() == 2 && !((uintptr_t)src & 15) && !(ss & 1) && nv == ((size_t)1 << (LOG_N - 1));
+  const size_t np = persist ? n_rows : 0;
+  if (canon && cp) return launch_t<F, true, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np);
+  if (canon) return launch_t<F, true, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np);
+  if (cp) return launch_t<F, false, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np);
+  return launch_t<F, false, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np);
 }
 
-// the proof-of-storage commit from the file image (BYTES above): canonical output, coefficient copy
+// the proof-of-storage commit from the file image (BYTES above): canonical output, coefficient copy;
+// the file's ragged last row (if any) one workgroup of its own
 template <class F>
 hipError_t launch_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst, size_t ds,
                         size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
-  prof::Scope ps("ntt_row1", s);
-  hipLaunchKernelGGL((k_row_ntt15<F, true, true, true>), dim3((unsigned)n_rows), dim3(1024), 0, s,
-                     reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds, p.d_tw, p.d_tw_canon, cp, cs);
-  return hipGetLastError();
+  const size_t whole = n_bytes / ROW_BYTES < n_rows ? n_bytes / ROW_BYTES : n_rows;
+  return launch_t<F, true, true, true>(p, reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds, n_rows,
+                                       s, cp, cs, row1_mode() == 2 ? whole : 0);
 }
 
 }  // namespace ntt_row1

@@ -10,11 +10,12 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def row1_on():
-    """the one-pass kernel for every call of these tests unless four_step() says otherwise"""
+@pytest.fixture(autouse=True, params=["1", "2"], ids=["per_row", "persistent"])
+def row1_on(request):
+    """the one-pass kernel (one workgroup per row, or persistent workgroups with the next row
+    prefetched) for every call of these tests unless four_step() says otherwise"""
     old = os.environ.get("LCPC_NTT_ROW1")
-    os.environ["LCPC_NTT_ROW1"] = "1"
+    os.environ["LCPC_NTT_ROW1"] = request.param
     yield
     if old is None:
         del os.environ["LCPC_NTT_ROW1"]
@@ -76,7 +77,7 @@ def test_row1_extreme_values(gpu, oracle, pattern):
     assert np.array_equal(got, oracle.fft_io(0, row))
 
 
-@pytest.mark.parametrize("length", [37 * NP, 37 * NP + 5, 3 * NP - 1, 1000])
+@pytest.mark.parametrize("length", [37 * NP, 37 * NP + 5, 3 * NP - 1, 1000, 300 * NP])
 def test_row1_commit_device_matches_oracle(gpu, oracle, hipmem, length):
     """the commit path (canonical output + the commitment's coefficient copy), full and ragged
     last rows, against the oracle's coefficient matrix, codeword, hashes and root"""
@@ -99,9 +100,10 @@ def test_row1_commit_device_matches_oracle(gpu, oracle, hipmem, length):
         hipmem.free(d)
 
 
-@pytest.mark.parametrize("row1", ["1", "0"])
+@pytest.mark.parametrize("row1", ["mode", "0"])
 @pytest.mark.parametrize("dims,n_bytes", [
     ((NP, NC), 7 * NP * 5),            # whole rows, one-pass fused unpack
+    ((NP, NC), 7 * NP * 300 + 11),     # more rows than CUs (persistent workgroups loop), a ragged last row
     ((NP, NC), 7 * NP * 5 + 1001),     # a partial last row, a partial last element
     ((NP, NC), 13),                    # two elements, one row
     ((100, 256), 7 * 100 * 3 + 5),     # other dims: packed first
@@ -109,7 +111,8 @@ def test_row1_commit_device_matches_oracle(gpu, oracle, hipmem, length):
 def test_pos_commit_bytes_device(gpu, oracle, hipmem, row1, dims, n_bytes):
     """lcpc_pos_commit_bytes_device == DataField::from_byte_vec + LcCommit::commit (the oracle's
     pos_bytes_to_field + Commit), and == the two-call device path"""
-    os.environ["LCPC_NTT_ROW1"] = row1
+    if row1 == "0":
+        os.environ["LCPC_NTT_ROW1"] = "0"
     np_, nc = dims
     data = np.random.default_rng(n_bytes).integers(0, 256, n_bytes, dtype=np.uint8)
     data[-1] = 0xff

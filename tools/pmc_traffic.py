@@ -67,7 +67,7 @@ def main():
     else:
         # (pos-row1: the one-pass Ft63 row kernel, whose 8-byte loads arrive as 128-byte runs; the
         # x2 read correction is checked by its read figure against the input's size)
-        n_enc = nf["pos_pack7"] if a.code.startswith("pos") else nf["leaf_chunks"]
+        n_enc = nf["pos_pack7"] if a.code == "pos" else nf["leaf_chunks"]
         enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in ("ntt_pass_a", "ntt_pass_b", "ntt_row1")) / n_enc
     for k in kern:
         kern[k]["hbm_bytes_per_step"] = (2.0 * ftot[k] + wtot.get(k, 0.0)) / n_enc
