@@ -217,21 +217,20 @@ def ntt_muls(n):
     return (n // 2) * max(lg - 2, 0) + n
 
 
-ROW1_DEFAULT = "0"  # csrc/ntt_row1.hpp ROW1_DEFAULT
+def row1_active(n, file_image=False):
+    """whether the one-pass Ft63 row kernel (csrc/ntt_row1.hpp) encodes these rate-1/2 2^n-point
+    rows: LCPC_NTT_ROW1 = 1..3 selects it, 0 the four-step pair; unset, the file-image commit
+    (lcpc_pos_commit_bytes_device) takes it and element rows the four-step pair (its row1_mode)"""
+    mode = os.environ.get("LCPC_NTT_ROW1", "1" if file_image else "0")[:1]
+    return n == 1 << 15 and mode in ("1", "2", "3")
 
 
-def row1_active(n):
-    """the one-pass Ft63 row kernel (csrc/ntt_row1.hpp) encodes rate-1/2 2^15-point rows unless
-    LCPC_NTT_ROW1=0 selects the four-step pair"""
-    return n == 1 << 15 and os.environ.get("LCPC_NTT_ROW1", ROW1_DEFAULT)[:1] != "0"
-
-
-def pos_ntt_muls(n):
+def pos_ntt_muls(n, file_image=False):
     """(products per row, model) of the Ft63 encode at the PoS dims: the one-pass kernel does
     stage 0 (16384, the sum branch's R^-1 scaling by a reduction counted as half a product),
     stages 1-9 (16384 each) and round 3's 49 nontrivial products per thread; the four-step pair
     ntt_muls(n)"""
-    if row1_active(n):
+    if row1_active(n, file_image):
         return (n // 2) * 10 + 1024 * 49 + n // 4, ("one-pass 2^15 DIF (ntt_row1): stages 0-9 all products, "
                                                     "stages 10-14 the 49 nontrivial per thread, + n/2 half-cost "
                                                     "R^-1 reductions")
@@ -572,6 +571,7 @@ def pos_workload(args, L, torch, rank, local_rank):
         opened = c.open_columns(cols)
         return pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, c.get_root(), ev, opened)
 
+    fi = args.pos_commit == "bytes"  # the file-image commit (its own row-kernel default)
     return Workload(
         units=n_el, unit="field-elements/s", bytes_per_unit=8,
         metric="proof-of-storage server request: committed field-elements/s (pack+commit+eval+256-col open), "
@@ -585,12 +585,12 @@ def pos_workload(args, L, torch, rank, local_rank):
                                 else "lcpc_pos_bytes_to_field_device + lcpc_commit_new_device")},
         step=step, cpu_baseline=cpu_baseline, parity=parity,
         enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small", "ntt_row1"),
-        enc_kernel_desc=(f"ntt_encode = ntt_row1 (one launch per commit, all {n_rows} rows)" if row1_active(nc) else
+        enc_kernel_desc=(f"ntt_encode = ntt_row1 (one launch per commit, all {n_rows} rows)" if row1_active(nc, fi) else
                          f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
         algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
         leaf_compressions=leaf_compressions(n_rows, nc, 8),
-        traffic_key=(n_el, "Ft63", "pos-row1" if row1_active(nc) else "pos"),
-        mul_count=n_rows * pos_ntt_muls(nc)[0], mul_model=pos_ntt_muls(nc)[1])
+        traffic_key=(n_el, "Ft63", "pos-row1" if row1_active(nc, fi) else "pos"),
+        mul_count=n_rows * pos_ntt_muls(nc, fi)[0], mul_model=pos_ntt_muls(nc, fi)[1])
 
 
 # ---------------------------------------------------------------- launch, cores, shared output

@@ -52,7 +52,7 @@ hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, si
 // element (zero padded); canonical output, the coefficient matrix written to copy.  Only at the
 // one-pass kernel's shape (ntt_rows_pos_bytes_ok), 16-byte-aligned bytes.
 bool ntt_rows_pos_bytes_ok(const NttPlan &p, size_t n_per_row);
-bool ntt_row1_default();  // whether the one-pass kernel is on when LCPC_NTT_ROW1 is unset
+bool ntt_row1_bytes();  // whether the file-image commit takes the one-pass kernel (LCPC_NTT_ROW1)
 hipError_t ntt_rows_pos_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst,
                               size_t dst_stride, size_t n_rows, hipStream_t s, uint32_t *copy, size_t copy_stride);
 

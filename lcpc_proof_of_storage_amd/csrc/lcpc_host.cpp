@@ -120,9 +120,7 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   const uint8_t *src_b = nullptr;
   if (src_bytes) {
     if (fid != LCPC_FT63 || src_is_host) return fail(LCPC_ERR_INVALID_ARG, "file image: device WriteableFt63 only");
-    const char *r1 = std::getenv("LCPC_NTT_ROW1");
-    const bool row1 = r1 ? r1[0] != '0' : ntt_row1_default();
-    if (e->kind != KIND_SDIG && row1 && ntt_rows_pos_bytes_ok(e->plan, np) && !((uintptr_t)d_src & 15)) {
+    if (e->kind != KIND_SDIG && ntt_row1_bytes() && ntt_rows_pos_bytes_ok(e->plan, np) && !((uintptr_t)d_src & 15)) {
       src_b = (const uint8_t *)d_src;
     } else {
       HIP_TRY(packed.alloc(dev, len * 8));

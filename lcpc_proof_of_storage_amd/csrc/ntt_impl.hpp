@@ -166,7 +166,7 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
   if constexpr (F::ID == 0) {
     // PoS default dims: the one-pass row kernel (ntt_row1.hpp) when LCPC_NTT_ROW1 selects it
     // (ROW1_DEFAULT otherwise; 0 = the four-step pair)
-    if (p.log_n == ntt_row1::LOG_N && halfz && ntt_row1::row1_mode() != 0)
+    if (p.log_n == ntt_row1::LOG_N && halfz && ntt_row1::row1_mode(ntt_row1::ROW1_DEFAULT) != 0)
       return ntt_row1::launch<F>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, canon);
   }
   constexpr int HI = F::N >= 8 ? 11 : 12;  // LDS budget of 32-byte fields

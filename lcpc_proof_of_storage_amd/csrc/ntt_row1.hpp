@@ -33,7 +33,10 @@ namespace lcpc {
 namespace ntt_row1 {
 
 constexpr int LOG_N = 15;
-constexpr int ROW1_DEFAULT = 0;  // LCPC_NTT_ROW1 unset: the four-step pair (until measured)
+// LCPC_NTT_ROW1 unset (row1_mode below): element rows take the four-step pair (2.57 ms per 1 GiB
+// request against 2.75-2.97 for this kernel), the file-image commit this kernel one workgroup per
+// row (2.75 ms against 2.93 for k_pack7 + the four-step pair)
+constexpr int ROW1_DEFAULT = 0, ROW1_BYTES_DEFAULT = 1;
 
 // element (hi, mid, lo & 15) of the half lo >> 4 (exchange 1); the XOR spreads a ds_read's lanes
 // (16 values of hi) over 16 bank pairs
@@ -121,7 +124,7 @@ __device__ __forceinline__ void stage_row(const uint32_t *src, size_t src_stride
   for (int i = 0; i < PIECES; i++) glds16(g + i * 1024, sb + i * 1024);
 }
 
-template <class F, bool CANON, bool COPY, bool BYTES, bool PERSIST>
+template <class F, bool CANON, bool COPY, bool BYTES, bool PERSIST, bool DIRECT = PERSIST>
 __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__ src, size_t src_stride,
                                                     size_t n_valid, uint32_t *__restrict__ dst, size_t dst_stride,
                                                     const uint32_t *__restrict__ tw,
@@ -251,15 +254,16 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
     lo_stage<F, 12>(x, wtab);
     lo_stage<F, 13>(x, wtab);
     lo_stage<F, 14>(x, wtab);
-    if constexpr (PERSIST) {
+    if constexpr (DIRECT) {
       // the prefetch has landed (every wave's part: the barrier at the next row's top)
-      __builtin_amdgcn_s_waitcnt(0);
+      if constexpr (PERSIST) __builtin_amdgcn_s_waitcnt(0);
       uint4 *out = reinterpret_cast<uint4 *>(dst + row * dst_stride * 2) + (((hi << 10) | (mid << 5)) >> 1);
 #pragma unroll
       for (int lp = 0; lp < 16; lp++) {
         const Fe<F> a = fe_reduce_2p<F>(x[2 * lp]), b = fe_reduce_2p<F>(x[2 * lp + 1]);
         out[lp] = make_uint4(a.v[0], a.v[1], b.v[0], b.v[1]);
       }
+      if constexpr (!PERSIST) break;
       row = next;
       if (row >= n_rows) break;
     } else {
@@ -291,11 +295,13 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
   }
 }
 
-// LCPC_NTT_ROW1: 0 = the four-step pair, 1 = one workgroup per row, 2 = persistent workgroups with
-// the next row prefetched; unset = ROW1_DEFAULT
-inline int row1_mode() {
+// LCPC_NTT_ROW1: 0 = the four-step pair (after k_pack7 for a file image), 1 = one workgroup per
+// row, 2 = persistent workgroups with the next row prefetched, 3 = as 1 with the outputs stored
+// straight from registers; unset = dflt (ntt_rows: 0, the file-image commit: 1 -- the measured
+// choices)
+inline int row1_mode(int dflt) {
   const char *r1 = std::getenv("LCPC_NTT_ROW1");
-  return r1 ? r1[0] - '0' : ROW1_DEFAULT;
+  return r1 && r1[0] >= '0' && r1[0] <= '3' ? r1[0] - '0' : dflt;
 }
 
 inline unsigned persist_grid(size_t n_rows) {
@@ -310,14 +316,17 @@ inline unsigned persist_grid(size_t n_rows) {
 
 template <class F, bool CANON, bool COPY, bool BYTES>
 hipError_t launch_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
-                    size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, size_t n_persist) {
+                    size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, size_t n_persist, bool direct) {
   // rows [0, n_persist): persistent workgroups (whole rows); the rest one workgroup per row
   const uint32_t *tw0 = CANON ? p.d_tw_canon : p.d_tw;
   prof::Scope ps("ntt_row1", s);
   if (n_persist)
     hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, true>), dim3(persist_grid(n_persist)), dim3(1024), 0, s,
                        src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs, n_persist, (size_t)0);
-  if (n_rows > n_persist)
+  if (n_rows > n_persist && direct)
+    hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, false, true>), dim3((unsigned)(n_rows - n_persist)),
+                       dim3(1024), 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs, n_rows, n_persist);
+  else if (n_rows > n_persist)
     hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, false>), dim3((unsigned)(n_rows - n_persist)), dim3(1024),
                        0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs, n_rows, n_persist);
   return hipGetLastError();
@@ -327,12 +336,14 @@ template <class F>
 hipError_t launch(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                   size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
   // the LDS-DMA prefetch moves whole rows of 16-byte pieces
-  const bool persist = row1_mode() == 2 && !((uintptr_t)src & 15) && !(ss & 1) && nv == ((size_t)1 << (LOG_N - 1));
+  const int mode = row1_mode(ROW1_DEFAULT);
+  const bool persist = mode == 2 && !((uintptr_t)src & 15) && !(ss & 1) && nv == ((size_t)1 << (LOG_N - 1));
   const size_t np = persist ? n_rows : 0;
-  if (canon && cp) return launch_t<F, true, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np);
-  if (canon) return launch_t<F, true, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np);
-  if (cp) return launch_t<F, false, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np);
-  return launch_t<F, false, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np);
+  const bool dr = mode == 3;
+  if (canon && cp) return launch_t<F, true, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np, dr);
+  if (canon) return launch_t<F, true, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np, dr);
+  if (cp) return launch_t<F, false, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np, dr);
+  return launch_t<F, false, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np, dr);
 }
 
 // the proof-of-storage commit from the file image (BYTES above): canonical output, coefficient copy;
@@ -341,8 +352,9 @@ template <class F>
 hipError_t launch_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst, size_t ds,
                         size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
   const size_t whole = n_bytes / ROW_BYTES < n_rows ? n_bytes / ROW_BYTES : n_rows;
+  const int mode = row1_mode(ROW1_BYTES_DEFAULT);
   return launch_t<F, true, true, true>(p, reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds, n_rows,
-                                       s, cp, cs, row1_mode() == 2 ? whole : 0);
+                                       s, cp, cs, mode == 2 ? whole : 0, mode == 3);
 }
 
 }  // namespace ntt_row1

@@ -10,7 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["1", "2"], ids=["per_row", "persistent"])
+@pytest.fixture(autouse=True, params=["1", "2", "3"], ids=["per_row", "persistent", "per_row_direct"])
 def row1_on(request):
     """the one-pass kernel (one workgroup per row, or persistent workgroups with the next row
     prefetched) for every call of these tests unless four_step() says otherwise"""

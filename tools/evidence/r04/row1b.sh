@@ -13,4 +13,5 @@ LCPC_NTT_ROW1=0 timeout -k 10 300 python -u bench.py --code pos --steps 16 --pos
 LCPC_NTT_ROW1=2 bash tools/pmc_ntt.sh r04i/pmc_row2 --code pos > $O/pmc_row2.log 2>&1 && \
 LCPC_NTT_ROW1=1 bash tools/pmc_ntt.sh r04i/pmc_row1 --code pos > $O/pmc_row1.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --sharded-n1 0 > $O/k20_a.json 2> $O/k20_a.err && \
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --sharded-n1 0 > $O/k20_b.json 2> $O/k20_b.err
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --sharded-n1 0 > $O/k20_b.json 2> $O/k20_b.err && \
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --field Ft255 --rho 1/4 --sharded-n1 0 > $O/ft255_rho14.json 2> $O/ft255_rho14.err
