@@ -147,3 +147,21 @@ def test_pos_commit_bytes_device_rejects(gpu, hipmem):
             gpu.LcCommit.commit_pos_bytes_device(d, 0, enc)           # empty
     finally:
         hipmem.free(d)
+
+
+def test_pos_commit_bytes_device_sdig(gpu, oracle, hipmem):
+    """a Brakedown (SDIG) WriteableFt63 encoding takes the packed path: the same commitment as
+    packing first and committing the elements"""
+    n_bytes = 7 * 3000 + 3
+    data = np.random.default_rng(7).integers(0, 256, n_bytes, dtype=np.uint8)
+    el = oracle.pos_bytes_to_field(data.tobytes())
+    enc = gpu.SdigEncoding.new(0, el.size, 0)
+    d = hipmem.to_device(np.concatenate([data, np.zeros((-n_bytes) % 8, np.uint8)]).view(np.uint64))
+    de = hipmem.to_device(el)
+    try:
+        g = gpu.LcCommit.commit_pos_bytes_device(d, n_bytes, enc)
+        assert gpu.LcCommit.commit_device(de, el.size, enc).get_root() == g.get_root()
+        assert g.get_root() == gpu.LcCommit.commit(el, enc).get_root()
+    finally:
+        hipmem.free(d)
+        hipmem.free(de)
