@@ -118,11 +118,14 @@ struct Device {
     (void)hipSetDevice(id);
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = lo = 0;
-    static const bool prio = [] {
+    // LCPC_PRIORITY_STREAMS: 1 (default) the prover's streams above the bulk ones, 0 one
+    // priority, 2 the other way round (bulk commits first; the prover's kernels fill their gaps)
+    static const int prio = [] {
       const char *v = getenv("LCPC_PRIORITY_STREAMS");
-      return !(v && v[0] == '0');
+      return v && (v[0] == '0' || v[0] == '2') ? v[0] - '0' : 1;
     }();
-    if (!prio) hi = lo;
+    if (prio == 0) hi = lo;
+    if (prio == 2) std::swap(hi, lo);
     if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? hi : lo) != hipSuccess) return nullptr;
     return s;
   }
