@@ -589,7 +589,8 @@ def pos_workload(args, L, torch, rank, local_rank):
                          f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
         algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
         leaf_compressions=leaf_compressions(n_rows, nc, 8),
-        traffic_key=(n_el, "Ft63", "pos-row1" if row1_active(nc, fi) else "pos"),
+        traffic_key=(n_el, "Ft63", "pos-row1" if row1_active(nc, fi) else
+                     "pos-a7" if fi and os.environ.get("LCPC_NTT_ROW1", "")[:1] == "4" else "pos"),
         mul_count=n_rows * pos_ntt_muls(nc, fi)[0], mul_model=pos_ntt_muls(nc, fi)[1])
 
 

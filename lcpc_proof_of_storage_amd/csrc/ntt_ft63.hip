@@ -16,6 +16,8 @@ hipError_t ntt_rows_pos_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_b
   if (!ntt_rows_pos_bytes_ok(p, (size_t)1 << (ntt_row1::LOG_N - 1)) || ((uintptr_t)bytes & 15) || !copy)
     return hipErrorInvalidValue;
   if (n_rows == 0) return hipSuccess;
+  if (ntt_row1::row1_mode(ntt_row1::ROW1_BYTES_DEFAULT) == 4)
+    return ntt_detail::ntt_rows_bytes_fourstep(p, bytes, n_bytes, dst, dst_stride, n_rows, s, copy, copy_stride);
   return ntt_row1::launch_bytes<Ft63>(p, bytes, n_bytes, dst, dst_stride, n_rows, s, copy, copy_stride);
 }
 hipError_t ntt_tw_table_ft63(uint32_t *tw, int log_n, bool inverse, hipStream_t s) {

@@ -297,11 +297,11 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
 
 // LCPC_NTT_ROW1: 0 = the four-step pair (after k_pack7 for a file image), 1 = one workgroup per
 // row, 2 = persistent workgroups with the next row prefetched, 3 = as 1 with the outputs stored
-// straight from registers; unset = dflt (ntt_rows: 0, the file-image commit: 1 -- the measured
-// choices)
+// straight from registers, 4 = (file images) the four-step pair with the unpack in pass A;
+// unset = dflt (ntt_rows: 0, the file-image commit: 1 -- the measured choices)
 inline int row1_mode(int dflt) {
   const char *r1 = std::getenv("LCPC_NTT_ROW1");
-  return r1 && r1[0] >= '0' && r1[0] <= '3' ? r1[0] - '0' : dflt;
+  return r1 && r1[0] >= '0' && r1[0] <= '4' ? r1[0] - '0' : dflt;
 }
 
 inline unsigned persist_grid(size_t n_rows) {

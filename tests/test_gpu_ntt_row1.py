@@ -10,7 +10,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["1", "2", "3"], ids=["per_row", "persistent", "per_row_direct"])
+@pytest.fixture(autouse=True, params=["1", "2", "3", "4"],
+                ids=["per_row", "persistent", "per_row_direct", "fourstep_unpack"])
 def row1_on(request):
     """the one-pass kernel (one workgroup per row, or persistent workgroups with the next row
     prefetched) for every call of these tests unless four_step() says otherwise"""
