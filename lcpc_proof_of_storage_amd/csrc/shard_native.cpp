@@ -462,6 +462,14 @@ bool shard_mode2_allowed(int nranks) {
   return e && e[0] == '1';
 }
 bool shard_prio_streams() { return shard_prove_stream_mode() != 0; }
+// encode streams of the pipelined driver (LCPC_SHARD_BULK_STREAMS: 1 default, or 2)
+size_t shard_bulk_streams() {
+  static const size_t n = [] {
+    const char *v = getenv("LCPC_SHARD_BULK_STREAMS");
+    return v && v[0] == '2' ? (size_t)2 : (size_t)1;
+  }();
+  return n;
+}
 // (3: every stream of the driver -- encode, exchange, prove -- at high priority)
 bool shard_all_high() { return shard_prove_stream_mode() == 3; }
 bool shard_prove_high() { return shard_prove_stream_mode() >= 2; }
@@ -1557,18 +1565,31 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     comm->encoder = std::make_unique<TaskPool>(1, e->dev->id);
   }
   TaskPool &pool = *comm->pool, &launch = *comm->launch, &encoder = *comm->encoder;
-  hipStream_t bulk = e->dev->acquire_stream(shard_all_high());
-  if (!bulk) return fail(LCPC_ERR_DEVICE, "no HIP stream");
-  struct BulkRelease {  // (destroyed after cs: returns the stream to the pool)
+  // the encode streams: one (polynomials encode in order), or shard_bulk_streams() taken in turn
+  // (LCPC_SHARD_BULK_STREAMS=2: consecutive polynomials' encode kernels may overlap)
+  const size_t n_bulk = shard_bulk_streams();
+  hipStream_t bulks[2] = {nullptr, nullptr};
+  for (size_t i = 0; i < n_bulk; i++)
+    if (!(bulks[i] = e->dev->acquire_stream(shard_all_high()))) {
+      if (i) e->dev->release_stream(bulks[0], shard_all_high());
+      return fail(LCPC_ERR_DEVICE, "no HIP stream");
+    }
+  struct BulkRelease {  // (destroyed after cs: returns the streams to the pool)
     Device *d;
-    hipStream_t s;
-    ~BulkRelease() { d->release_stream(s, shard_all_high()); }
-  } bulk_release{e->dev, bulk};
+    hipStream_t *s;
+    ~BulkRelease() {
+      for (int i = 0; i < 2; i++)
+        if (s[i]) d->release_stream(s[i], shard_all_high());
+    }
+  } bulk_release{e->dev, bulks};
   std::vector<ShardPtr> cs(n_polys);
   struct BulkDrain {  // (destroyed before cs: no polynomial is torn down under its running encode)
-    hipStream_t s;
-    ~BulkDrain() { (void)hipStreamSynchronize(s); }
-  } bulk_drain{bulk};
+    hipStream_t *s;
+    ~BulkDrain() {
+      for (int i = 0; i < 2; i++)
+        if (s[i]) (void)hipStreamSynchronize(s[i]);
+    }
+  } bulk_drain{bulks};
   std::vector<std::future<lcpc_status>> pending(n_polys);  // the polynomial's outstanding launch task
   std::deque<std::pair<size_t, std::future<lcpc_status>>> finals;  // (poly, host_proof)
   std::vector<size_t> to_finalize;
@@ -1613,7 +1634,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   };
   auto start = [&](size_t k) {
     pending[k] = encoder.submit(wrap([&, k]() -> lcpc_status {
-      lcpc_status s2 = shard_init(e, comm, n_rows, cs[k], bulk);
+      lcpc_status s2 = shard_init(e, comm, n_rows, cs[k], bulks[k % n_bulk]);
       if (s2) return s2;
       cs[k]->poly = k;
       return stage_pre_commit(cs[k].get(), d_rows[k]);
@@ -1806,7 +1827,7 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
   // the streams lcpc_sharded_commit_prove_many acquires: one shared (bulk) encode stream, and a
   // prove stream per polynomial in flight
   std::vector<hipStream_t> lo, hi;
-  lo.push_back(dev->acquire_stream(shard_all_high()));
+  for (size_t i = 0; i < shard_bulk_streams(); i++) lo.push_back(dev->acquire_stream(shard_all_high()));
   for (size_t k = 0; k < depth && shard_prio_streams(); k++) hi.push_back(dev->acquire_stream(shard_prove_high()));
   for (hipStream_t x : lo)
     if (x) dev->release_stream(x, shard_all_high());
