@@ -462,11 +462,14 @@ bool shard_mode2_allowed(int nranks) {
   return e && e[0] == '1';
 }
 bool shard_prio_streams() { return shard_prove_stream_mode() != 0; }
-// encode streams of the pipelined driver (LCPC_SHARD_BULK_STREAMS: 1 default, or 2)
+// encode streams of the pipelined driver, taken in turn by polynomial (LCPC_SHARD_BULK_STREAMS=1
+// or 2, default 2): with two, consecutive polynomials' encode kernels overlap each other's tails
+// (one-rank K = 20: 11.1 / 11.5 against 11.0 / 11.3 G/s with one, interleaved runs,
+// profiles/r04_sharded_bulk_streams_ab.json) while the roots still arrive nearly in order
 size_t shard_bulk_streams() {
   static const size_t n = [] {
     const char *v = getenv("LCPC_SHARD_BULK_STREAMS");
-    return v && v[0] == '2' ? (size_t)2 : (size_t)1;
+    return v && v[0] == '1' ? (size_t)1 : (size_t)2;
   }();
   return n;
 }
@@ -1565,8 +1568,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     comm->encoder = std::make_unique<TaskPool>(1, e->dev->id);
   }
   TaskPool &pool = *comm->pool, &launch = *comm->launch, &encoder = *comm->encoder;
-  // the encode streams: one (polynomials encode in order), or shard_bulk_streams() taken in turn
-  // (LCPC_SHARD_BULK_STREAMS=2: consecutive polynomials' encode kernels may overlap)
+  // the encode streams (shard_bulk_streams(), taken in turn by polynomial)
   const size_t n_bulk = shard_bulk_streams();
   hipStream_t bulks[2] = {nullptr, nullptr};
   for (size_t i = 0; i < n_bulk; i++)
@@ -1824,7 +1826,7 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
   if (!st) st = take(rdsz, rpsz, root_depth);
   for (void *p : blocks) dev->release(p);
   for (void *p : pins) dev->pinned_put(p);
-  // the streams lcpc_sharded_commit_prove_many acquires: one shared (bulk) encode stream, and a
+  // the streams lcpc_sharded_commit_prove_many acquires: the shared (bulk) encode streams, and a
   // prove stream per polynomial in flight
   std::vector<hipStream_t> lo, hi;
   for (size_t i = 0; i < shard_bulk_streams(); i++) lo.push_back(dev->acquire_stream(shard_all_high()));
