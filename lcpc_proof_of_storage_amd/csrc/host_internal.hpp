@@ -22,6 +22,7 @@
 #include "field.hpp"
 #include "kernels.hpp"
 #include "pos.hpp"
+#include "pool.hpp"
 #include "prof.hpp"
 #include "sdig.hpp"
 #include "transcript.hpp"
@@ -70,6 +71,26 @@ inline FieldInfo field_info(int fid) {
 inline bool valid_field(int f) { return f >= 0 && f <= 4; }
 
 // ---------------------------------------------------------------- per-device context
+// The stream-ordered block pool's HIP backend (pool.hpp).
+struct HipPoolBackend {
+  using Stream = hipStream_t;
+  using Event = hipEvent_t;
+  Event event_new() {
+    hipEvent_t e = nullptr;
+    return hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess ? e : nullptr;
+  }
+  void event_free(Event e) { (void)hipEventDestroy(e); }
+  bool record(Event e, Stream s) { return hipEventRecord(e, s) == hipSuccess; }
+  bool done(Event e) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipErrorNotReady) (void)hipGetLastError();
+    return r == hipSuccess;
+  }
+  bool wait(Stream s, Event e) { return hipStreamWaitEvent(s, e, 0) == hipSuccess; }
+  bool sync(Event e) { return hipEventSynchronize(e) == hipSuccess; }
+  void drain(Stream s) { (void)hipStreamSynchronize(s); }
+};
+
 // A pool of HIP streams and a caching allocator per device.  Every API call leases its own
 // stream, so independent commitments run concurrently (their CPU-side Fiat-Shamir work
 // overlaps another commitment's kernels); only pool bookkeeping is locked.
@@ -79,7 +100,10 @@ struct Device {
   std::string init_err;
   std::mutex mu;  // guards the pools below
   std::vector<hipStream_t> idle_streams[2];  // [0] bulk (commit / encode), [1] high priority
-  std::multimap<size_t, void *> free_blocks;  // size -> block
+  // device blocks: cached by exact size, each ordered after a fence on the streams that used it
+  // (pool.hpp); sizes = every block this device allocated
+  HipPoolBackend pool_backend;
+  lcpc_pool::OrderedPool<HipPoolBackend> blocks{pool_backend};
   std::map<void *, size_t> sizes;
 
   // high-priority streams carry the prover's short latency-critical kernels (row
@@ -116,18 +140,25 @@ struct Device {
     prof::HostScope hs("rt_stream_create");
     hipStream_t s = nullptr;
     (void)hipSetDevice(id);
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = lo = 0;
-    // LCPC_PRIORITY_STREAMS: 1 (default) the prover's streams above the bulk ones, 0 one
-    // priority, 2 the other way round (bulk commits first; the prover's kernels fill their gaps)
-    static const int prio = [] {
-      const char *v = getenv("LCPC_PRIORITY_STREAMS");
-      return v && (v[0] == '0' || v[0] == '2') ? v[0] - '0' : 1;
-    }();
-    if (prio == 0) hi = lo;
-    if (prio == 2) std::swap(hi, lo);
-    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? hi : lo) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, stream_priority(high)) != hipSuccess) return nullptr;
     return s;
+  }
+  // Every stream at ONE priority (round 5): mixed priorities are the one condition under which a
+  // wrong commitment was ever observed (eight ranks on one GPU), and a high-priority
+  // prover bought nothing measurable (profiles/r04_k20_stream_priority_ab.json).  The two stream
+  // pools stay separate so that LCPC_PRIORITY_STREAMS=1 can still put the prover's streams (and the
+  // sharded driver's) above the bulk ones for A/B runs.
+  static bool priority_streams() {
+    static const bool v = [] {
+      const char *e = getenv("LCPC_PRIORITY_STREAMS");
+      return e && e[0] == '1';
+    }();
+    return v;
+  }
+  static int stream_priority(bool high) {
+    int lo = 0, hi = 0;
+    if (!priority_streams() || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return 0;
+    return high ? hi : lo;
   }
   // Commitments in FIFO order (LCPC_COMMIT_FIFO=1; off by default): every commit enqueues its
   // whole kernel sequence on this one stream under commit_mu, so concurrent commits run back to
@@ -156,18 +187,12 @@ struct Device {
     std::lock_guard<std::mutex> lk(mu);
     idle_streams[high ? 1 : 0].push_back(s);
   }
-  hipError_t alloc(void **p, size_t bytes) {
-    if (bytes == 0) bytes = 16;
-    bytes = (bytes + 255) & ~(size_t)255;
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      auto it = free_blocks.find(bytes);
-      if (it != free_blocks.end()) {
-        *p = it->second;
-        free_blocks.erase(it);
-        return hipSuccess;
-      }
-    }
+  static size_t round_bytes(size_t bytes) { return ((bytes ? bytes : 16) + 255) & ~(size_t)255; }
+  // a block of at least `bytes`, ordered after every earlier use of it: on stream `s` when given
+  // (device-side waits), on the host otherwise
+  hipError_t alloc(void **p, size_t bytes, hipStream_t s = nullptr) {
+    bytes = round_bytes(bytes);
+    if ((*p = blocks.take(bytes, s))) return hipSuccess;
     prof::HostScope hs("rt_hipMalloc");
     // a pool thread's current device is whatever it last set (GPU 0 for a fresh thread): the
     // block must come from THIS device, so make it current before allocating
@@ -185,13 +210,18 @@ struct Device {
     }
     return e;
   }
-  // the caller guarantees no queued work still uses p
-  void release(void *p) {
+  // back to the pool; the streams ss[0..n) may still have work queued on it (a fence is recorded
+  // on each), none if the caller knows every use has completed
+  void release(void *p, const hipStream_t *ss = nullptr, int n = 0) {
     if (!p) return;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = sizes.find(p);
-    if (it == sizes.end()) return;
-    free_blocks.emplace(it->second, p);
+    size_t bytes;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = sizes.find(p);
+      if (it == sizes.end()) return;
+      bytes = it->second;
+    }
+    blocks.put(p, bytes, ss, n);
   }
   // page-locked host blocks for the file paths' staging (pinning is slow: blocks are reused)
   std::multimap<size_t, void *> pinned_free;
@@ -225,12 +255,13 @@ struct Device {
   void trim() {
     (void)hipSetDevice(id);
     (void)hipDeviceSynchronize();
+    std::vector<void *> gone;
+    blocks.drain([&](void *p) { gone.push_back(p); });
     std::lock_guard<std::mutex> lk(mu);
-    for (auto &kv : free_blocks) {
-      sizes.erase(kv.second);
-      (void)hipFree(kv.second);
+    for (void *p : gone) {
+      sizes.erase(p);
+      (void)hipFree(p);
     }
-    free_blocks.clear();
   }
 };
 
@@ -312,38 +343,76 @@ struct Lease {
   Lease &operator=(const Lease &) = delete;
 };
 
-// RAII device buffer from the pool.  It remembers the stream it was allocated for and
-// drains that stream before returning the block (error paths leave work queued).
+// RAII device buffer from the stream-ordered pool.  It remembers the streams that use it -- the
+// one current when it was allocated (t_stream) and any added with use() -- and returns its block
+// with a fence on each (pool.hpp): the block's next owner is ordered after every write still
+// queued here, with no host drain.  settle() / settle(s) say that all / s's uses have completed
+// (the fence is then skipped), an optimisation only: an unsettled buffer is always safe.
 struct DBuf {
+  static constexpr int MAXS = lcpc_pool::OrderedPool<HipPoolBackend>::MAX_STREAMS;
   Device *d = nullptr;
   void *p = nullptr;
   size_t n = 0;
-  hipStream_t s = nullptr;
+  hipStream_t s = nullptr;      // the stream current at allocation (its first user)
+  hipStream_t xs[MAXS - 1] = {};  // further streams that use it (use())
+  int nx = 0;
   DBuf() = default;
   DBuf(const DBuf &) = delete;
   DBuf &operator=(const DBuf &) = delete;
-  DBuf(DBuf &&o) noexcept : d(o.d), p(o.p), n(o.n), s(o.s) { o.p = nullptr; }
+  DBuf(DBuf &&o) noexcept : d(o.d), p(o.p), n(o.n), s(o.s), nx(o.nx) {
+    for (int i = 0; i < nx; i++) xs[i] = o.xs[i];
+    o.p = nullptr;
+    o.nx = 0;
+  }
   DBuf &operator=(DBuf &&o) noexcept {
     reset();
-    d = o.d; p = o.p; n = o.n; s = o.s; o.p = nullptr;
+    d = o.d; p = o.p; n = o.n; s = o.s; nx = o.nx;
+    for (int i = 0; i < nx; i++) xs[i] = o.xs[i];
+    o.p = nullptr;
+    o.nx = 0;
     return *this;
   }
   ~DBuf() { reset(); }
   void reset() {
     if (p && d) {
-      if (s) (void)hipStreamSynchronize(s);
-      d->release(p);
+      hipStream_t ss[MAXS];
+      int k = 0;
+      if (s) ss[k++] = s;
+      for (int i = 0; i < nx; i++) ss[k++] = xs[i];
+      d->release(p, ss, k);
     }
     p = nullptr;
+    s = nullptr;
+    nx = 0;
   }
-  // the queued work using this buffer has completed (no drain needed at release)
-  void settle() { s = nullptr; }
+  // another stream works on this buffer (its work is fenced at release)
+  void use(hipStream_t x) {
+    if (!x || x == s) return;
+    for (int i = 0; i < nx; i++)
+      if (xs[i] == x) return;
+    if (nx < MAXS - 1) {
+      xs[nx++] = x;
+    } else {  // (never in the library: at most three streams touch a buffer) drain it instead
+      (void)hipStreamSynchronize(x);
+    }
+  }
+  // every queued use of this buffer has completed (no fence needed at release)
+  void settle() {
+    s = nullptr;
+    nx = 0;
+  }
+  // stream x has drained: its uses need no fence
+  void settle(hipStream_t x) {
+    if (x && s == x) s = nullptr;
+    for (int i = 0; i < nx; i++)
+      if (xs[i] == x) xs[i--] = xs[--nx];
+  }
   hipError_t alloc(Device *dev, size_t bytes) {
     reset();
     d = dev;
     n = bytes;
     s = t_stream;
-    return dev->alloc(&p, bytes);
+    return dev->alloc(&p, bytes, t_stream);
   }
   template <class T>
   T *as() const { return reinterpret_cast<T *>(p); }
@@ -558,8 +627,7 @@ inline lcpc_status encode_rows_any(const lcpc_encoding *e, const uint32_t *src, 
   HIP_TRY(transpose_elems(e->fid, src, n_rows, np, ss, nv < np ? nv : np, cw.as<uint32_t>(), n_rows, s));
   HIP_TRY(sdig_encode_cm(e->sdig, cw.as<uint32_t>(), n_rows, tmp.as<uint32_t>(), s));
   HIP_TRY(transpose_elems(e->fid, cw.as<uint32_t>(), nc, n_rows, n_rows, n_rows, dst, ds, s));
-  HIP_TRY(hipStreamSynchronize(s));  // before the pool reuses cw / tmp
-  return LCPC_OK;
+  return LCPC_OK;  // (cw / tmp go back to the pool fenced on s: no drain here)
 }
 
 // Device address of page-locked (hipHostMalloc'd) host memory, or nullptr for pageable memory.

@@ -143,27 +143,38 @@ class TaskPool {
 }  // namespace
 
 // ---------------------------------------------------------------- the communicator
+// What a communicator shares with its sharded commitments, refcounted so that either may be freed
+// first: the comm stream (a commitment freed while an exchange of it is still queued fences its
+// buffers on it) and the free list of per-(polynomial, stage) events.
+struct CommShared {
+  hipStream_t cs = nullptr;  // the comm stream: every exchange, in issue order
+  std::mutex ev_mu;
+  std::vector<hipEvent_t> ev_free;
+  ~CommShared() {
+    if (cs) {
+      (void)hipStreamSynchronize(cs);
+      (void)hipStreamDestroy(cs);
+    }
+    for (hipEvent_t e : ev_free) (void)hipEventDestroy(e);
+  }
+};
+
 struct lcpc_comm {
   int nranks = 1, rank = 0;
   bool is_rccl = false;
   ncclComm_t nc = nullptr;
   lcpc_comm_ops ops{};
   Device *dev = nullptr;
-  hipStream_t cs = nullptr;  // the comm stream: every exchange, in issue order
+  hipStream_t cs = nullptr;  // = shared->cs (owned by shared)
+  std::shared_ptr<CommShared> shared = std::make_shared<CommShared>();
   std::mutex mu;             // one sharded call at a time
   // the pipelined driver's host threads (transcripts and proofs, compute launches, encodes),
   // started on its first call and kept across calls: idle between calls, joined last
   std::unique_ptr<TaskPool> pool, launch, encoder;
-  // the per-(polynomial, stage) events of finished polynomials, for reuse (ev_take / ev_give)
-  std::mutex ev_mu;
-  std::vector<hipEvent_t> ev_free;
   ~lcpc_comm() {
-    if (cs) {
-      (void)hipStreamSynchronize(cs);
-      (void)hipStreamDestroy(cs);
-    }
-    for (hipEvent_t e : ev_free) (void)hipEventDestroy(e);
+    if (cs) (void)hipStreamSynchronize(cs);
     if (nc) rccl().CommDestroy(nc);
+    // the stream and the event free list go with the last holder of `shared`
   }
 };
 
@@ -378,7 +389,8 @@ constexpr size_t st_gather(size_t r) { return S_R0 + 2 * r + 1; }
 
 struct lcpc_sharded_commit {
   const lcpc_encoding *e = nullptr;
-  lcpc_comm *comm = nullptr;
+  lcpc_comm *comm = nullptr;              // (only during the calls that take it)
+  std::shared_ptr<CommShared> shared;     // its comm stream and event free list (outlive it if need be)
   Device *dev = nullptr;
   int fid = 1, wb = 16, G = 1, me = 0;
   bool sdig = false;  // Brakedown: element-major shard [n_cols][nr] (canonical codeword, as Ligero's)
@@ -420,9 +432,9 @@ struct lcpc_sharded_commit {
     for (hipEvent_t &x : ev)
       if (x) mine.push_back(x), x = nullptr;
     if (!mine.empty()) {
-      if (comm && ev_quiet) {
-        std::lock_guard<std::mutex> lk(comm->ev_mu);
-        comm->ev_free.insert(comm->ev_free.end(), mine.begin(), mine.end());
+      if (shared && ev_quiet) {
+        std::lock_guard<std::mutex> lk(shared->ev_mu);
+        shared->ev_free.insert(shared->ev_free.end(), mine.begin(), mine.end());
       } else {
         for (hipEvent_t x : mine) (void)hipEventDestroy(x);  // (HIP keeps a queued wait's marker alive)
       }
@@ -486,12 +498,17 @@ struct ShardDeleter {
     c->sp = nullptr;
     if (s) (void)hipStreamSynchronize(s);
     if (sp) (void)hipStreamSynchronize(sp);
-    // the stream has drained: no buffer needs its own drain on release (one hipStreamSynchronize
-    // per buffer cost ~0.4 ms per polynomial)
+    // s and sp have drained: their uses need no fence.  An exchange of this polynomial may still
+    // be queued on the comm stream when it is torn down early (an error path: !ev_quiet), so then
+    // every buffer is fenced on that stream: the pool orders the block's next owner after it
+    // (pool.hpp) without blocking here.
+    hipStream_t cs = !c->ev_quiet && c->shared ? c->shared->cs : nullptr;
     for (DBuf *b : {&c->coeffs, &c->comm_rows, &c->hashes, &c->cv_send, &c->cv_recv, &c->sub, &c->subs, &c->sdig_tmp,
                     &c->bt, &c->tens, &c->part_d, &c->allpart, &c->sum, &c->canon, &c->didx, &c->mycols,
-                    &c->allcols, &c->dpaths, &c->scratch})
+                    &c->allcols, &c->dpaths, &c->scratch}) {
       b->settle();
+      if (cs) b->use(cs);
+    }
     delete c;
     if (s) d->release_stream(s, shard_all_high());
     if (sp) d->release_stream(sp, shard_prove_high());
@@ -552,6 +569,7 @@ lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, S
   ShardPtr c(new lcpc_sharded_commit());
   c->e = e;
   c->comm = comm;
+  c->shared = comm->shared;
   c->dev = e->dev;
   shard_geom(c.get(), e->fid, e->n_per_row, e->n_cols, n_rows, comm->nranks, comm->rank, e->kind == KIND_SDIG);
   HIP_TRY(hipSetDevice(c->dev->id));
@@ -586,10 +604,10 @@ lcpc_status ev_need(lcpc_sharded_commit *c, size_t s0, size_t s1) {
   for (size_t i = 3 * s0; i < 3 * s1; i++) {
     if (c->ev[i]) continue;
     {
-      std::lock_guard<std::mutex> lk(c->comm->ev_mu);
-      if (!c->comm->ev_free.empty()) {
-        c->ev[i] = c->comm->ev_free.back();
-        c->comm->ev_free.pop_back();
+      std::lock_guard<std::mutex> lk(c->shared->ev_mu);
+      if (!c->shared->ev_free.empty()) {
+        c->ev[i] = c->shared->ev_free.back();
+        c->shared->ev_free.pop_back();
         continue;
       }
     }
@@ -1281,13 +1299,10 @@ static lcpc_status comm_common(lcpc_comm *c) {
     g_prio_override.store(3);
   }
   HIP_TRY(hipSetDevice(c->dev->id));
-  if (shard_all_high()) {
-    int lo = 0, hi = 0;
-    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIP_TRY(hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, hi));
-  } else {
-    HIP_TRY(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
-  }
+  // the comm stream at the priority of the driver's other streams (one priority unless
+  // LCPC_PRIORITY_STREAMS=1 asks for the A/B split, Device::stream_priority)
+  HIP_TRY(hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, Device::stream_priority(shard_all_high())));
+  c->shared->cs = c->cs;
   return LCPC_OK;
 }
 

@@ -1,0 +1,23 @@
+"""The stream-ordered device pool (lcpc_proof_of_storage_amd/csrc/pool.hpp) on a simulated device
+(CPU, no HIP): a block's next owner is ordered after every use still queued on any stream that
+used it, under 200 random interleavings plus the directed cases (own stream: no wait; completed
+fence: free; host taker: host wait; events reused only after their record completed).
+tests/cpp/test_pool.cpp, built with ASan + UBSan."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_pool_ordering_on_simulated_streams(tmp_path):
+    exe = tmp_path / "test_pool"
+    src = os.path.join(ROOT, "tests", "cpp", "test_pool.cpp")
+    subprocess.run(["g++", "-std=c++20", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-Wall", "-o", str(exe), src], check=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "pool ordering: ok" in r.stdout
