@@ -219,10 +219,9 @@ def ntt_muls(n):
 
 def row1_active(n, file_image=False):
     """whether the one-pass Ft63 row kernel (csrc/ntt_row1.hpp) encodes these rate-1/2 2^n-point
-    rows: LCPC_NTT_ROW1 = 1..3 selects it, 0 the four-step pair; unset, the file-image commit
-    (lcpc_pos_commit_bytes_device) takes it and element rows the four-step pair (its row1_mode)"""
-    mode = os.environ.get("LCPC_NTT_ROW1", "1" if file_image else "0")[:1]
-    return n == 1 << 15 and mode in ("1", "2", "3")
+    rows: the library's AUTO row kernel takes it for the file-image commit
+    (lcpc_pos_commit_bytes_device) and the four-step pair for element rows"""
+    return n == 1 << 15 and file_image
 
 
 def pos_ntt_muls(n, file_image=False):
@@ -589,8 +588,7 @@ def pos_workload(args, L, torch, rank, local_rank):
                          f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
         algo_bytes=n_rows * np_ * 8 + n_rows * nc * 8,
         leaf_compressions=leaf_compressions(n_rows, nc, 8),
-        traffic_key=(n_el, "Ft63", "pos-row1" if row1_active(nc, fi) else
-                     "pos-a7" if fi and os.environ.get("LCPC_NTT_ROW1", "")[:1] == "4" else "pos"),
+        traffic_key=(n_el, "Ft63", "pos-row1" if row1_active(nc, fi) else "pos"),
         mul_count=n_rows * pos_ntt_muls(nc, fi)[0], mul_model=pos_ntt_muls(nc, fi)[1])
 
 

@@ -137,6 +137,15 @@ size_t lcpc_encoding_n_col_opens(const lcpc_encoding *e);
 size_t lcpc_encoding_n_degree_tests(const lcpc_encoding *e);
 size_t lcpc_encoding_n_per_row(const lcpc_encoding *e);
 size_t lcpc_encoding_n_cols(const lcpc_encoding *e);
+/* Which kernel encodes rows of 2^15-point Ft63 rate-1/2 encodings (the proof-of-storage default
+ * dims; no effect on any other encoding): AUTO (default) = the one-pass row kernel for file images
+ * (lcpc_pos_commit_bytes_device) and the four-step pair for element rows, the measured choices
+ * (DESIGN.md §4); FOURSTEP / ONEPASS force one kernel for both.  Results are identical either way.
+ * No reference counterpart (fffft has one FFT). */
+#define LCPC_ROW_KERNEL_AUTO 0
+#define LCPC_ROW_KERNEL_FOURSTEP 1
+#define LCPC_ROW_KERNEL_ONEPASS 2
+lcpc_status lcpc_encoding_set_row_kernel(lcpc_encoding *e, int kernel);
 /* Pre-allocates the calling thread's page-locked staging for lcpc_prove on commitments of
  * n_rows rows under e (host only).  Optional: a thread's first prove otherwise pays the
  * hipHostMalloc.  No reference counterpart (rayon threads have no device staging). */

@@ -78,6 +78,7 @@ SIGNATURES = {
     "lcpc_reserve": (i32, [vp, sz, sz]),
     "lcpc_encoding_n_per_row": (sz, [vp]),
     "lcpc_encoding_n_cols": (sz, [vp]),
+    "lcpc_encoding_set_row_kernel": (i32, [vp, i32]),
     "lcpc_encode": (i32, [vp, u64p, sz]),
     "lcpc_encode_rows": (i32, [vp, u64p, sz, sz]),
     "lcpc_encode_rows_device": (i32, [vp, vp, sz, sz, vp, sz, sz, vp]),

@@ -173,13 +173,8 @@ size_t mfma_splits_for(size_t n_rows, size_t n_per_row) {
   return splits < 1 ? 1 : splits;
 }
 
-// LCPC_COLLAPSE_VALU=1 selects the VALU kernels for every field (A/B measurements)
 bool use_mfma(int fid, int n_tensors) {
-  static const bool valu_only = [] {
-    const char *e = getenv("LCPC_COLLAPSE_VALU");
-    return e && *e && *e != '0';
-  }();
-  return !valu_only && fid == Ft127::ID && n_tensors >= 1 && n_tensors <= 3;
+  return !no_mfma() && fid == Ft127::ID && n_tensors >= 1 && n_tensors <= 3;
 }
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -216,21 +211,24 @@ __global__ __launch_bounds__(256) void k_copy_words(W *__restrict__ dst, const W
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
 }
-size_t copy_max_blocks() {  // LCPC_COPY_BLOCKS (A/B knob), default 64
-  static const size_t v = [] {
-    const char *e = getenv("LCPC_COPY_BLOCKS");
-    const long n = e ? atol(e) : 0;
-    return n > 0 ? (size_t)n : (size_t)64;
+constexpr size_t COPY_MAX_BLOCKS = 64;  // (measured: a full grid cost K = 256 0.5 G/s)
+
+}  // namespace
+
+// LCPC_NO_MFMA=1: the VALU kernels instead of the int8 matrix-core ones (row combinations, SDIG
+// levels) for A/B measurements; the results are identical
+bool no_mfma() {
+  static const bool v = [] {
+    const char *e = getenv("LCPC_NO_MFMA");
+    return e && *e && *e != '0';
   }();
   return v;
 }
 
-}  // namespace
-
 hipError_t copy_words(void *dst, const void *src, size_t bytes, hipStream_t s, bool over_link) {
   if (!bytes) return hipSuccess;
   // device-to-device copies are HBM-bound: a full grid; copies over the host link: a few groups
-  const size_t cap = over_link ? copy_max_blocks() : (size_t)1 << 20;
+  const size_t cap = over_link ? COPY_MAX_BLOCKS : (size_t)1 << 20;
   if (((uintptr_t)dst | (uintptr_t)src | bytes) & 7) return hipErrorInvalidValue;
   if (!(((uintptr_t)dst | (uintptr_t)src | bytes) & 15)) {
     const size_t n = bytes / 16;

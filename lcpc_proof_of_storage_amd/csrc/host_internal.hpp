@@ -160,28 +160,6 @@ struct Device {
     if (!priority_streams() || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return 0;
     return high ? hi : lo;
   }
-  // Commitments in FIFO order (LCPC_COMMIT_FIFO=1; off by default): every commit enqueues its
-  // whole kernel sequence on this one stream under commit_mu, so concurrent commits run back to
-  // back at the full GPU, first come first finished, instead of side by side on streams of their
-  // own.  Same-box A/B (profiles/r03_commit_fifo_ab.json): cfg3 K = 20 12.2 either way (the
-  // commits then complete every 1.15 ms and the last proof's 4.1 ms is the tail), K = 256
-  // 15.6 against 16.3, cfg5 29.2 against 27.8, cfg4 5.5 against 6.6: not the default.
-  std::mutex commit_mu;
-  hipStream_t commit_s = nullptr;
-  static bool fifo_commits() {
-    static const bool v = [] {
-      const char *e = getenv("LCPC_COMMIT_FIFO");
-      return e && e[0] == '1' && !serial_mode();
-    }();
-    return v;
-  }
-  hipStream_t commit_stream() {  // (under commit_mu)
-    if (!commit_s) {
-      (void)hipSetDevice(id);
-      if (hipStreamCreateWithFlags(&commit_s, hipStreamNonBlocking) != hipSuccess) commit_s = nullptr;
-    }
-    return commit_s;
-  }
   void release_stream(hipStream_t s, bool high) {
     if (serial_mode()) return;
     std::lock_guard<std::mutex> lk(mu);

@@ -18,6 +18,9 @@ bool field_gpu_supported(int fid);
 //   pass A: 2^l1-point DIF down each of the 2^l2 columns of the row viewed as [2^l1][2^l2],
 //           input zero-padded past n_valid, then the inter-pass twiddle w^(c * bitrev(t'));
 //   pass B: 2^l2-point DIF along each contiguous block.
+// LCPC_NO_MFMA=1: VALU kernels instead of the int8 matrix-core ones (A/B runs; identical results)
+bool no_mfma();
+
 struct NttPlan {
   int fid = -1;
   int log_n = 0, l1 = 0, l2 = 0;
@@ -28,6 +31,10 @@ struct NttPlan {
   // the flat table they were c * bitrev(t) apart, one cache line per lane); log_n > 12 only
   uint32_t *d_tw2 = nullptr;
   uint32_t *d_tw2_canon = nullptr;  // forward plans: canonical words
+  // which kernel encodes the PoS-dims rows (2^15-point Ft63, rate 1/2): LCPC_ROW_KERNEL_AUTO (the
+  // measured choice: the one-pass kernel for file images, the four-step pair for element rows),
+  // _FOURSTEP or _ONEPASS (lcpc_encoding_set_row_kernel)
+  int row_kernel = 0;
 };
 // the [t][c] table above for a pass-A split l1 from a flat table tw (n = 2^log_n elements)
 hipError_t ntt_tw2_table(int fid, const uint32_t *tw, int log_n, int l1, uint32_t *out, hipStream_t s);
@@ -52,7 +59,7 @@ hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, si
 // element (zero padded); canonical output, the coefficient matrix written to copy.  Only at the
 // one-pass kernel's shape (ntt_rows_pos_bytes_ok), 16-byte-aligned bytes.
 bool ntt_rows_pos_bytes_ok(const NttPlan &p, size_t n_per_row);
-bool ntt_row1_bytes();  // whether the file-image commit takes the one-pass kernel (LCPC_NTT_ROW1)
+bool ntt_row1_bytes(const NttPlan &p);  // whether the file-image commit takes the one-pass kernel (p.row_kernel)
 hipError_t ntt_rows_pos_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst,
                               size_t dst_stride, size_t n_rows, hipStream_t s, uint32_t *copy, size_t copy_stride);
 

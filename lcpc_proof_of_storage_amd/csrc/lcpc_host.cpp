@@ -102,25 +102,12 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   hipStream_t s = lease.s;
-  // FIFO commits: the whole sequence below goes on the device's commit stream while commit_mu is
-  // held (buffers allocated meanwhile record that stream), then this call waits for its own
-  // completion event only
-  std::unique_lock<std::mutex> fifo;
-  hipEvent_t done = nullptr;
-  if (Device::fifo_commits()) {
-    fifo = std::unique_lock<std::mutex>(dev->commit_mu);
-    if (hipStream_t cs = dev->commit_stream()) {
-      s = cs;
-      t_stream = cs;  // (restored by ~Lease)
-      done = t_event(dev->id);
-    }
-  }
   const int fid = e->fid, wb = field_bytes(fid);
   DBuf packed;  // bytes off the fused path: the element image (at function scope: no block-exit drain)
   const uint8_t *src_b = nullptr;
   if (src_bytes) {
     if (fid != LCPC_FT63 || src_is_host) return fail(LCPC_ERR_INVALID_ARG, "file image: device WriteableFt63 only");
-    if (e->kind != KIND_SDIG && ntt_row1_bytes() && ntt_rows_pos_bytes_ok(e->plan, np) && !((uintptr_t)d_src & 15)) {
+    if (e->kind != KIND_SDIG && ntt_row1_bytes(e->plan) && ntt_rows_pos_bytes_ok(e->plan, np) && !((uintptr_t)d_src & 15)) {
       src_b = (const uint8_t *)d_src;
     } else {
       HIP_TRY(packed.alloc(dev, len * 8));
@@ -204,17 +191,11 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   uint8_t *h_root = (uint8_t *)t_pin[PIN_OUTER].get(32);
   if (!h_root) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
   HIP_TRY(d2h(h_root, c->hashes.as<uint8_t>() + (c->n_hashes - 1) * 32, 32, s));
-  if (done) {
-    HIP_TRY(hipEventRecord(done, s));
-    fifo.unlock();
-    HIP_TRY(hipEventSynchronize(done));
-    // this commit's work is complete: its scratch needs no drain of the shared stream
-    tmp.settle();
-    scratch.settle();
-    packed.settle();
-  } else {
-    HIP_TRY(hipStreamSynchronize(s));
-  }
+  HIP_TRY(hipStreamSynchronize(s));
+  // this commit's work is complete: its scratch needs no fence
+  tmp.settle();
+  scratch.settle();
+  packed.settle();
   std::memcpy(c->root, h_root, 32);
   c->coeffs.settle();
   c->comm.settle();
@@ -388,6 +369,12 @@ size_t lcpc_encoding_n_col_opens(const lcpc_encoding *e) { return e->n_col_opens
 size_t lcpc_encoding_n_degree_tests(const lcpc_encoding *e) { return e->n_degree_tests; }
 size_t lcpc_encoding_n_per_row(const lcpc_encoding *e) { return e->n_per_row; }
 size_t lcpc_encoding_n_cols(const lcpc_encoding *e) { return e->n_cols; }
+lcpc_status lcpc_encoding_set_row_kernel(lcpc_encoding *e, int kernel) {
+  if (!e || kernel < LCPC_ROW_KERNEL_AUTO || kernel > LCPC_ROW_KERNEL_ONEPASS)
+    return fail(LCPC_ERR_INVALID_ARG, "row kernel");
+  e->plan.row_kernel = kernel;
+  return LCPC_OK;
+}
 
 lcpc_status lcpc_reserve(const lcpc_encoding *e, size_t len, size_t count) {
   if (!e || !len) return fail(LCPC_ERR_INVALID_ARG, "reserve arguments");

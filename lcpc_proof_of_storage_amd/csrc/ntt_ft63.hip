@@ -6,7 +6,7 @@ hipError_t ntt_rows_ft63(const NttPlan &p, const uint32_t *src, size_t ss, size_
                       size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
   return ntt_detail::ntt_rows_t<Ft63>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, canon);
 }
-bool ntt_row1_bytes() { return ntt_row1::row1_mode(ntt_row1::ROW1_BYTES_DEFAULT) != 0; }
+bool ntt_row1_bytes(const NttPlan &p) { return p.row_kernel != 1; }  // (LCPC_ROW_KERNEL_FOURSTEP: pack first)
 bool ntt_rows_pos_bytes_ok(const NttPlan &p, size_t n_per_row) {
   return p.fid == 0 && p.log_n == ntt_row1::LOG_N && n_per_row == ((size_t)1 << (ntt_row1::LOG_N - 1)) &&
          p.d_tw_canon;
@@ -16,8 +16,6 @@ hipError_t ntt_rows_pos_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_b
   if (!ntt_rows_pos_bytes_ok(p, (size_t)1 << (ntt_row1::LOG_N - 1)) || ((uintptr_t)bytes & 15) || !copy)
     return hipErrorInvalidValue;
   if (n_rows == 0) return hipSuccess;
-  if (ntt_row1::row1_mode(ntt_row1::ROW1_BYTES_DEFAULT) == 4)
-    return ntt_detail::ntt_rows_bytes_fourstep(p, bytes, n_bytes, dst, dst_stride, n_rows, s, copy, copy_stride);
   return ntt_row1::launch_bytes<Ft63>(p, bytes, n_bytes, dst, dst_stride, n_rows, s, copy, copy_stride);
 }
 hipError_t ntt_tw_table_ft63(uint32_t *tw, int log_n, bool inverse, hipStream_t s) {

@@ -164,10 +164,10 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
   constexpr int R = Shape<F>::R, E = Shape<F>::E;
   const bool halfz = 2 * nv <= ((size_t)1 << p.log_n);
   if constexpr (F::ID == 0) {
-    // PoS default dims: the one-pass row kernel (ntt_row1.hpp) when LCPC_NTT_ROW1 selects it
-    // (ROW1_DEFAULT otherwise; 0 = the four-step pair)
-    const int r1 = ntt_row1::row1_mode(ntt_row1::ROW1_DEFAULT);
-    if (p.log_n == ntt_row1::LOG_N && halfz && r1 >= 1 && r1 <= 3)
+    // PoS default dims: element rows take the four-step pair (2.57 ms per 1 GiB request against
+    // 2.97 for the one-pass kernel on elements) unless the encoding asks for the
+    // one-pass row kernel (ntt_row1.hpp; LCPC_ROW_KERNEL_ONEPASS)
+    if (p.log_n == ntt_row1::LOG_N && halfz && p.row_kernel == 2)
       return ntt_row1::launch<F>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, canon);
   }
   constexpr int HI = F::N >= 8 ? 11 : 12;  // LDS budget of 32-byte fields
@@ -200,18 +200,6 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
     constexpr int T = L + CW - R;
     return ntt_v2::launch_b<F, L, CW, T>(dst, ds, p.d_tw, p.log_n, n_rows, s);
   });
-}
-
-// the file image through the four-step pair, unpacked by pass A (LCPC_NTT_ROW1=4): the PoS dims'
-// shapes of ntt_rows_t (pass A 256-point columns x 32 in 1024 threads, pass B 128-point blocks)
-inline hipError_t ntt_rows_bytes_fourstep(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst,
-                                          size_t ds, size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
-  if (p.fid != 0 || p.log_n != 15 || p.l1 != 8 || !p.d_tw2_canon) return hipErrorInvalidValue;
-  hipError_t e = ntt_v2::launch_a<Ft63, 8, 5, 10, true, true, true>(reinterpret_cast<const uint32_t *>(bytes), 0,
-                                                                    n_bytes, dst, ds, p.d_tw, p.log_n, n_rows, s, cp,
-                                                                    cs, p.d_tw2_canon);
-  if (e != hipSuccess) return e;
-  return ntt_v2::launch_b<Ft63, 7, 5, 9>(dst, ds, p.d_tw, p.log_n, n_rows, s);
 }
 
 }  // namespace ntt_detail

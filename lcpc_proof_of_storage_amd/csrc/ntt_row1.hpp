@@ -33,10 +33,11 @@ namespace lcpc {
 namespace ntt_row1 {
 
 constexpr int LOG_N = 15;
-// LCPC_NTT_ROW1 unset (row1_mode below): element rows take the four-step pair (2.57 ms per 1 GiB
-// request against 2.75-2.97 for this kernel), the file-image commit this kernel one workgroup per
-// row (2.75 ms against 2.93 for k_pack7 + the four-step pair)
-constexpr int ROW1_DEFAULT = 0, ROW1_BYTES_DEFAULT = 1;
+// Which rows take this kernel (NttPlan::row_kernel, LCPC_ROW_KERNEL_AUTO): the file-image commit
+// (2.75 ms per 1 GiB request against 2.93 for k_pack7 + the four-step pair); element rows keep the
+// four-step pair (2.57 against 2.97 ms) unless the encoding asks for this one.  The
+// round-4 variants that measured slower -- persistent workgroups with an LDS-DMA prefetch, outputs
+// stored from registers, the four-step pair unpacking in pass A -- are no longer built.
 
 // element (hi, mid, lo & 15) of the half lo >> 4 (exchange 1); the XOR spreads a ds_read's lanes
 // (16 values of hi) over 16 bank pairs
@@ -101,58 +102,27 @@ __device__ __forceinline__ void lo_stage(Fe<F> *x, const uint2 *wtab) {
 // limb, zero-padded), row r = elements [16384 r, 16384 (r + 1)); the row's 112 KiB are staged in
 // the exchange buffer with coalesced 16-byte loads and each thread unpacks its 16 elements from
 // there -- k_pack7 fused into the encode (no element image written and read back).
-// PERSIST: one workgroup per CU walks rows blockIdx.x, + gridDim.x, ...; the next row's input goes
-// into the exchange buffer by LDS-DMA (global_load_lds_dwordx4) while round 3 computes, and the
-// outputs are stored straight from registers (16-byte stores, a lane's 32 outputs contiguous), so
-// the buffer is free for the prefetch -- a row's HBM load no longer waits between two rows.
 constexpr int ROW_BYTES = 7 << 14;  // one row of the file image
 
-__device__ __forceinline__ void glds16(const void *g, void *l) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
-                                   (__attribute__((address_space(3))) void *)l, 16, 0, 0);
-}
-
-// a whole row's input into xbuf by LDS-DMA (PERSIST rows are whole: every 16-byte piece in bounds)
-template <bool BYTES>
-__device__ __forceinline__ void stage_row(const uint32_t *src, size_t src_stride, size_t row, uint2 *xbuf, int tid) {
-  uint4 *sb = reinterpret_cast<uint4 *>(xbuf) + (tid & ~63);
-  const uint4 *g = BYTES ? reinterpret_cast<const uint4 *>(reinterpret_cast<const uint8_t *>(src) + row * (size_t)ROW_BYTES)
-                         : reinterpret_cast<const uint4 *>(src + row * src_stride * 2);
-  g += tid;
-  constexpr int PIECES = BYTES ? ROW_BYTES / 16 / 1024 : 8;
-#pragma unroll
-  for (int i = 0; i < PIECES; i++) glds16(g + i * 1024, sb + i * 1024);
-}
-
-template <class F, bool CANON, bool COPY, bool BYTES, bool PERSIST, bool DIRECT = PERSIST>
+template <class F, bool CANON, bool COPY, bool BYTES>
 __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__ src, size_t src_stride,
                                                     size_t n_valid, uint32_t *__restrict__ dst, size_t dst_stride,
                                                     const uint32_t *__restrict__ tw,
                                                     const uint32_t *__restrict__ tw0,
-                                                    uint32_t *__restrict__ copy, size_t copy_stride, size_t n_rows,
-                                                    size_t row_base) {
+                                                    uint32_t *__restrict__ copy, size_t copy_stride) {
   static_assert(F::N == 2, "8-byte fields");
   __shared__ __align__(16) uint2 xbuf[16384];  // half a row
   __shared__ uint2 wtab[512];                   // w^(32 k)
   const int tid = threadIdx.x;
-  size_t row = row_base + blockIdx.x;
+  const size_t row = blockIdx.x;
   if (tid < 512) wtab[tid] = reinterpret_cast<const uint2 *>(tw)[32 * tid];
-  if constexpr (PERSIST) {
-    stage_row<BYTES>(src, src_stride, row, xbuf, tid);
-    __builtin_amdgcn_s_waitcnt(0);
-  }
   Fe<F> x[32];
-  for (;;) {
-    // (PERSIST: tid through an opaque zero, so that the row-independent twiddle loads and LDS
-    // addresses are recomputed per row, not hoisted out of the loop into ~100 live registers)
-    int z = 0;
-    if constexpr (PERSIST) asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-    const int tid = threadIdx.x + z;
+  {
     // ---- round 1: thread (mid, lo), lo's top bit at thread-id bit 9
     {
       const int lo = ((tid >> 9) << 4) | (tid & 15), mid = (tid >> 4) & 31;
       const int tl = (mid << 5) | lo;
-      if constexpr (BYTES && !PERSIST) {
+      if constexpr (BYTES) {
         const size_t row0 = row * (size_t)ROW_BYTES;
         const uint8_t *rb = reinterpret_cast<const uint8_t *>(src) + row0;
         uint4 *sb = reinterpret_cast<uint4 *>(xbuf);
@@ -168,7 +138,7 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
           }
         }
       }
-      if constexpr (BYTES || PERSIST) __syncthreads();  // the staged row (every wave's part) is in
+      if constexpr (BYTES) __syncthreads();  // the staged row (every wave's part) is in
       const uint32_t *in = src + row * src_stride * 2;
 #pragma unroll
       for (int h = 0; h < 16; h++) {
@@ -181,9 +151,6 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
           a.v[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
           a.v[1] = __builtin_amdgcn_alignbyte(d2, d1, sh) & 0xffffffu;
           if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
-        } else if constexpr (PERSIST) {
-          a = lds_ld<F>(xbuf, pos);  // (whole rows: n_valid = 16384)
-          if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
         } else if ((size_t)pos < n_valid) {
           a = fe_load<F>(in, pos);
           if constexpr (COPY) fe_store<F>(copy + row * copy_stride * 2, pos, a);
@@ -195,7 +162,7 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
         else
           x[h] = a;
       }
-      if constexpr (BYTES || PERSIST) __syncthreads();  // every input read before exchange 1 reuses xbuf
+      if constexpr (BYTES) __syncthreads();  // every input read before exchange 1 reuses xbuf
       reg_stage<F, 8>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 1); });
       reg_stage<F, 4>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 2); });
       reg_stage<F, 2>(x, [&](int jm) { return fe_load<F>(tw, ((jm << 10) | tl) << 3); });
@@ -244,29 +211,12 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
     }
     // ---- round 3: thread (hi, mid) holds lo = 0..31; twiddles w^(jm << s) = wtab[jm << (s - 5)]
     const int mid = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
-    const size_t next = row + gridDim.x;
-    if constexpr (PERSIST) {
-      if (next < n_rows) stage_row<BYTES>(src, src_stride, next, xbuf, tid);
-      asm volatile("" ::: "memory");  // issue the prefetch here, before round 3 (not sunk past it)
-    }
     lo_stage<F, 10>(x, wtab);
     lo_stage<F, 11>(x, wtab);
     lo_stage<F, 12>(x, wtab);
     lo_stage<F, 13>(x, wtab);
     lo_stage<F, 14>(x, wtab);
-    if constexpr (DIRECT) {
-      // the prefetch has landed (every wave's part: the barrier at the next row's top)
-      if constexpr (PERSIST) __builtin_amdgcn_s_waitcnt(0);
-      uint4 *out = reinterpret_cast<uint4 *>(dst + row * dst_stride * 2) + (((hi << 10) | (mid << 5)) >> 1);
-#pragma unroll
-      for (int lp = 0; lp < 16; lp++) {
-        const Fe<F> a = fe_reduce_2p<F>(x[2 * lp]), b = fe_reduce_2p<F>(x[2 * lp + 1]);
-        out[lp] = make_uint4(a.v[0], a.v[1], b.v[0], b.v[1]);
-      }
-      if constexpr (!PERSIST) break;
-      row = next;
-      if (row >= n_rows) break;
-    } else {
+    {
       // ---- out: through LDS in halves (hi >> 4), 16-byte units u = ((hi & 15) << 9) | (mid << 4) | (lo >> 1)
       //      stored at u ^ (hi & 7): a ds_write's 64 lanes land on 8 distinct 16-byte bank slots
       uint4 *ubuf = reinterpret_cast<uint4 *>(xbuf);
@@ -290,71 +240,36 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
       store_half(0);
       __syncthreads();
       store_half(1);
-      break;
     }
   }
 }
 
-// LCPC_NTT_ROW1: 0 = the four-step pair (after k_pack7 for a file image), 1 = one workgroup per
-// row, 2 = persistent workgroups with the next row prefetched, 3 = as 1 with the outputs stored
-// straight from registers, 4 = (file images) the four-step pair with the unpack in pass A;
-// unset = dflt (ntt_rows: 0, the file-image commit: 1 -- the measured choices)
-inline int row1_mode(int dflt) {
-  const char *r1 = std::getenv("LCPC_NTT_ROW1");
-  return r1 && r1[0] >= '0' && r1[0] <= '4' ? r1[0] - '0' : dflt;
-}
-
-inline unsigned persist_grid(size_t n_rows) {
-  static int n_cu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  return (unsigned)(n_rows < (size_t)n_cu ? n_rows : (size_t)n_cu);
-}
-
 template <class F, bool CANON, bool COPY, bool BYTES>
 hipError_t launch_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
-                    size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, size_t n_persist, bool direct) {
-  // rows [0, n_persist): persistent workgroups (whole rows); the rest one workgroup per row
+                    size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
   const uint32_t *tw0 = CANON ? p.d_tw_canon : p.d_tw;
   prof::Scope ps("ntt_row1", s);
-  if (n_persist)
-    hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, true>), dim3(persist_grid(n_persist)), dim3(1024), 0, s,
-                       src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs, n_persist, (size_t)0);
-  if (n_rows > n_persist && direct)
-    hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, false, true>), dim3((unsigned)(n_rows - n_persist)),
-                       dim3(1024), 0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs, n_rows, n_persist);
-  else if (n_rows > n_persist)
-    hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, false>), dim3((unsigned)(n_rows - n_persist)), dim3(1024),
-                       0, s, src, ss, nv, dst, ds, p.d_tw, tw0, cp, cs, n_rows, n_persist);
+  hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES>), dim3((unsigned)n_rows), dim3(1024), 0, s, src, ss, nv, dst,
+                     ds, p.d_tw, tw0, cp, cs);
   return hipGetLastError();
 }
 
 template <class F>
 hipError_t launch(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                   size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs, bool canon) {
-  // the LDS-DMA prefetch moves whole rows of 16-byte pieces
-  const int mode = row1_mode(ROW1_DEFAULT);
-  const bool persist = mode == 2 && !((uintptr_t)src & 15) && !(ss & 1) && nv == ((size_t)1 << (LOG_N - 1));
-  const size_t np = persist ? n_rows : 0;
-  const bool dr = mode == 3;
-  if (canon && cp) return launch_t<F, true, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np, dr);
-  if (canon) return launch_t<F, true, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np, dr);
-  if (cp) return launch_t<F, false, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np, dr);
-  return launch_t<F, false, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, np, dr);
+  if (canon && cp) return launch_t<F, true, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs);
+  if (canon) return launch_t<F, true, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs);
+  if (cp) return launch_t<F, false, true, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs);
+  return launch_t<F, false, false, false>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs);
 }
 
 // the proof-of-storage commit from the file image (BYTES above): canonical output, coefficient copy;
-// the file's ragged last row (if any) one workgroup of its own
+// the file's ragged last row (if any) is zero padded as it is staged
 template <class F>
 hipError_t launch_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst, size_t ds,
                         size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
-  const size_t whole = n_bytes / ROW_BYTES < n_rows ? n_bytes / ROW_BYTES : n_rows;
-  const int mode = row1_mode(ROW1_BYTES_DEFAULT);
-  return launch_t<F, true, true, true>(p, reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds, n_rows,
-                                       s, cp, cs, mode == 2 ? whole : 0, mode == 3);
+  return launch_t<F, true, true, true>(p, reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds, n_rows, s,
+                                       cp, cs);
 }
 
 }  // namespace ntt_row1

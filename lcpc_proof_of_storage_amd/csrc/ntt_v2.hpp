@@ -120,29 +120,7 @@ constexpr int last_s0() {  // first stage of the last round
 // form (see ntt_rows' canon_out).  tw2: the inter-pass twiddles w^(c bitrev(t)) laid out [t][c]
 // (NttPlan::d_tw2 / d_tw2_canon), so the lanes of a store (adjacent columns c) load adjacent
 // twiddles.
-// BYTES (Ft63, HALFZ): src is a proof-of-storage file image of n_valid bytes, row r's element i
-// at byte 7 (r n / 2 + i), 7 little-endian bytes per element (DataField::from_byte_vec,
-// fields/data_field.rs:38-46; zero padded past the image) -- unpacked as it is loaded.
-template <int LOG_N>
-__device__ __forceinline__ Fe<Ft63> load7(const uint8_t *__restrict__ img, size_t n_bytes, size_t row, size_t pos) {
-  const size_t b = row * (size_t)(7u << (LOG_N - 1)) + 7 * pos;
-  Fe<Ft63> a;
-  if ((b & ~(size_t)3) + 12 <= n_bytes) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(img + (b & ~(size_t)3));
-    const uint32_t sh = (uint32_t)(b & 3), d0 = w[0], d1 = w[1], d2 = w[2];
-    a.v[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    a.v[1] = __builtin_amdgcn_alignbyte(d2, d1, sh) & 0xffffffu;
-  } else {  // the image's last bytes
-    uint64_t v = 0;
-    for (int k = 0; k < 7; k++)
-      if (b + k < n_bytes) v |= (uint64_t)img[b + k] << (8 * k);
-    a.v[0] = (uint32_t)v;
-    a.v[1] = (uint32_t)(v >> 32);
-  }
-  return a;
-}
-
-template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ, bool CANON, bool BYTES = false>
+template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ, bool CANON>
 __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restrict__ src,
                                                        size_t src_stride, size_t n_valid,
                                                        uint32_t *__restrict__ dst,
@@ -182,11 +160,7 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_a(const uint32_t *__restric
         x[j] = fe_zero<F>();
       } else {
         const size_t pos = c + ((size_t)(q + j * GL) << log_m);
-        if constexpr (BYTES) {
-          static_assert(HALFZ && F::ID == 0, "file images: Ft63 rate-1/2 rows");
-          x[j] = load7<15>(reinterpret_cast<const uint8_t *>(src), n_valid, row, pos);
-          if (cp) fe_store<F>(cp, pos, x[j]);
-        } else if (pos < n_valid) {
+        if (pos < n_valid) {
           x[j] = fe_load<F>(in, pos);
           if (cp) fe_store<F>(cp, pos, x[j]);  // coalesced: lanes = adjacent columns
         } else {
@@ -280,13 +254,13 @@ __global__ __launch_bounds__(1 << LOG_T) void k_pass_b(uint32_t *__restrict__ da
   }
 }
 
-template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ, bool CANON = false, bool BYTES = false>
+template <class F, int LOG_S, int LOG_CW, int LOG_T, bool HALFZ, bool CANON = false>
 hipError_t launch_a(const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                     const uint32_t *tw, int log_n, size_t n_rows, hipStream_t s, uint32_t *cp,
                     size_t cs, const uint32_t *tw2) {
   const size_t groups = (size_t)1 << (log_n - LOG_S - LOG_CW);
   prof::Scope ps("ntt_pass_a", s);
-  hipLaunchKernelGGL((k_pass_a<F, LOG_S, LOG_CW, LOG_T, HALFZ, CANON, BYTES>), dim3((unsigned)(n_rows * groups)),
+  hipLaunchKernelGGL((k_pass_a<F, LOG_S, LOG_CW, LOG_T, HALFZ, CANON>), dim3((unsigned)(n_rows * groups)),
                      dim3(1 << LOG_T), 0, s, src, ss, nv, dst, ds, tw, tw2, log_n, cp, cs);
   return hipGetLastError();
 }

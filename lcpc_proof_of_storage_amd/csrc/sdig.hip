@@ -245,19 +245,12 @@ __global__ __launch_bounds__(256) void k_transpose(const uint32_t *__restrict__ 
   }
 }
 
-// rows per wave of k_spmm_mfma: chunks of at most LCPC_SDIG_TILES (default 8, at most 10) tiles of
-// 16 rows, as few tiles as cover R.  More tiles per wave amortise a 4-nonzero group's A-fragment
-// work over more rows (two commitments' 144 rows in one wave with 9) at the cost of registers.
-inline int mfma_max_tiles() {
-  static const int v = [] {
-    const char *e = std::getenv("LCPC_SDIG_TILES");
-    const int t = e ? std::atoi(e) : 8;
-    return t < 1 ? 8 : (t > 10 ? 10 : t);
-  }();
-  return v;
-}
+// rows per wave of k_spmm_mfma: chunks of at most 8 tiles of 16 rows, as few tiles as cover R
+// (9 or 10 tiles per wave -- two commitments' 144 rows in one wave -- measured slower in round 4:
+// 13.9-14.1 against 16.1 G/s; no longer built)
+constexpr int MFMA_MAX_TILES = 8;
 inline void mfma_tiling(size_t R, int &tiles, unsigned &chunks) {
-  const size_t per = 16 * (size_t)mfma_max_tiles();
+  const size_t per = 16 * (size_t)MFMA_MAX_TILES;
   chunks = (unsigned)((R + per - 1) / per);
   tiles = (int)((R + 16 * chunks - 1) / (16 * chunks));
 }
@@ -288,9 +281,7 @@ hipError_t spmm(const SdigPlan &p, const CsrDev &M, const uint32_t *x, uint32_t 
         case 5: launch_spmm_mfma<F, 5>(M, x, y, R, b0, nb, chunks, s); break;
         case 6: launch_spmm_mfma<F, 6>(M, x, y, R, b0, nb, chunks, s); break;
         case 7: launch_spmm_mfma<F, 7>(M, x, y, R, b0, nb, chunks, s); break;
-        case 8: launch_spmm_mfma<F, 8>(M, x, y, R, b0, nb, chunks, s); break;
-        case 9: launch_spmm_mfma<F, 9>(M, x, y, R, b0, nb, chunks, s); break;
-        default: launch_spmm_mfma<F, 10>(M, x, y, R, b0, nb, chunks, s); break;
+        default: launch_spmm_mfma<F, 8>(M, x, y, R, b0, nb, chunks, s); break;
       }
       return hipGetLastError();
     }
@@ -298,17 +289,6 @@ hipError_t spmm(const SdigPlan &p, const CsrDev &M, const uint32_t *x, uint32_t 
   hipLaunchKernelGGL((k_spmm<F>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M.ptr, M.idx,
                      M.val, x, y, M.rows, (uint32_t)R, (uint32_t)b0, (uint32_t)nb);
   return hipGetLastError();
-}
-
-// Rows per pass of the level chain (LCPC_SDIG_ROWS; 0 = all).  Rows are independent, so the
-// whole chain can run on a slice of the rows at a time: a smaller slice keeps each level's
-// input resident in the 256 MB infinity cache across its d re-reads (A/B runs).
-inline size_t sdig_rows_per_pass() {
-  static const size_t v = [] {
-    const char *e = std::getenv("LCPC_SDIG_ROWS");
-    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)0;
-  }();
-  return v;
 }
 
 template <class F>
@@ -350,13 +330,10 @@ hipError_t encode_rows_slice(const SdigPlan &p, uint32_t *cw, size_t R, size_t b
 
 template <class F>
 hipError_t encode_cm(const SdigPlan &p, uint32_t *cw, size_t R, uint32_t *tmp, hipStream_t s) {
+  // (the whole chain over all R rows: running it on row slices so that a level's input stays in
+  // the infinity cache measured slower, 1.14-2.0 against 0.85 ms)
   prof::Scope ps("sdig_encode", s);
-  const size_t step = sdig_rows_per_pass() ? std::min(sdig_rows_per_pass(), R) : R;
-  for (size_t b0 = 0; b0 < R; b0 += step) {
-    const hipError_t e = encode_rows_slice<F>(p, cw, R, b0, std::min(step, R - b0), tmp, s);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
+  return encode_rows_slice<F>(p, cw, R, 0, R, tmp, s);
 }
 
 }  // namespace
@@ -411,13 +388,12 @@ hipError_t sdig_plan_upload(SdigPlan &plan, int fid, const std::vector<CsrHost> 
   return hipStreamSynchronize(s);  // host vectors may be freed after return
 }
 
-// The matrix-core forms of every level (Ft127; LCPC_SDIG_VALU=1 keeps the VALU kernel for A/B
+// The matrix-core forms of every level (Ft127; LCPC_NO_MFMA=1 keeps the VALU kernel for A/B
 // runs).  Every output needs at most 4 SPMM_MAX_GROUPS nonzeros (the int32 accumulator bound).
 hipError_t sdig_plan_mfma(SdigPlan &plan, const std::vector<CsrHost> &pre, const std::vector<CsrHost> &post,
                           hipStream_t s) {
   plan.mfma = false;
-  const char *env = std::getenv("LCPC_SDIG_VALU");
-  if (plan.fid != Ft127::ID || (env && env[0] == '1')) return hipSuccess;
+  if (plan.fid != Ft127::ID || no_mfma()) return hipSuccess;
   std::vector<const CsrHost *> hs;
   std::vector<CsrDev *> ds;
   for (size_t i = 0; i < pre.size(); i++) hs.push_back(&pre[i]), ds.push_back(&plan.pre[i]);

@@ -447,47 +447,22 @@ namespace {
 
 // Each polynomial's exchange-side and prove kernels run on a stream of their own beside the
 // shared in-order encode stream and the comm stream, ordered against them by cross-stream event
-// waits alone.  All three are at ONE priority.  With high-priority prove streams over
-// normal-priority encode / comm streams (LCPC_SHARD_PRIO=2, kept for A/B runs only) eight ranks
-// sharing one GPU produced a wrong commitment root for one of the later polynomials in about one
-// run in four (tests/test_gpu_shard_native.py::test_native_pipeline_world8_rccl_one_gpu: every
-// rank's subtrees of that polynomial wrong, its recommitment on one GPU right); at one priority
-// it never did (0 in 28 runs, profiles/r03_world8_priority_race.json).  The cause under mixed
-// priorities was not isolated further.  Modes (LCPC_SHARD_PRIO), with the sharded engine's
-// one-rank K = 20 rate on one box: 3 (default) every stream of the driver high priority, 10.1-10.3
-// G/s; 1 every stream normal priority, 8.5-9.0; 0 the prove work on the encode stream, 9.5-10.2;
-// 2 the old mixed priorities, 10.1-11.1 (unsafe).
-std::atomic<int> g_prio_override{-1};  // set once a multi-rank communicator rejects mode 2
-int shard_prove_stream_mode() {
-  static const int v = [] {
-    const char *e = getenv("LCPC_SHARD_PRIO");
-    return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 3;
-  }();
-  const int o = g_prio_override.load(std::memory_order_relaxed);
-  return o >= 0 ? o : v;
-}
-// mode 2 across ranks only for A/B runs that ask for it (LCPC_SHARD_PRIO_AB=1): otherwise a
-// multi-rank communicator falls back to mode 3 with a warning (check_shardable)
-bool shard_mode2_allowed(int nranks) {
-  if (shard_prove_stream_mode() != 2 || nranks <= 1) return true;
-  const char *e = getenv("LCPC_SHARD_PRIO_AB");
-  return e && e[0] == '1';
-}
-bool shard_prio_streams() { return shard_prove_stream_mode() != 0; }
-// encode streams of the pipelined driver, taken in turn by polynomial (LCPC_SHARD_BULK_STREAMS=1
-// or 2, default 2): with two, consecutive polynomials' encode kernels overlap each other's tails
-// (one-rank K = 20: 11.1 / 11.5 against 11.0 / 11.3 G/s with one, interleaved runs,
-// profiles/r04_sharded_bulk_streams_ab.json) while the roots still arrive nearly in order
-size_t shard_bulk_streams() {
-  static const size_t n = [] {
-    const char *v = getenv("LCPC_SHARD_BULK_STREAMS");
-    return v && v[0] == '1' ? (size_t)1 : (size_t)2;
-  }();
-  return n;
-}
-// (3: every stream of the driver -- encode, exchange, prove -- at high priority)
-bool shard_all_high() { return shard_prove_stream_mode() == 3; }
-bool shard_prove_high() { return shard_prove_stream_mode() >= 2; }
+// waits alone.  All three are at ONE priority (the device's, Device::stream_priority).  With
+// high-priority prove streams over normal-priority encode / comm streams (round 3's mode 2) eight
+// ranks sharing one GPU produced a wrong commitment root for one of the later polynomials in about
+// one run in four (tests/test_gpu_shard_native.py::test_native_pipeline_world8_rccl_one_gpu); at
+// one priority it never did.  Round 5 removed the mixed mode.
+bool shard_prio_streams() { return true; }
+// encode streams of the pipelined driver, taken in turn by polynomial: with two, consecutive
+// polynomials' encode kernels overlap each other's tails (one-rank K = 20: 11.1 / 11.5 against
+// 11.0 / 11.3 G/s with one, interleaved runs, profiles/r04_sharded_bulk_streams_ab.json) while the
+// roots still arrive nearly in order
+constexpr size_t SHARD_BULK_STREAMS = 2;
+size_t shard_bulk_streams() { return SHARD_BULK_STREAMS; }
+// the pool a stream comes from (Device::acquire_stream): the prover's pool, whose priority equals
+// the bulk pool's unless LCPC_PRIORITY_STREAMS=1, for every stream of the driver
+bool shard_all_high() { return true; }
+bool shard_prove_high() { return true; }
 
 struct ShardDeleter {
   void operator()(lcpc_sharded_commit *c) const {
@@ -1292,12 +1267,6 @@ static lcpc_status comm_common(lcpc_comm *c) {
   lcpc_status st;
   c->dev = current_device(&st);
   if (!c->dev) return st;
-  if (!shard_mode2_allowed(c->nranks)) {
-    fprintf(stderr, "liblcpc_mi: LCPC_SHARD_PRIO=2 (mixed stream priorities) across %d ranks is an A/B mode "
-                    "(set LCPC_SHARD_PRIO_AB=1); using mode 3 (every stream of the driver at high priority)\n",
-            c->nranks);
-    g_prio_override.store(3);
-  }
   HIP_TRY(hipSetDevice(c->dev->id));
   // the comm stream at the priority of the driver's other streams (one priority unless
   // LCPC_PRIORITY_STREAMS=1 asks for the A/B split, Device::stream_priority)
@@ -1660,11 +1629,8 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   // polynomial k's encode is launched AHEAD ticks before its chaining-value exchange, so a tick's
   // exchange group (which waits for every producer in it) does not wait on a just-launched encode
   // and the encode stream stays fed while a tick waits on the host
-  static const size_t AHEAD = [] {  // (LCPC_SHARD_AHEAD: A/B runs)
-    const char *v = getenv("LCPC_SHARD_AHEAD");
-    const long n = v ? atol(v) : 0;
-    return n > 0 ? (size_t)n : (size_t)3;
-  }();
+  // (look-ahead 3: a sweep of 1-6 was within the run-to-run spread, profiles/r04_sharded_ahead_sweep.json)
+  constexpr size_t AHEAD = 3;
   for (size_t k = 0; k < std::min(AHEAD, n_polys); k++) start(k);
   hs_setup.reset();
   for (size_t t = 0; t < n_ticks; t++) {

@@ -232,6 +232,14 @@ class LcEncoding:
     def get_n_degree_tests(self) -> int:
         return N.load().lcpc_encoding_n_degree_tests(self._h)
 
+    ROW_KERNEL_AUTO, ROW_KERNEL_FOURSTEP, ROW_KERNEL_ONEPASS = 0, 1, 2
+
+    def set_row_kernel(self, kernel: int):
+        """lcpc_encoding_set_row_kernel: the kernel for 2^15-point Ft63 rate-1/2 rows (AUTO: one-pass
+        for file images, four-step for element rows; results identical)."""
+        _raise(N.load().lcpc_encoding_set_row_kernel(self._h, kernel))
+        return self
+
     def prepare_thread(self, n_rows: int):
         """Pre-allocate the calling thread's pinned staging for prove (lcpc_prepare_thread)."""
         _raise(N.load().lcpc_prepare_thread(self._h, n_rows))

@@ -1,29 +1,13 @@
 """GPU parity of the one-pass Ft63 row encode (csrc/ntt_row1.hpp) at the proof-of-storage
 default dims (2^15-point rows, rate 1/2: 16384 coefficients -> 32768), against the oracle's
 fft_io and commit (lcpc-ligero-pc/src/lib.rs:162-164, lcpc-2d/src/lib.rs:651-700), and against
-the four-step pair it replaces (LCPC_NTT_ROW1=0)."""
-import os
-
+the four-step pair (lcpc_encoding_set_row_kernel selects the kernel per encoding)."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-
-@pytest.fixture(autouse=True, params=["1", "2", "3", "4"],
-                ids=["per_row", "persistent", "per_row_direct", "fourstep_unpack"])
-def row1_on(request):
-    """the one-pass kernel (one workgroup per row, or persistent workgroups with the next row
-    prefetched) for every call of these tests unless four_step() says otherwise"""
-    old = os.environ.get("LCPC_NTT_ROW1")
-    os.environ["LCPC_NTT_ROW1"] = request.param
-    yield
-    if old is None:
-        del os.environ["LCPC_NTT_ROW1"]
-    else:
-        os.environ["LCPC_NTT_ROW1"] = old
-
-
+AUTO, FOURSTEP, ONEPASS = 0, 1, 2
 NP, NC = 16384, 32768
 
 
@@ -31,30 +15,16 @@ def rand_elems(oracle, n, seed):
     return oracle.ChaCha(seed_u64=seed).field_random(0, n)
 
 
-class four_step:
-    """LCPC_NTT_ROW1=0 for the duration (the library reads it at every launch)"""
-
-    def __enter__(self):
-        self.old = os.environ.get("LCPC_NTT_ROW1")
-        os.environ["LCPC_NTT_ROW1"] = "0"
-
-    def __exit__(self, *a):
-        if self.old is None:
-            del os.environ["LCPC_NTT_ROW1"]
-        else:
-            os.environ["LCPC_NTT_ROW1"] = self.old
-
-
 def test_row1_encode_rows_match_fffft(gpu, oracle):
-    """batched rows (Montgomery output, no coefficient copy) against fft_io row by row"""
-    enc = gpu.RsEncoding.new(0, NP, NC, 4, 1)
+    """batched rows (Montgomery output, no coefficient copy) against fft_io row by row, through
+    the one-pass kernel and the four-step pair"""
+    enc = gpu.RsEncoding.new(0, NP, NC, 4, 1).set_row_kernel(ONEPASS)
     rows = np.zeros((5, NC), np.uint64)
     rows[:, :NP] = rand_elems(oracle, 5 * NP, 61).reshape(5, NP)
     got = enc.encode_rows(rows.copy()).reshape(5, NC)
     for r in range(5):
         assert np.array_equal(got[r], oracle.fft_io(0, rows[r])), r
-    with four_step():
-        got4 = enc.encode_rows(rows.copy()).reshape(5, NC)
+    got4 = enc.set_row_kernel(FOURSTEP).encode_rows(rows.copy()).reshape(5, NC)
     assert np.array_equal(got, got4)
 
 
@@ -72,10 +42,12 @@ def test_row1_extreme_values(gpu, oracle, pattern):
         row[0] = 1
     else:
         row[NP - 1] = pm1
-    enc = gpu.RsEncoding.new(0, NP, NC, 4, 1)
-    got = row.copy()
-    enc.encode(got)
-    assert np.array_equal(got, oracle.fft_io(0, row))
+    want = oracle.fft_io(0, row)
+    for kernel in (ONEPASS, FOURSTEP):
+        enc = gpu.RsEncoding.new(0, NP, NC, 4, 1).set_row_kernel(kernel)
+        got = row.copy()
+        enc.encode(got)
+        assert np.array_equal(got, want), kernel
 
 
 @pytest.mark.parametrize("length", [37 * NP, 37 * NP + 5, 3 * NP - 1, 1000, 300 * NP])
@@ -83,7 +55,7 @@ def test_row1_commit_device_matches_oracle(gpu, oracle, hipmem, length):
     """the commit path (canonical output + the commitment's coefficient copy), full and ragged
     last rows, against the oracle's coefficient matrix, codeword, hashes and root"""
     coeffs = rand_elems(oracle, length, 17)
-    g_enc = gpu.RsEncoding.new(0, NP, NC, 16, 2)
+    g_enc = gpu.RsEncoding.new(0, NP, NC, 16, 2).set_row_kernel(ONEPASS)
     o_enc = oracle.Encoding.ligero(0, NP, NC, 16, 2)
     d = hipmem.to_device(coeffs)
     try:
@@ -93,15 +65,14 @@ def test_row1_commit_device_matches_oracle(gpu, oracle, hipmem, length):
         assert np.array_equal(g.comm.reshape(-1), o.comm)
         assert g.hashes == o.hashes
         assert g.get_root() == o.root()
-        with four_step():
-            g4 = gpu.LcCommit.commit_device(d, length, g_enc)
+        g4 = gpu.LcCommit.commit_device(d, length, g_enc.set_row_kernel(FOURSTEP))
         assert g4.get_root() == g.get_root()
         del g, g4
     finally:
         hipmem.free(d)
 
 
-@pytest.mark.parametrize("row1", ["mode", "0"])
+@pytest.mark.parametrize("kernel", [AUTO, FOURSTEP], ids=["auto_onepass", "fourstep_packed"])
 @pytest.mark.parametrize("dims,n_bytes", [
     ((NP, NC), 7 * NP * 5),            # whole rows, one-pass fused unpack
     ((NP, NC), 7 * NP * 300 + 11),     # more rows than CUs (persistent workgroups loop), a ragged last row
@@ -109,16 +80,15 @@ def test_row1_commit_device_matches_oracle(gpu, oracle, hipmem, length):
     ((NP, NC), 13),                    # two elements, one row
     ((100, 256), 7 * 100 * 3 + 5),     # other dims: packed first
 ])
-def test_pos_commit_bytes_device(gpu, oracle, hipmem, row1, dims, n_bytes):
+def test_pos_commit_bytes_device(gpu, oracle, hipmem, kernel, dims, n_bytes):
     """lcpc_pos_commit_bytes_device == DataField::from_byte_vec + LcCommit::commit (the oracle's
-    pos_bytes_to_field + Commit), and == the two-call device path"""
-    if row1 == "0":
-        os.environ["LCPC_NTT_ROW1"] = "0"
+    pos_bytes_to_field + Commit), and == the two-call device path; AUTO = the one-pass kernel with
+    the fused unpack at the PoS dims, FOURSTEP = k_pack7 + the four-step pair"""
     np_, nc = dims
     data = np.random.default_rng(n_bytes).integers(0, 256, n_bytes, dtype=np.uint8)
     data[-1] = 0xff
     el = oracle.pos_bytes_to_field(data.tobytes())
-    g_enc = gpu.RsEncoding.new(0, np_, nc, 16, 2)
+    g_enc = gpu.RsEncoding.new(0, np_, nc, 16, 2).set_row_kernel(kernel)
     o_enc = oracle.Encoding.ligero(0, np_, nc, 16, 2)
     d = hipmem.to_device(np.concatenate([data, np.zeros((-n_bytes) % 8, np.uint8)]).view(np.uint64))
     de = hipmem.to_device(el)
@@ -128,7 +98,7 @@ def test_pos_commit_bytes_device(gpu, oracle, hipmem, row1, dims, n_bytes):
         assert np.array_equal(g.coeffs.reshape(-1), o.coeffs)
         assert np.array_equal(g.comm.reshape(-1), o.comm)
         assert g.get_root() == o.root()
-        assert gpu.LcCommit.commit_device(de, el.size, g_enc).get_root() == g.get_root()
+        assert gpu.LcCommit.commit_device(de, el.size, g_enc.set_row_kernel(AUTO)).get_root() == g.get_root()
         del g
     finally:
         hipmem.free(d)
