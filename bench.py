@@ -401,27 +401,30 @@ def encode_workload(args, L, torch, rank, local_rank):
         enc.encode_rows_device(d_src.data_ptr(), n_per_row, n_per_row, dst[slot].data_ptr(), n_cols, n_rows)
         return None
 
+    ocache = {}
+
     def cpu_baseline(O):
-        # the same rows through the oracle's fft_io, then every GPU row against it
-        # (repeated passes over the rows until about 10 s of CPU work; rate per pass)
-        rows = coeffs.reshape(n_rows, n_per_row * nl)
+        # the oracle's fft_io on every row of the same workload, rows in parallel on the threads
+        # of_set_threads gives it (the reference encodes a commitment's rows in parallel,
+        # lcpc-2d/src/lib.rs:677-682), output buffer allocated once; whole passes until about 5 s,
+        # rate per pass; then every GPU row against the oracle's
+        if not ocache:
+            ocache["enc"] = O.Encoding.ligero(fid, n_per_row, n_cols, rho=args.rho_t)
+            ocache["out"] = np.empty(n_rows * n_cols * nl, np.uint64)
+        o_enc, out = ocache["enc"], ocache["out"]
         passes, t1 = 0, time.perf_counter()
         while True:
-            outs = []
-            for r in range(n_rows):
-                x = np.zeros(n_cols * nl, np.uint64)
-                x[:n_per_row * nl] = rows[r]
-                outs.append(O.fft_io(fid, x))
+            o_enc.encode_rows(coeffs, n_rows, out)
             passes += 1
-            if time.perf_counter() - t1 >= 10.0 or passes >= 64:
+            if time.perf_counter() - t1 >= 5.0 or passes >= 256:
                 break
         dt = (time.perf_counter() - t1) / passes
         step(0)
         torch.cuda.synchronize()
-        got = dst[0].cpu().numpy().view(np.uint64).reshape(n_rows, n_cols * nl)
-        ok = all(np.array_equal(got[r], outs[r]) for r in range(n_rows))
-        return dt, ok, (f"fft_io of all {n_rows} rows of the same 2^{args.log_len} {args.field} workload, "
-                        f"{passes} passes, time per pass")
+        got = dst[0].cpu().numpy().view(np.uint64).reshape(-1)
+        ok = bool(np.array_equal(got, out))
+        return dt, ok, (f"fft_io of all {n_rows} rows of the same 2^{args.log_len} {args.field} workload "
+                        f"(oracle of_enc_encode_rows), {passes} passes, time per pass")
 
     B = 8 * nl
     return Workload(
@@ -432,7 +435,7 @@ def encode_workload(args, L, torch, rank, local_rank):
         config={"workload": f"Ligero R-S encode, {args.field}, 2^{args.log_len} coeffs, "
                             f"{n_rows}x{n_per_row}->{n_cols}",
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols},
-        step=step, cpu_baseline=cpu_baseline, cpu_cores=1, root_is_parity=True, cpu_reps_ok=False,
+        step=step, cpu_baseline=cpu_baseline, root_is_parity=True, cpu_reps_ok=False,
         enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small"),
         enc_kernel_desc=f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per step, all {n_rows} rows)",
         algo_bytes=n_rows * n_per_row * B + n_rows * n_cols * B,
@@ -462,23 +465,29 @@ def sdig_encode_workload(args, L, torch, rank, local_rank):
         enc.encode_rows_device(d_src.data_ptr(), n_per_row, n_per_row, dst[slot].data_ptr(), n_cols, n_rows)
         return None
 
+    ocache = {}
+
     def cpu_baseline(O):
-        # bounded sample: the oracle's encode (encode.rs:36-94) on rows of this workload, one
-        # thread, until about 10 s; then the GPU's rows against those
-        o_enc = O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3)
-        rows = coeffs.reshape(n_rows, n_per_row * nl)
-        outs, t1 = [], time.perf_counter()
-        while len(outs) < n_rows and (time.perf_counter() - t1 < 10.0 or not outs):
-            x = np.zeros(n_cols * nl, np.uint64)
-            x[:n_per_row * nl] = rows[len(outs)]
-            outs.append(o_enc.encode(x))
-        dt = (time.perf_counter() - t1) / len(outs) * n_rows
+        # the oracle's encode (encode.rs:36-94) on every row of this workload, rows in parallel on
+        # the threads of_set_threads gives it (lcpc-2d/src/lib.rs:677-682), output allocated once;
+        # whole passes until about 5 s (at least one); then every GPU row against the oracle's
+        if not ocache:
+            ocache["enc"] = O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3)
+            ocache["out"] = np.empty(n_rows * n_cols * nl, np.uint64)
+        o_enc, out = ocache["enc"], ocache["out"]
+        passes, t1 = 0, time.perf_counter()
+        while True:
+            o_enc.encode_rows(coeffs, n_rows, out)
+            passes += 1
+            if time.perf_counter() - t1 >= 5.0:
+                break
+        dt = (time.perf_counter() - t1) / passes
         step(0)
         torch.cuda.synchronize()
-        got = dst[0].cpu().numpy().view(np.uint64).reshape(n_rows, n_cols * nl)
-        ok = all(np.array_equal(got[r], outs[r]) for r in range(len(outs)))
-        return dt, ok, (f"the oracle's encode of the first {len(outs)} of the {n_rows} rows on one thread "
-                        f"({time.perf_counter() - t1:.1f} s), scaled to all rows; those rows compared")
+        got = dst[0].cpu().numpy().view(np.uint64).reshape(-1)
+        ok = bool(np.array_equal(got, out))
+        return dt, ok, (f"the oracle's encode of all {n_rows} rows (of_enc_encode_rows), {passes} passes, time per "
+                        f"pass; every row compared")
 
     B = 8 * nl
     nnz = enc.matrix_nnz
@@ -491,7 +500,7 @@ def sdig_encode_workload(args, L, torch, rank, local_rank):
                             f"call, {n_rows}x{n_per_row}->{n_cols}",
                 "field": args.field, "len": n, "batch": k, "n_rows": n_rows, "n_per_row": n_per_row,
                 "n_cols": n_cols, "matrix_nnz": nnz},
-        step=step, cpu_baseline=cpu_baseline, cpu_cores=1, root_is_parity=True, cpu_reps_ok=False,
+        step=step, cpu_baseline=cpu_baseline, root_is_parity=True, cpu_reps_ok=False,
         enc_kernels=("transpose", "sdig_encode"),
         enc_kernel_desc=(f"sdig_encode = transpose to element-major + 13 SpMM / Reed-Solomon levels + transpose "
                          f"back (one call, all {n_rows} rows)"),
@@ -854,6 +863,13 @@ def main():
         out["sharded_n1"] = sharded_n1
         if "parity_ok" in out and sharded_n1.get("root") is not None:
             out["parity_ok"] = bool(out["parity_ok"] and sharded_n1["root_equals_replicas"])
+        if sharded_n1.get("value"):
+            # the N = 1 point of the N > 1 lines' own engine: N > 1 runs the row-sharded driver, so a
+            # 1 -> N curve is N's value / this one (the replicas value above is the one-GPU headline)
+            out["scale_base"] = {"value": sharded_n1["value"], "unit": out.get("unit"), "engine": "sharded",
+                                 "what": "the row-sharded engine (--mode sharded, the N > 1 default) at N = 1, same "
+                                         "workload, steps and warm-up: divide an N > 1 line's value by this for its "
+                                         "speed-up on one engine"}
     if rank == 0:
         out["world_formed"] = formed
         print(json.dumps(out), flush=True)
@@ -1354,8 +1370,8 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
             out["parity_vs_oracle"] = bool(oroot)
         elif oroot is not None:
             out["parity_root_vs_oracle"] = oroot == root if root is not None else None
-        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and args.code == "ligero"
-                                               and world == 1):
+        if args.cpu_baseline_1core == "on" or (args.cpu_baseline_1core == "auto" and world == 1 and
+                                               args.code in ("ligero", "encode", "sdig-encode")):
             O.lib().of_set_threads(1)
             cpu1_s, oroot1, sample1 = wl.cpu_baseline(O)
             out["cpu_baseline_1core"] = {"value": wl.units / cpu1_s, "unit": wl.unit, "cores": 1, "kind": "port",

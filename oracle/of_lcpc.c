@@ -164,15 +164,23 @@ typedef struct {
   uint64_t *comm;
   const uint64_t *coeffs;
   int err;
+  size_t src_stride; /* elements between rows of coeffs (n_per_row for a commitment) */
 } enc_ctx;
 static void enc_rows(void *p, size_t lo, size_t hi) {
   enc_ctx *c = (enc_ctx *)p;
   const int nl = of_field_limbs(c->e->fid);
+  const size_t np = c->e->n_per_row, nc = c->e->n_cols;
   for (size_t r = lo; r < hi; r++) {
-    uint64_t *row = c->comm + r * c->e->n_cols * nl;
-    memcpy(row, c->coeffs + r * c->e->n_per_row * nl, sizeof(uint64_t) * nl * c->e->n_per_row);
+    uint64_t *row = c->comm + r * nc * nl;
+    memcpy(row, c->coeffs + r * c->src_stride * nl, sizeof(uint64_t) * nl * np);
+    memset(row + np * nl, 0, sizeof(uint64_t) * nl * (nc - np));
     if (of_enc_encode(c->e, row)) c->err = 1;
   }
+}
+int of_enc_encode_rows(const of_enc *e, const uint64_t *src, size_t src_stride, size_t n_rows, uint64_t *dst) {
+  enc_ctx ec = {e, dst, src, 0, src_stride};
+  of_parallel_for(n_rows, 1, enc_rows, &ec);
+  return ec.err ? 8 : 0;
 }
 
 typedef struct {
@@ -228,7 +236,7 @@ of_commit *of_commit_new(const of_enc *e, const uint64_t *coeffs_in, size_t len)
   c->coeffs = (uint64_t *)calloc(n_rows * n_per_row * nl, sizeof(uint64_t));
   c->comm = (uint64_t *)calloc(n_rows * n_cols * nl, sizeof(uint64_t));
   memcpy(c->coeffs, coeffs_in, sizeof(uint64_t) * nl * len);
-  enc_ctx ec = {e, c->comm, c->coeffs, 0};
+  enc_ctx ec = {e, c->comm, c->coeffs, 0, n_per_row};
   of_parallel_for(n_rows, 1, enc_rows, &ec);
   if (ec.err) {
     of_commit_free(c);

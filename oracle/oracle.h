@@ -113,6 +113,10 @@ of_enc *of_enc_ligero(int fid, size_t n_per_row, size_t n_cols, size_t n_col_ope
                       size_t n_degree_tests);
 void of_enc_free(of_enc *e);
 int of_enc_encode(const of_enc *e, uint64_t *row); /* in place on n_cols elements */
+/* rows r < n_rows: dst + r n_cols = encode(src + r src_stride's n_per_row elements, zero padded),
+ * rows in parallel on of_set_threads threads (the row-parallel encode of commit,
+ * lcpc-2d/src/lib.rs:677-682); 0 or the first error */
+int of_enc_encode_rows(const of_enc *e, const uint64_t *src, size_t src_stride, size_t n_rows, uint64_t *dst);
 
 typedef struct of_commit {
   int fid, nl;

@@ -101,6 +101,7 @@ def _setup(L):
                                            C.c_size_t, C.c_size_t]),
         "of_enc_free": (None, [C.POINTER(OfEnc)]),
         "of_enc_encode": (C.c_int, [C.POINTER(OfEnc), u64p]),
+        "of_enc_encode_rows": (C.c_int, [C.POINTER(OfEnc), u64p, C.c_size_t, C.c_size_t, u64p]),
         "of_set_threads": (None, [C.c_int]),
         "of_commit_new": (C.POINTER(OfCommit), [C.POINTER(OfEnc), u64p, C.c_size_t]),
         "of_commit_free": (None, [C.POINTER(OfCommit)]),
@@ -338,6 +339,19 @@ class Encoding:
         if rc:
             raise ValueError(f"encode error {rc}")
         return a
+
+    def encode_rows(self, src: np.ndarray, n_rows: int, out: np.ndarray = None) -> np.ndarray:
+        """every row's n_per_row leading coefficients (rows n_per_row apart in src) encoded, rows in
+        parallel on of_set_threads threads; out: [n_rows][n_cols] limbs"""
+        nl = limbs(self.fid)
+        s = np.ascontiguousarray(src, dtype=np.uint64).reshape(-1)
+        assert s.size >= n_rows * self.n_per_row * nl
+        if out is None:
+            out = np.empty(n_rows * self.n_cols * nl, np.uint64)
+        rc = lib().of_enc_encode_rows(self.ptr, p64(s), self.n_per_row, n_rows, p64(out))
+        if rc:
+            raise ValueError(f"encode error {rc}")
+        return out
 
     def __del__(self):
         try:

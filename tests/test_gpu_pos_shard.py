@@ -6,8 +6,10 @@ client.rs:443-456) with their Merkle paths.
 
 Each rank packs only its own rows' bytes (7 per WriteableFt63 element, data_field.rs:38-46) on
 the device, commits its rows (csrc/shard_native.cpp), and the request's partial sums and column
-pieces are gathered at the root.  One rank (no exchanges), and two / four ranks sharing the one
-GPU with host-staged gloo collectives (RCCL refuses two ranks on one GPU).
+pieces are gathered at the root.  One rank (no exchanges), two / four ranks sharing the one
+GPU with host-staged gloo collectives, and eight ranks on the one GPU through RCCL itself (a
+distinct NCCL_HOSTID per rank: RCCL then connects the ranks over its socket transport instead of
+refusing two ranks on one GPU) -- cfg5's N = 8 exchange pattern.
 """
 import hashlib
 import os
@@ -75,8 +77,13 @@ def test_sharded_pos_request_world1(gpu, hipmem):
     assert all(res.values()), res
 
 
-def _worker(rank, world, port, args, q):
+RCCL_SAME_GPU_ENV = {"NCCL_IB_DISABLE": "1", "NCCL_SOCKET_IFNAME": "lo", "LCPC_SHARD_WATCHDOG_S": "120"}
+
+
+def _worker(rank, world, port, args, q, rccl=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if rccl:
+        os.environ.update(RCCL_SAME_GPU_ENV, NCCL_HOSTID=f"lcpc-pos-rank-{rank}")
     sys.path.insert(0, ROOT)
     sys.path.insert(0, HERE)
     import torch.distributed as dist
@@ -86,7 +93,8 @@ def _worker(rank, world, port, args, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         L.set_device(0)
-        comm = shard.NativeComm.host(dist)
+        comm = shard.NativeComm.rccl(dist) if rccl else shard.NativeComm.host(dist)
+        assert comm.is_rccl == rccl and comm.world == world
         q.put((rank, _request(L, _HipMem(), comm, *args)))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, {"error": repr(e)}))
@@ -94,14 +102,14 @@ def _worker(rank, world, port, args, q):
         dist.destroy_process_group()
 
 
-def _spawn(args, world, timeout=280):
+def _spawn(args, world, timeout=280, rccl=False):
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, args, q, rccl)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=timeout) for _ in range(world))
@@ -116,6 +124,17 @@ def test_sharded_pos_request_64mib(gpu, world, root):
     res = _spawn((64 << 20, 7, root), world)
     for r in range(world):
         assert "error" not in res[r] and all(res[r].values()), (r, res[r])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("root", [0, 5])
+def test_sharded_pos_request_64mib_world8_rccl_one_gpu(gpu, root):
+    """cfg5's eight-rank exchanges (row shards cut at BLAKE3 chunk boundaries, chaining-value
+    all-to-all, subtree all-gather, partial u^T Enc(M) and column-piece gathers) through RCCL,
+    eight ranks on the one GPU: root, tree, u^T Enc(M), columns and paths against the oracle"""
+    res = _spawn((64 << 20, 11, root), 8, rccl=True)
+    bad = {r: res[r] for r in range(8) if "error" in res[r] or not all(res[r].values())}
+    assert not bad, bad
 
 
 @pytest.mark.slow
