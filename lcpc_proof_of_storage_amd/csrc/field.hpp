@@ -283,8 +283,21 @@ __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
   uint32_t m[N], out[N];
   uint64_t acc = 0;
   uint32_t r2 = 0;
+  // column 0 alone: a0 b0 <= (2^32 - 1)^2 cannot carry out of 64 bits, and its high word is at
+  // most 2^32 - 2, so hi + (lo != 0) cannot carry either: m0 = -lo, next addend (hi + borrow, 0)
+  // -- two instructions after the product instead of a carry fold and a three-instruction step
+  {
+    const uint64_t p0 = (uint64_t)a.v[0] * b.v[0];
+    uint32_t nlo;
+    uint64_t c0, c1;
+    asm("v_sub_co_u32_e64 %0, %2, 0, %4\n\t"
+        "v_addc_co_u32_e64 %1, %3, %5, 0, %2"
+        : "=&v"(m[0]), "=&v"(nlo), "=&s"(c0), "=&s"(c1)
+        : "v"((uint32_t)p0), "v"((uint32_t)(p0 >> 32)));
+    acc = nlo;
+  }
 #pragma unroll
-  for (int k = 0; k < 2 * N; k++) {
+  for (int k = 1; k < 2 * N; k++) {
     uint64_t cprev = 0, ccur;
     bool have = false;
 #pragma unroll
