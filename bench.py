@@ -1294,6 +1294,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     L.prof_reset()
     barrier()
     t0 = time.perf_counter()
+    t0_mono_ns = time.clock_gettime_ns(time.CLOCK_MONOTONIC)  # (--timeline: aligns with a rocprofv3 trace)
     c0, th0 = os.times(), cgroup_throttle()
     start.set()
     for w in workers:
@@ -1307,7 +1308,9 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     c1, th1 = os.times(), cgroup_throttle()
     if args.timeline and getattr(wl, "timeline", None) is not None:
         tl = [(s_, a - t0, b - t0, c - t0, d - t0) for s_, a, b, c, d in wl.timeline if a >= t0]
-        json.dump({"elapsed": elapsed, "steps": sorted(tl, key=lambda r: r[2])}, open(args.timeline, "w"))
+        json.dump({"elapsed": elapsed, "t0_monotonic_ns": t0_mono_ns,
+                   "columns": ["slot", "t_gate", "t_commit_start", "t_commit_end", "t_prove_end"],
+                   "steps": sorted(tl, key=lambda r: r[2])}, open(args.timeline, "w"))
     L.prof_enable(False)
     stats = L.prof_stats() if (prof and args.prof_timed) else {}
     iso = {}
