@@ -103,10 +103,18 @@ void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
       V2(7, 3, 7, 9, 2, 8)
       V2(7, 4, 8, 9, 2, 8)
       V2(6, 4, 7, 10, 1, 8)
-    } else if (log_n == 14) {
-      V2(7, 3, 7, 7, 3, 7)
+    } else if (log_n == 14) {  // cfg2 (128 rows): the product shape first, then occupancy / tile sweeps
       V2(7, 4, 8, 7, 4, 8)
+      V2(7, 3, 7, 7, 3, 7)
       V2(7, 2, 6, 7, 2, 6)
+      V2(7, 4, 9, 7, 4, 9)
+      V2(7, 3, 8, 7, 3, 8)
+      V2(7, 2, 7, 7, 2, 7)
+      V2(7, 5, 9, 7, 5, 9)
+      V2(7, 5, 10, 7, 5, 10)
+      V2(7, 3, 7, 7, 4, 8)
+      V2(7, 4, 8, 7, 3, 7)
+      V2(7, 2, 6, 7, 3, 7)
     }
   } else if constexpr (F::ID == 0) {
     if (log_n == 15) {  // PoS default dims: l1 = 7, l2 = 8; pass-A shapes at a fixed pass B, then B
@@ -190,6 +198,7 @@ void bench(const char *fname, int log_n, size_t rows, bool with_copy = false) {
 int main(int argc, char **argv) {
   const int which = argc > 1 ? atoi(argv[1]) : 1;
   if (which == 1) { bench<Ft127>("Ft127", 16, 512); bench<Ft127>("Ft127", 14, 128); }
+  if (which == 2) bench<Ft127>("Ft127 cfg2", 14, 128);
   if (which == 0) bench<Ft63>("Ft63", 16, 512);
   if (which == 5) bench<Ft63>("Ft63 PoS 1 GiB (copy)", 15, 9363, true);
   if (which == 7) bench<Ft63>("Ft63 PoS bench dims (copy)", 17, 2341, true);
