@@ -420,6 +420,8 @@ struct PinnedSlot {
 };
 enum { PIN_REPR = 0, PIN_PRANDOM, PIN_PEVAL, PIN_COLS, PIN_PATHS, PIN_TENSOR, PIN_OUTER, PIN_STAGE, PIN_STAGE2, PIN_N };
 inline thread_local PinnedSlot t_pin[PIN_N];
+// lcpc_prove: the evaluation's repr bytes, converted with the first degree test's (host memory)
+inline thread_local std::vector<uint8_t> t_eval_repr;
 
 inline size_t next_pow2(size_t v) {
   size_t p = 1;

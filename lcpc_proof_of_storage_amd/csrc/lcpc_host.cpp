@@ -431,6 +431,7 @@ lcpc_status lcpc_prepare_thread(const lcpc_encoding *e, size_t n_rows) {
   const size_t want[PIN_N] = {2 * np * wb, 1, 1, 1, nco * 8, n_rows * wb, n_rows * wb, 1, 1};
   for (int i = 0; i < PIN_N; i++)
     if (!t_pin[i].get(std::max<size_t>(1, want[i]))) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  t_eval_repr.reserve(np * wb);
   return LCPC_OK;
 }
 
@@ -699,6 +700,10 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   std::vector<uint64_t> tensor;
   const uint8_t *repr = nullptr;
   bool eval_done = false;
+  // the evaluation's repr bytes, converted in the first round's GPU round trip (its absorb comes
+  // after the last degree test's): one round trip fewer on the proof's serial path
+  std::vector<uint8_t> &eval_repr = t_eval_repr;
+  bool eval_repr_ready = false;
   for (size_t i = 0; i < ndt; i++) {
     {
       prof::HostScope hs("host_prove_round_issue");
@@ -714,11 +719,16 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
         eval_done = true;
       }
     }
+    const bool with_eval = i == 0;  // round 0 also holds the evaluation (dres[np, 2 np))
     {
       prof::HostScope hs("host_prove_gpu_wait");
-      st = to_repr_host(dev, fid, dres.as<uint32_t>(), np, &repr);  // syncs the stream
+      st = to_repr_host(dev, fid, dres.as<uint32_t>(), with_eval ? 2 * np : np, &repr);  // syncs the stream
     }
     if (st) return st;
+    if (with_eval) {
+      eval_repr.assign(repr + np * wb, repr + 2 * np * wb);
+      eval_repr_ready = true;
+    }
     {
       prof::HostScope hs("host_prove_transcript");
       tr->t.append_messages(LABEL_PR, 6, repr, wb, np);
@@ -731,7 +741,9 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
     HIP_TRY(d2h(h_peval, dres.p, np * wb, s));
     d_eval = dres.as<uint32_t>();
   }
-  {
+  if (eval_repr_ready) {
+    repr = eval_repr.data();
+  } else {
     prof::HostScope hs("host_prove_gpu_wait");
     st = to_repr_host(dev, fid, d_eval, np, &repr);
   }
