@@ -46,12 +46,15 @@ class OrderedPool {
   // A cached block of exactly `bytes`, ordered after its fence on `s` (on the host when s is
   // none), or nullptr when none is cached.
   void *take(size_t bytes, Stream s) {
-    std::lock_guard<std::mutex> lk(mu_);
-    auto it = free_.find(bytes);
-    if (it == free_.end()) return nullptr;
-    Entry e = std::move(it->second);
-    free_.erase(it);
-    order_after(e, s);
+    Entry e;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = free_.find(bytes);
+      if (it == free_.end()) return nullptr;
+      e = std::move(it->second);
+      free_.erase(it);
+    }
+    order_after(e, s);  // (device-side waits, or a host wait, outside the lock)
     return e.p;
   }
 
@@ -108,9 +111,18 @@ class OrderedPool {
     std::lock_guard<std::mutex> lk(mu_);
     return retiring_.size();
   }
-  size_t waits_issued() const { return waits_; }
-  size_t host_syncs() const { return syncs_; }
-  size_t same_stream() const { return same_; }
+  size_t waits_issued() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return waits_;
+  }
+  size_t host_syncs() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return syncs_;
+  }
+  size_t same_stream() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return same_;
+  }
 
   ~OrderedPool() {
     for (Event e : idle_) b_.event_free(e);
@@ -128,23 +140,32 @@ class OrderedPool {
   };
 
   void order_after(Entry &e, Stream s) {
+    Event to_retire[MAX_STREAMS], to_idle[MAX_STREAMS];
+    int nr = 0, ni = 0;
+    size_t waits = 0, syncs = 0, same = 0;
     for (int i = 0; i < e.n; i++) {
       Event ev = e.ev[i];
       if (s != Stream{} && s == e.st[i]) {
-        retiring_.push_back(ev);  // the taker's own stream: already ordered after the fence
-        same_++;
+        to_retire[nr++] = ev;  // the taker's own stream: already ordered after the fence
+        same++;
       } else if (b_.done(ev)) {
-        recycle(ev);
+        to_idle[ni++] = ev;
       } else if (s != Stream{} && b_.wait(s, ev)) {
-        waits_++;
-        retiring_.push_back(ev);
+        waits++;
+        to_retire[nr++] = ev;
       } else {
         b_.sync(ev);
-        syncs_++;
-        recycle(ev);
+        syncs++;
+        to_idle[ni++] = ev;
       }
     }
     e.n = 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int i = 0; i < nr; i++) retiring_.push_back(to_retire[i]);
+    for (int i = 0; i < ni; i++) recycle(to_idle[i]);
+    waits_ += waits;
+    syncs_ += syncs;
+    same_ += same;
     reap(false);
   }
 
@@ -178,7 +199,7 @@ class OrderedPool {
   std::mutex mu_;
   std::multimap<size_t, Entry> free_;
   std::vector<Event> idle_, retiring_;
-  size_t waits_ = 0, syncs_ = 0, same_ = 0;
+  size_t waits_ = 0, syncs_ = 0, same_ = 0;  // (under mu_)
 };
 
 }  // namespace lcpc_pool
