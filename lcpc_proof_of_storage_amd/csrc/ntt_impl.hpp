@@ -171,8 +171,7 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
       return ntt_row1::launch<F>(p, src, ss, nv, dst, ds, n_rows, s, cp, cs, canon);
   }
   constexpr int HI = F::N >= 8 ? 11 : 12;  // LDS budget of 32-byte fields
-  auto pass_a = [&]<int L, int CW>() {
-    constexpr int T = L + CW - R;
+  auto pass_a = [&]<int L, int CW, int T = L + CW - R>() {
     // the inter-pass twiddles in [t][c] layout (canonical words for canon_out)
     const uint32_t *t2 = canon ? p.d_tw2_canon : p.d_tw2;
     if (halfz && canon)
@@ -184,6 +183,17 @@ hipError_t ntt_rows_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t n
     return ntt_v2::launch_a<F, L, CW, T, false>(src, ss, nv, dst, ds, p.d_tw, p.log_n, n_rows, s, cp, cs, t2);
   };
   hipError_t e;
+  if constexpr (F::ID == 1) {
+    // cfg2 (2^14-point rows, 128 rows per 2^20-coefficient commitment): both passes over 32
+    // vectors of 128 points in 1024 threads, radix-2^2 register rounds -- one launch holds only
+    // 1024 tiles of the default shape (one partial wave of blocks), and twice the waves per CU
+    // hide its load and store phases: 0.059 against 0.066 ms for the pair
+    // (tools/microbench/nttbench.hip mode 2, profiles/r05_nttbench_cfg2.txt)
+    if (p.log_n == 14 && p.l1 == 7) {
+      if ((e = pass_a.template operator()<7, 5, 10>()) != hipSuccess) return e;
+      return ntt_v2::launch_b<F, 7, 5, 10>(dst, ds, p.d_tw, p.log_n, n_rows, s);
+    }
+  }
   if constexpr (F::ID == 0) {
     // PoS default dims (n_cols = 2^15, ntt_plan_init's l1 = 8): pass A over 32 columns of
     // 256-point DIFs in 1024 threads (tools/microbench/nttbench.hip mode 5, fastest split).

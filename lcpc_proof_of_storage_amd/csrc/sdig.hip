@@ -82,7 +82,11 @@ __device__ __forceinline__ uint32_t pick4(uint32_t d0, uint32_t d1, uint32_t d2,
   const uint32_t s = __builtin_amdgcn_perm(d3, d2, sel_lo);
   return __builtin_amdgcn_perm(s, t, sel_hi);
 }
-template <class F, int TILES>
+// SPLIT = 4 (the small levels): the four waves of a block share ONE output and take its
+// 4-nonzero groups in turn (wave w: groups w, w + 4, ...); their int32 digit sums are added
+// through LDS before the one reduction.  A level with few outputs is latency-bound -- each wave's
+// groups are a dependent gather -> MFMA chain -- and this cuts that chain by four.
+template <class F, int TILES, int SPLIT = 1>
 __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ gptr,
                                                    const uint32_t *__restrict__ pidx,
                                                    const uint32_t *__restrict__ gval,
@@ -93,9 +97,10 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ 
   __shared__ int red[4][TILES][16][17];
   __shared__ uint32_t nbr[4][4 * SPMM_MAX_GROUPS];
   __shared__ uint32_t tr[4][2][4][4][16];  // [wave][buffer][g][u / 4][a]
+  static_assert(SPLIT == 1 || SPLIT == 4, "one output per wave, or per block of four waves");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t j = (size_t)blockIdx.x * 4 + wave;
-  if (j >= m) return;  // whole waves only: the kernel synchronises within a wave
+  const size_t j = SPLIT == 1 ? (size_t)blockIdx.x * 4 + wave : (size_t)blockIdx.x;
+  if (j >= m) return;  // whole waves (SPLIT: the whole block) only: they synchronise below
   const int n = lane & 15, g = lane >> 4;
   const size_t b0 = row0 + (size_t)blockIdx.y * TILES * 16;
   const uint32_t q0 = gptr[j], nq = gptr[j + 1] - q0;
@@ -127,16 +132,17 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ 
       xv[t] = rowok[t] ? x4[id * R + b0 + 16 * t + n] : make_uint4(0, 0, 0, 0);
   };
   uint4 xc[TILES], xn[TILES], vc, vn;
-  if (nq) load(0, xc, vc);
-  for (uint32_t q = 0; q < nq; q++) {
-    const bool more = q + 1 < nq;
-    if (more) load(q + 1, xn, vn);
+  const uint32_t q_first = SPLIT == 1 ? 0u : (uint32_t)wave;
+  if (q_first < nq) load(q_first, xc, vc);
+  for (uint32_t q = q_first; q < nq; q += SPLIT) {
+    const bool more = q + SPLIT < nq;
+    if (more) load(q + SPLIT, xn, vn);
     // A fragment of group q
     Fe<F> v;
     v.v[0] = vc.x; v.v[1] = vc.y; v.v[2] = vc.z; v.v[3] = vc.w;
     const Fe<F> h = fe_mul<F>(v, pn);
     const cmfma::v4i hd = cmfma::balanced_digits(h.v[0], h.v[1], h.v[2], h.v[3]);
-    uint32_t(*T)[4][16] = tr[wave][q & 1];
+    uint32_t(*T)[4][16] = tr[wave][(q / SPLIT) & 1];
     T[g][0][n] = (uint32_t)hd.x;
     T[g][1][n] = (uint32_t)hd.y;
     T[g][2][n] = (uint32_t)hd.z;
@@ -171,18 +177,33 @@ __global__ __launch_bounds__(256) void k_spmm_mfma(const uint32_t *__restrict__ 
     rw[t][4 * g + 2][n] = acc[t].z;
     rw[t][4 * g + 3][n] = acc[t].w;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if constexpr (SPLIT == 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-  for (int p = 0; p < TILES; p += 4) {
-    const int t = p + g;
-    const size_t b = b0 + 16 * (size_t)t + n;
-    if (t < TILES && b < row_end) {
-      int Y[16];
+    for (int p = 0; p < TILES; p += 4) {
+      const int t = p + g;
+      const size_t b = b0 + 16 * (size_t)t + n;
+      if (t < TILES && b < row_end) {
+        int Y[16];
 #pragma unroll
-      for (int u = 0; u < 16; u++) Y[u] = rw[t][u][n];
-      fe_store<F>(y, j * R + b, cmfma::recombine_redc<F>(Y));
+        for (int u = 0; u < 16; u++) Y[u] = rw[t][u][n];
+        fe_store<F>(y, j * R + b, cmfma::recombine_redc<F>(Y));
+      }
+    }
+  } else {
+    __syncthreads();  // every wave's partial digit sums are in red[]
+    // thread (t, n): the four waves' sums for row n of tile t, then the one reduction
+    for (int i = threadIdx.x; i < TILES * 16; i += 256) {
+      const int t = i >> 4, r = i & 15;
+      const size_t b = b0 + 16 * (size_t)t + r;
+      if (b < row_end) {
+        int Y[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) Y[u] = red[0][t][u][r] + red[1][t][u][r] + red[2][t][u][r] + red[3][t][u][r];
+        fe_store<F>(y, j * R + b, cmfma::recombine_redc<F>(Y));
+      }
     }
   }
 }
@@ -255,11 +276,20 @@ inline void mfma_tiling(size_t R, int &tiles, unsigned &chunks) {
   tiles = (int)((R + 16 * chunks - 1) / (16 * chunks));
 }
 
+// levels with fewer outputs than this take the split kernel (four waves per output): the
+// expander's small levels (SdigCode3 at cfg4: pre2-pre5 and post2-post5, 8-1864 outputs) are
+// latency chains of 8-19 groups per wave, 15-26 us each with one wave per output
+constexpr size_t SPMM_SPLIT_BELOW = 2048;
+
 template <class F, int TILES>
 void launch_spmm_mfma(const CsrDev &M, const uint32_t *x, uint32_t *y, size_t R, size_t b0, size_t nb,
                       unsigned chunks, hipStream_t s) {
-  hipLaunchKernelGGL((k_spmm_mfma<F, TILES>), dim3((unsigned)((M.rows + 3) / 4), chunks), dim3(256), 0, s,
-                     M.gptr, M.pidx, M.gval, x, y, M.rows, (uint32_t)R, (uint32_t)b0, (uint32_t)(b0 + nb));
+  if (M.rows < SPMM_SPLIT_BELOW)
+    hipLaunchKernelGGL((k_spmm_mfma<F, TILES, 4>), dim3((unsigned)M.rows, chunks), dim3(256), 0, s, M.gptr, M.pidx,
+                       M.gval, x, y, M.rows, (uint32_t)R, (uint32_t)b0, (uint32_t)(b0 + nb));
+  else
+    hipLaunchKernelGGL((k_spmm_mfma<F, TILES>), dim3((unsigned)((M.rows + 3) / 4), chunks), dim3(256), 0, s,
+                       M.gptr, M.pidx, M.gval, x, y, M.rows, (uint32_t)R, (uint32_t)b0, (uint32_t)(b0 + nb));
 }
 
 // y = M x on rows [b0, b0 + nb) of the element-major vectors (R rows)
