@@ -51,7 +51,7 @@ def _words(v: int, nl: int):
 
 
 @pytest.mark.parametrize("fid", FIELDS)
-@pytest.mark.parametrize("log_n", [13, 16])
+@pytest.mark.parametrize("log_n", [13, 14, 16])  # (14: Ft127's cfg2 shape, 1024-thread radix-2^2 passes)
 @pytest.mark.parametrize("pattern", ["max", "alternating", "max_zero_half", "max_halfz"])
 def test_encode_extreme_values(gpu, oracle, fid, log_n, pattern):
     """Rows of the largest residue p - 1 (raw Montgomery words), alternating 0 / p - 1, and a
