@@ -64,6 +64,14 @@ def main():
         # one encode = one transpose + every SpMM level + the R-S base
         n_enc = nf["transpose"]
         enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in SDIG_ENCODE) / n_enc
+    elif a.code.startswith("sdig-encode"):
+        # LcEncoding::encode of row-major device rows: transpose in, the levels, transpose back
+        n_enc = nf["transpose"] // 2
+        enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in SDIG_ENCODE) / n_enc
+    elif a.code == "encode":
+        # the R-S encode alone: one pass-A + pass-B pair per step
+        n_enc = nf["ntt_pass_a"]
+        enc = sum(2.0 * ftot.get(k, 0.0) + wtot.get(k, 0.0) for k in ("ntt_pass_a", "ntt_pass_b")) / n_enc
     else:
         # (pos-row1: the one-pass Ft63 row kernel, whose 8-byte loads arrive as 128-byte runs; the
         # x2 read correction is checked by its read figure against the input's size)
