@@ -91,6 +91,8 @@ struct HipPoolBackend {
   void drain(Stream s) { (void)hipStreamSynchronize(s); }
 };
 
+enum { POOL_BULK = 0, POOL_HIGH = 1, POOL_PROVER = 2 };
+
 // A pool of HIP streams and a caching allocator per device.  Every API call leases its own
 // stream, so independent commitments run concurrently (their CPU-side Fiat-Shamir work
 // overlaps another commitment's kernels); only pool bookkeeping is locked.
@@ -99,7 +101,9 @@ struct Device {
   bool ok = false;
   std::string init_err;
   std::mutex mu;  // guards the pools below
-  std::vector<hipStream_t> idle_streams[2];  // [0] bulk (commit / encode), [1] high priority
+  // [POOL_BULK] commit / encode, [POOL_HIGH] the latency-side calls (verify, openings, the sharded
+  // driver), [POOL_PROVER] lcpc_prove's row combinations and gathers (optionally CU-masked)
+  std::vector<hipStream_t> idle_streams[3];
   // device blocks: cached by exact size, each ordered after a fence on the streams that used it
   // (pool.hpp); sizes = every block this device allocated
   HipPoolBackend pool_backend;
@@ -118,7 +122,7 @@ struct Device {
     return v;
   }
 
-  hipStream_t acquire_stream(bool high) {
+  hipStream_t acquire_stream(int pool) {
     if (serial_mode()) {
       std::lock_guard<std::mutex> lk(mu);
       if (!shared_stream) {
@@ -130,18 +134,42 @@ struct Device {
     }
     {
       std::lock_guard<std::mutex> lk(mu);
-      auto &pool = idle_streams[high ? 1 : 0];
-      if (!pool.empty()) {
-        hipStream_t s = pool.back();
-        pool.pop_back();
+      auto &idle = idle_streams[pool];
+      if (!idle.empty()) {
+        hipStream_t s = idle.back();
+        idle.pop_back();
         return s;
       }
     }
     prof::HostScope hs("rt_stream_create");
     hipStream_t s = nullptr;
     (void)hipSetDevice(id);
-    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, stream_priority(high)) != hipSuccess) return nullptr;
+    if (pool == POOL_PROVER && prover_cus() > 0) {
+      // the prover's streams on a subset of the CUs, spread evenly (every k-th CU index, whatever
+      // the index-to-XCD mapping): its short row combinations and gathers then never hold CUs the
+      // commitments' encodes need, and the last root lands earlier
+      int n_cu = 0;
+      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, id) == hipSuccess && n_cu > 0 &&
+          prover_cus() < n_cu) {
+        std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
+        const int step = n_cu / prover_cus();
+        for (int k = 0, c = 0; k < prover_cus() && c < n_cu; k++, c += step) mask[c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return s;
+        (void)hipGetLastError();
+        s = nullptr;
+      }
+    }
+    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, stream_priority(pool != POOL_BULK)) != hipSuccess)
+      return nullptr;
     return s;
+  }
+  // LCPC_PROVER_CUS=k: lcpc_prove's streams run on k of the device's CUs (0 / unset: all)
+  static int prover_cus() {
+    static const int v = [] {
+      const char *e = getenv("LCPC_PROVER_CUS");
+      return e ? std::max(0, atoi(e)) : 0;
+    }();
+    return v;
   }
   // Every stream at ONE priority (round 5): mixed priorities are the one condition under which a
   // wrong commitment was ever observed (eight ranks on one GPU), and a high-priority
@@ -160,10 +188,10 @@ struct Device {
     if (!priority_streams() || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return 0;
     return high ? hi : lo;
   }
-  void release_stream(hipStream_t s, bool high) {
+  void release_stream(hipStream_t s, int pool) {
     if (serial_mode()) return;
     std::lock_guard<std::mutex> lk(mu);
-    idle_streams[high ? 1 : 0].push_back(s);
+    idle_streams[pool].push_back(s);
   }
   static size_t round_bytes(size_t bytes) { return ((bytes ? bytes : 16) + 255) & ~(size_t)255; }
   // a block of at least `bytes`, ordered after every earlier use of it: on stream `s` when given
@@ -303,17 +331,16 @@ struct Lease {
   Device *d;
   hipStream_t s;
   hipStream_t prev;
-  bool high;
-  explicit Lease(Device *dev, bool high_priority = false)
-      : d(dev), s(nullptr), prev(t_stream), high(high_priority) {
+  int pool;
+  explicit Lease(Device *dev, int stream_pool = POOL_BULK) : d(dev), s(nullptr), prev(t_stream), pool(stream_pool) {
     (void)hipSetDevice(dev->id);
-    s = dev->acquire_stream(high);
+    s = dev->acquire_stream(pool);
     t_stream = s;
   }
   ~Lease() {
     if (s) {
       (void)hipStreamSynchronize(s);
-      d->release_stream(s, high);
+      d->release_stream(s, pool);
     }
     t_stream = prev;
   }

@@ -402,13 +402,13 @@ lcpc_status lcpc_reserve(const lcpc_encoding *e, size_t len, size_t count) {
   for (void *p : blocks) dev->release(p);
   std::vector<hipStream_t> lo, hi;
   for (size_t k = 0; k < count; k++) {
-    lo.push_back(dev->acquire_stream(false));
-    hi.push_back(dev->acquire_stream(true));
+    lo.push_back(dev->acquire_stream(POOL_BULK));
+    hi.push_back(dev->acquire_stream(POOL_PROVER));
   }
   for (hipStream_t s : lo)
-    if (s) dev->release_stream(s, false);
+    if (s) dev->release_stream(s, POOL_BULK);
   for (hipStream_t s : hi)
-    if (s) dev->release_stream(s, true);
+    if (s) dev->release_stream(s, POOL_PROVER);
   // the page-locked blocks of `count` proofs (p_random, p_eval, columns, paths)
   const size_t ndt = e->n_degree_tests;
   std::vector<void *> pins;
@@ -666,7 +666,7 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   if (outer_len != c->n_rows || (!outer && outer_len))
     return fail(LCPC_PROVER_OUTER_TENSOR, "ProverError::OuterTensor");
   Device *dev = c->dev;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_PROVER);
   HIP_TRY(hipSetDevice(dev->id));
   hipStream_t s = lease.s;
   const int fid = c->fid, wb = field_bytes(fid), limbs = wb / 8;
