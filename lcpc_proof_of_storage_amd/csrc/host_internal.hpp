@@ -102,7 +102,9 @@ struct Device {
   std::string init_err;
   std::mutex mu;  // guards the pools below
   // [POOL_BULK] commit / encode, [POOL_HIGH] the latency-side calls (verify, openings, the sharded
-  // driver), [POOL_PROVER] lcpc_prove's row combinations and gathers (optionally CU-masked)
+  // driver), [POOL_PROVER] lcpc_prove's row combinations and gathers.  (Confining the prover's
+  // streams to a quarter or eighth of the CUs, so that its kernels never hold CUs the encodes
+  // need, changed the K = 20 line by less than its spread: profiles/r05_k20_prover_cu_mask_ab.json.)
   std::vector<hipStream_t> idle_streams[3];
   // device blocks: cached by exact size, each ordered after a fence on the streams that used it
   // (pool.hpp); sizes = every block this device allocated
@@ -144,32 +146,9 @@ struct Device {
     prof::HostScope hs("rt_stream_create");
     hipStream_t s = nullptr;
     (void)hipSetDevice(id);
-    if (pool == POOL_PROVER && prover_cus() > 0) {
-      // the prover's streams on a subset of the CUs, spread evenly (every k-th CU index, whatever
-      // the index-to-XCD mapping): its short row combinations and gathers then never hold CUs the
-      // commitments' encodes need, and the last root lands earlier
-      int n_cu = 0;
-      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, id) == hipSuccess && n_cu > 0 &&
-          prover_cus() < n_cu) {
-        std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
-        const int step = n_cu / prover_cus();
-        for (int k = 0, c = 0; k < prover_cus() && c < n_cu; k++, c += step) mask[c / 32] |= 1u << (c % 32);
-        if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return s;
-        (void)hipGetLastError();
-        s = nullptr;
-      }
-    }
     if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, stream_priority(pool != POOL_BULK)) != hipSuccess)
       return nullptr;
     return s;
-  }
-  // LCPC_PROVER_CUS=k: lcpc_prove's streams run on k of the device's CUs (0 / unset: all)
-  static int prover_cus() {
-    static const int v = [] {
-      const char *e = getenv("LCPC_PROVER_CUS");
-      return e ? std::max(0, atoi(e)) : 0;
-    }();
-    return v;
   }
   // Every stream at ONE priority (round 5): mixed priorities are the one condition under which a
   // wrong commitment was ever observed (eight ranks on one GPU), and a high-priority
