@@ -558,6 +558,18 @@ lcpc_status lcpc_sharded_p2p_schedule(lcpc_field f, size_t n_rows, size_t n_per_
                                       size_t n_polys, size_t lag, lcpc_p2p_record *out, size_t cap,
                                       size_t *n_out);
 
+/* ------------------------------------------------------------------ diagnostics
+ * On-device check of the stream-ordered buffer pool the commit / prove / shard paths share
+ * (no reference counterpart: its buffers are host Vecs).  Each round releases a 1 MiB block
+ * while a writer that spins spin_us before storing still owns it, takes the same block on
+ * another stream and overwrites it at once: *violations counts words the late writer clobbered
+ * across the pool's fences (two fenced rounds per round: writer on the allocating stream, writer
+ * on a second stream), *control_violations the same for one unfenced control round (expected
+ * non-zero when the streams run concurrently), *reused the takes that returned the same block.
+ * spin_us <= 100000. */
+lcpc_status lcpc_selftest_pool_ordering(int rounds, uint32_t spin_us, uint64_t *violations,
+                                        uint64_t *control_violations, uint64_t *reused);
+
 /* ------------------------------------------------------------------ kernel timing
  * HIP-event timing of every kernel launch on the handle streams (off by default). */
 void lcpc_prof_enable(int enable);

@@ -10,5 +10,5 @@ from .lcpc2d import (  # noqa: F401
     Transcript, LcEncoding, LigeroEncoding, RsEncoding, SdigEncoding, LcCommit, LcEvalProof, LcColumn,
     collapse_columns, merkle_tree, hash_columns, verify_column_path, verify_column_value,
     n_degree_tests, log2, limbs, num_bits, set_device, device_count, field_random,
-    prof_enable, prof_reset, prof_stats,
+    prof_enable, prof_reset, prof_stats, selftest_pool_ordering,
 )

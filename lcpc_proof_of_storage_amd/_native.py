@@ -191,6 +191,7 @@ SIGNATURES = {
     "lcpc_prof_reset": (None, []),
     "lcpc_prof_get": (i32, [C.c_char_p, C.POINTER(C.c_double), u64p]),
     "lcpc_prof_names": (sz, [C.c_char_p, sz]),
+    "lcpc_selftest_pool_ordering": (i32, [i32, C.c_uint32, u64p, u64p, u64p]),
 }
 
 

@@ -131,6 +131,15 @@ def prof_stats() -> dict:
     return out
 
 
+def selftest_pool_ordering(rounds: int = 8, spin_us: int = 300) -> dict:
+    """On-device check of the stream-ordered buffer pool (lcpc_selftest_pool_ordering):
+    {"violations": words clobbered across a fence (must be 0), "control_violations": the same
+    without the fence, "reused": takes that returned the released block}."""
+    v, cv, r = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    _raise(N.load().lcpc_selftest_pool_ordering(rounds, spin_us, C.byref(v), C.byref(cv), C.byref(r)))
+    return {"violations": v.value, "control_violations": cv.value, "reused": r.value}
+
+
 def set_device(device: int):
     _raise(N.load().lcpc_set_device(device), DeviceError)
 
