@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void k_fill(uint32_t *__restrict__ p, size_t n
     p[i] = v;
 }
 
-constexpr size_t WORDS = (1 << 18) + 37;  // an odd block size no library buffer shares
+constexpr size_t WORDS = (1 << 18) + 37;
 constexpr unsigned BLOCKS = 1024;
 
 // one round: the block is allocated on `a`, the writer runs on `w` (a itself, or a second stream
@@ -81,6 +81,11 @@ extern "C" lcpc_status lcpc_selftest_pool_ordering(int rounds, uint32_t spin_us,
   if (!dev) return st;
   *violations = *control_violations = *reused = 0;
   const uint64_t ticks = (uint64_t)spin_us * 100;  // wall_clock64 runs at 100 MHz on gfx950
+  // blocks of the test's size that earlier calls left cached are held aside for the run (a
+  // host-ordered take), so that every take below can only return the block just released
+  const size_t rb = Device::round_bytes(WORDS * 4);
+  std::vector<void *> held;
+  while (void *q = dev->blocks.take(rb, hipStream_t{})) held.push_back(q);
   Lease la(dev, POOL_BULK);
   const hipStream_t a = la.s;
   hipStream_t w = dev->acquire_stream(POOL_HIGH);
@@ -97,5 +102,6 @@ extern "C" lcpc_status lcpc_selftest_pool_ordering(int rounds, uint32_t spin_us,
   (void)hipStreamSynchronize(b);
   dev->release_stream(w, POOL_HIGH);
   dev->release_stream(b, POOL_PROVER);
+  for (void *q : held) dev->blocks.put(q, rb, nullptr, 0);
   return rc;
 }
