@@ -1346,6 +1346,18 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
         out["kernels_timed_region"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "total_ms": v[0]}
                                        for k, v in stats.items()}
     out.update(roofline_objects(wl, iso, stats, args))
+    if args.code in ("encode", "sdig-encode") and out.get("roofline"):
+        # each timed step of these lines is exactly one encode call (inputs resident, no other
+        # kernels): the rate over the timed region, with P calls in flight, is the steady state
+        # the serial launches above cannot reach when one call holds less than a wave of tiles
+        st_ms = 1e3 * elapsed / args.steps
+        for key, num in (("roofline", wl.algo_bytes / 1e9), ("roofline_valu", (wl.mul_count or 0) / 1e9),
+                         ("roofline_gather", getattr(wl, "gather_bytes", 0) / 1e9)):
+            o = out.get(key)
+            if o and num and o.get("peak"):
+                ach = num / (st_ms * 1e-3)
+                o["steady_state"] = {"achieved": ach, "frac": ach / o["peak"], "ms_per_step": st_ms,
+                                     "what": f"per-step work / the timed region's ms_per_step ({P} calls in flight)"}
 
     gev = None
     if getattr(wl, "verify_bench", None) and args.verify_reps > 0:
