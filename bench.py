@@ -1039,9 +1039,10 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
     else:
         ev = None
 
-    # CPU baseline and parity: the oracle (C restatement) on the same workload, on rank 0 at EVERY
-    # N (after the timed region), so that an N > 1 line carries its own proof of a right answer:
-    # every timed step's root, the kept warm-up proof and the verifier's value against the oracle's
+    # Parity: the oracle (C restatement) on the same workload, on rank 0 at EVERY N (after the timed
+    # region), so that an N > 1 line carries its own proof of a right answer: every timed step's
+    # root, the kept warm-up proof and the verifier's value against the oracle's.  The timed CPU
+    # baseline is the N = 1 line's (--cpu-baseline on forces it at every N)
     want_cpu = args.cpu_baseline in ("on", "auto")
     if rank == 0 and want_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -1060,10 +1061,15 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
         cores, basis = available_cores()
         if args.cpu_threads:
             cores, basis = args.cpu_threads, "--cpu-threads"
-        med, runs, oroot, sample = time_cpu_baseline(Workload(cpu_baseline=cpu_once), O, cores, args.cpu_reps)
-        out["cpu_baseline"] = {"value": n / med, "unit": "field-elements/s", "cores": cores, "kind": "port",
-                               "sample": f"{sample}: median of {len(runs)} runs after a warm-up on {cores} threads "
-                                         f"({', '.join(f'{r:.3f}' for r in runs)} s)", "cores_basis": basis}
+        if world == 1 or args.cpu_baseline == "on":
+            med, runs, oroot, sample = time_cpu_baseline(Workload(cpu_baseline=cpu_once), O, cores, args.cpu_reps)
+            out["cpu_baseline"] = {"value": n / med, "unit": "field-elements/s", "cores": cores, "kind": "port",
+                                   "sample": f"{sample}: median of {len(runs)} runs after a warm-up on {cores} "
+                                             f"threads ({', '.join(f'{r:.3f}' for r in runs)} s)",
+                                   "cores_basis": basis}
+        else:  # N > 1: the oracle runs once, as the checker only (the CPU baseline is the N = 1 line's)
+            O.lib().of_set_threads(cores)
+            _, oroot, _ = cpu_once(O)
         out["parity_root_vs_oracle"] = oroot == roots[0]
         out["parity_steps_vs_oracle"] = {"steps": len(troots) + len(roots),
                                          "equal": sum(r == oroot for r in list(troots) + list(roots)),
@@ -1196,17 +1202,18 @@ def run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share):
         o_enc = O.Encoding.ligero(0, np_, nc)
         cores, basis = available_cores()
         O.lib().of_set_threads(cores)
-        # timed sample: the first 1/16 of the file, scaled to the whole
-        sample = host[: n_bytes // 16]
-        el = O.pos_bytes_to_field(sample.tobytes())
-        t1 = time.perf_counter()
-        oc = O.Commit(o_enc, el)
-        O.collapse(0, oc.comm, O.pos_side_vectors(0, x.reshape(-1), oc.n_rows, nc)[0], oc.n_rows, nc)
-        dt = (time.perf_counter() - t1) * 16
-        del oc
-        out["cpu_baseline"] = {"value": n_el / dt, "unit": "field-elements/s", "cores": cores, "kind": "port",
-                               "sample": f"commit + u^T Enc(M) of the first 1/16 of the file, scaled to the whole "
-                                         f"file ({dt / 16:.2f} s)", "cores_basis": basis}
+        if world == 1 or args.cpu_baseline == "on":  # (N > 1: the N = 1 line's baseline)
+            # timed sample: the first 1/16 of the file, scaled to the whole
+            sample = host[: n_bytes // 16]
+            el = O.pos_bytes_to_field(sample.tobytes())
+            t1 = time.perf_counter()
+            oc = O.Commit(o_enc, el)
+            O.collapse(0, oc.comm, O.pos_side_vectors(0, x.reshape(-1), oc.n_rows, nc)[0], oc.n_rows, nc)
+            dt = (time.perf_counter() - t1) * 16
+            del oc
+            out["cpu_baseline"] = {"value": n_el / dt, "unit": "field-elements/s", "cores": cores, "kind": "port",
+                                   "sample": f"commit + u^T Enc(M) of the first 1/16 of the file, scaled to the "
+                                             f"whole file ({dt / 16:.2f} s)", "cores_basis": basis}
         out.update(pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, root, ev, opened))
         out["parity_ok"] = bool(out["steps_agree"] and out["parity_root_vs_oracle"]
                                 and out["parity_eval_vs_oracle"] and out["parity_cols_vs_oracle"])
@@ -1367,7 +1374,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     if root is not None:
         out["root"] = root.hex()
     out["steps_agree"] = steps_agree
-    want_cpu = args.cpu_baseline in ("on", "auto")  # rank 0's polynomial, at every N
+    want_cpu = args.cpu_baseline in ("on", "auto")  # rank 0's polynomial checked at every N
     if rank == 0 and want_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ffi as O  # checker / CPU baseline only
@@ -1377,10 +1384,15 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
         elif args.cpu_threads:
             cores, basis = args.cpu_threads, "--cpu-threads"
         reps = args.cpu_reps if getattr(wl, "cpu_reps_ok", True) else 1
-        med, runs, oroot, sample = time_cpu_baseline(wl, O, cores, reps)
-        out["cpu_baseline"] = {"value": wl.units / med, "unit": wl.unit, "cores": cores, "kind": "port",
-                               "sample": f"{sample}: median of {len(runs)} runs after a warm-up on {cores} threads "
-                                         f"({', '.join(f'{r:.3f}' for r in runs)} s)", "cores_basis": basis}
+        if world == 1 or args.cpu_baseline == "on":
+            med, runs, oroot, sample = time_cpu_baseline(wl, O, cores, reps)
+            out["cpu_baseline"] = {"value": wl.units / med, "unit": wl.unit, "cores": cores, "kind": "port",
+                                   "sample": f"{sample}: median of {len(runs)} runs after a warm-up on {cores} "
+                                             f"threads ({', '.join(f'{r:.3f}' for r in runs)} s)",
+                                   "cores_basis": basis}
+        else:  # N > 1: the oracle runs once, as the checker only (the CPU baseline is the N = 1 line's)
+            O.lib().of_set_threads(cores)
+            _, oroot, _ = wl.cpu_baseline(O)
         if getattr(wl, "root_is_parity", False):
             out["parity_vs_oracle"] = bool(oroot)
         elif oroot is not None:

@@ -84,14 +84,15 @@ def _bench_ranks(world, extra_env, *args, timeout=280):
 
 def _check_self_checking(d, world):
     """an N > 1 line carries its own evidence of a right answer: the oracle's root against every
-    warm-up and timed step, the kept proof, the verifier's value and a cpu_baseline"""
+    warm-up and timed step, the kept proof and the verifier's value (the timed cpu_baseline is the
+    N = 1 line's: at N > 1 the oracle runs once, as the checker)"""
     assert d["n_gpus"] == world and d["world_formed"] == world and d["scaling"] == "strong"
     assert d["parity_root_vs_oracle"] is True and d["parity_proof_vs_oracle"] is True
     ps = d["parity_steps_vs_oracle"]
     assert ps["steps"] == d["steps"] + d["warmup"] and ps["equal"] == ps["steps"]
     assert d["steps_agree"] is True and d["parity_ok"] is True
     assert d["verify"]["parity_vs_oracle"] is True
-    _check_cpu(d)
+    assert "cpu_baseline" not in d
 
 
 @pytest.mark.timeout(300)
@@ -106,7 +107,7 @@ def test_bench_sharded_two_ranks_one_gpu(gpu):
 @pytest.mark.timeout(300)
 def test_bench_sharded_two_ranks_rccl_one_gpu(gpu):
     """the same line through the library's RCCL communicator (per-rank NCCL_HOSTID: RCCL's socket
-    transport over loopback), with the default cpu_baseline setting: every N > 1 line self-checks"""
+    transport over loopback), with the default cpu_baseline setting: every N > 1 line self-checks against the oracle"""
     d = _bench_ranks(2, {"LCPC_BENCH_RCCL_SAME_GPU": "1"}, "--steps", "4", "--warmup", "2", "--log-len", "16",
                      "--verify-reps", "1")
     _check_self_checking(d, 2)
