@@ -86,15 +86,25 @@ class OrderedPool {
     }
   }
 
-  // Every cached block (for trimming or teardown): the caller has drained the device.
+  // Every cached block (for trimming or teardown), each freed only after its fence has completed
+  // on the host: a block released by another thread after the caller's device drain may still
+  // have work queued on it.
   template <class FreeFn>
   void drain(FreeFn &&free_block) {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto &kv : free_) {
-      for (int i = 0; i < kv.second.n; i++) recycle(kv.second.ev[i]);
+      for (int i = 0; i < kv.second.n; i++) {
+        if (!b_.done(kv.second.ev[i])) {
+          b_.sync(kv.second.ev[i]);
+          syncs_++;
+        }
+        recycle(kv.second.ev[i]);
+      }
       free_block(kv.second.p);
     }
     free_.clear();
+    for (Event e : retiring_)
+      if (!b_.done(e)) b_.sync(e);
     reap(true);
   }
 

@@ -212,6 +212,19 @@ static void basic_cases() {
   std::vector<void *> freed;
   pool.drain([&](void *p) { freed.push_back(p); });
   assert(pool.cached() == 0);
+
+  // trimming with a fence still pending (a block another thread released after the caller's
+  // device drain): the block is freed only once the work queued on it has completed
+  sim.work(A, 5);
+  sim.work(C, 5);
+  int ss4[] = {A, C};
+  pool.put((void *)0x7000, 256, ss4, 2);
+  const size_t h1 = pool.host_syncs();
+  pool.drain([&](void *p) {
+    assert(p == (void *)0x7000);
+    assert(sim.done_[A] == (long)sim.q[A].size() && sim.done_[C] == (long)sim.q[C].size());
+  });
+  assert(pool.host_syncs() >= h1 + 1 && pool.cached() == 0);
 }
 
 // random interleavings: 4 streams, 6 blocks, owners hand blocks on through the pool while the
