@@ -111,6 +111,11 @@ def parse():
                          "finishing together at its end")
     ap.add_argument("--workers", type=int, default=0,
                     help="replicas: host worker threads (steps in flight) exactly; 0: --pipeline's rule")
+    ap.add_argument("--prove-order", choices=("interleaved", "commits-first"), default="interleaved",
+                    help="replicas (ligero / sdig), timed steps: a proof starts right after its commitment "
+                         "(interleaved), or waits until no commitment is queued or running and no step is "
+                         "left to start (or every worker waits), so the commitments run back to back and "
+                         "the proofs' kernels fill the GPU while the last transcripts run")
     ap.add_argument("--timeline", default=None,
                     help="replicas (ligero / sdig): write every timed step's gate / commit / prove "
                          "times (s, from the start of the timed region) to this JSON file")
@@ -277,17 +282,27 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
 
     timeline = []  # (slot, t_gate, t_commit_start, t_commit_end, t_prove_end) with --timeline
 
+    hooks = {}  # the runner's scheduling hooks (--prove-order)
+
     def step(slot):
         t_a = time.perf_counter()
-        if gate is not None:
-            with gate:
-                t_b = time.perf_counter()
+        if "commit_begin" in hooks:
+            hooks["commit_begin"]()
+        try:
+            if gate is not None:
+                with gate:
+                    t_b = time.perf_counter()
+                    c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+            else:
+                t_b = t_a
                 c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
-        else:
-            t_b = t_a
-            c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+        finally:
+            if "commit_end" in hooks:
+                hooks["commit_end"]()
         t_c = time.perf_counter()
         root = c.get_root()
+        if "before_prove" in hooks:
+            hooks["before_prove"]()
         tr = L.Transcript(b"test transcript")
         tr.append_message(b"polycommit", root)
         tr.append_message(b"ncols", nco.to_bytes(8, "big"))
@@ -365,7 +380,8 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
                                    f"BLAKE3 Merkle",
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                 "n_col_opens": nco, "n_degree_tests": ndt},
-        step=step, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify, latency=latency,
+        step=step, hooks=hooks, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify,
+        latency=latency,
         prepare=lambda: enc.prepare_thread(n_rows), reserve=lambda count: enc.reserve(n, count),
         timeline=timeline,
         enc_kernels=("transpose", "sdig_encode") if sdig else ("ntt_pass_a", "ntt_pass_b", "ntt_small"),
@@ -1263,6 +1279,33 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     roots, errors = [], []
     ready = threading.Barrier(n_workers + 1)
     start = threading.Event()
+    # --prove-order commits-first (timed steps only): a proof waits while a commitment is queued
+    # or running, until no step is left to start -- or every live worker is waiting, so that a
+    # run with fewer workers than steps cannot stall
+    sched = threading.Condition()
+    st = {"committing": 0, "waiting": 0, "live": n_workers, "on": False}
+    if args.prove_order == "commits-first" and getattr(wl, "hooks", None) is not None:
+        def commit_begin():
+            with sched:
+                st["committing"] += 1
+
+        def commit_end():
+            with sched:
+                st["committing"] -= 1
+                sched.notify_all()
+
+        def before_prove():
+            with sched:
+                if not st["on"]:
+                    return
+                st["waiting"] += 1
+                sched.notify_all()
+                sched.wait_for(lambda: errors or (st["committing"] == 0 and todo[0] <= 0)
+                               or st["waiting"] >= st["live"])
+                st["waiting"] -= 1
+                sched.notify_all()
+
+        wl.hooks.update(commit_begin=commit_begin, commit_end=commit_end, before_prove=before_prove)
 
     def worker(slot):
         try:
@@ -1278,16 +1321,21 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
             errors.append(e)
         ready.wait()
         start.wait()
-        while not errors:
-            with lock:
-                if todo[0] <= 0:
+        try:
+            while not errors:
+                with lock:
+                    if todo[0] <= 0:
+                        return
+                    todo[0] -= 1
+                try:
+                    roots.append(wl.step(slot))
+                except Exception as e:
+                    errors.append(e)
                     return
-                todo[0] -= 1
-            try:
-                roots.append(wl.step(slot))
-            except Exception as e:
-                errors.append(e)
-                return
+        finally:
+            with sched:
+                st["live"] -= 1
+                sched.notify_all()
 
     if getattr(wl, "reserve", None):
         wl.reserve(n_workers + 1)  # device pool blocks and streams of every concurrent step (not steps)
@@ -1300,12 +1348,14 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     L.prof_enable(prof and args.prof_timed)
     L.prof_reset()
     barrier()
+    st["on"] = True
     t0 = time.perf_counter()
     t0_mono_ns = time.clock_gettime_ns(time.CLOCK_MONOTONIC)  # (--timeline: aligns with a rocprofv3 trace)
     c0, th0 = os.times(), cgroup_throttle()
     start.set()
     for w in workers:
         w.join()
+    st["on"] = False
     if errors:
         raise errors[0]
     root = roots[-1] if roots else None
@@ -1338,7 +1388,9 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     value = job_throughput(wl.units, args.steps, world if scaling == "weak" else 1, elapsed)
     out = {
         "metric": wl.metric, "value": value, "unit": wl.unit, "n_gpus": world, "steps": args.steps,
-        "warmup": warmup_done, "ms_per_step": 1e3 * elapsed / args.steps, "pipeline": P, "higher_is_better": True,
+        "warmup": warmup_done, "ms_per_step": 1e3 * elapsed / args.steps, "pipeline": P,
+        **({"prove_order": args.prove_order} if getattr(wl, "hooks", None) is not None else {}),
+        "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": wl.dtype, "data": wl.data,
         "config": dict(wl.config, parallelism=f"replicas x{world} (independent commitments per GPU, {P} in flight, "
                                               f"{args.stream_mode} streams)"),
