@@ -28,6 +28,7 @@ events on the launching stream, on serial launches after the timed region) and a
 N = 1: warm-up + median of 5, which doubles as the bit-exactness check of the root).
 """
 import argparse
+import collections
 import glob
 import json
 import os
@@ -111,6 +112,9 @@ def parse():
                          "finishing together at its end")
     ap.add_argument("--workers", type=int, default=0,
                     help="replicas: host worker threads (steps in flight) exactly; 0: --pipeline's rule")
+    ap.add_argument("--prove-defer", type=int, default=0,
+                    help="replicas (ligero / sdig), timed steps: up to this many finished commitments' proofs "
+                         "wait (first in, first out) while commitments are queued or running (0: none)")
     ap.add_argument("--prove-order", choices=("interleaved", "commits-first"), default="interleaved",
                     help="replicas (ligero / sdig), timed steps: a proof starts right after its commitment "
                          "(interleaved), or waits until no commitment is queued or running and no step is "
@@ -1279,12 +1283,24 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     roots, errors = [], []
     ready = threading.Barrier(n_workers + 1)
     start = threading.Event()
-    # --prove-order commits-first (timed steps only): a proof waits while a commitment is queued
-    # or running, until no step is left to start -- or every live worker is waiting, so that a
-    # run with fewer workers than steps cannot stall
+    # --prove-order commits-first / --prove-defer M (timed steps only): a finished commitment's
+    # proof joins a FIFO and waits while commitments are queued or running; the oldest waiter is
+    # released whenever more than M wait (commits-first: no bound), and all of them once no
+    # commitment is running and no step is left to start -- or every live worker waits, so a run
+    # with fewer workers than steps cannot stall
     sched = threading.Condition()
-    st = {"committing": 0, "waiting": 0, "live": n_workers, "on": False}
-    if args.prove_order == "commits-first" and getattr(wl, "hooks", None) is not None:
+    st = {"committing": 0, "live": n_workers, "on": False}
+    waiters = collections.deque()
+    bound = args.steps if args.prove_order == "commits-first" else args.prove_defer
+    if bound > 0 and getattr(wl, "hooks", None) is not None:
+        def release():  # (under sched)
+            if (st["committing"] == 0 and todo[0] <= 0) or len(waiters) >= st["live"]:
+                while waiters:
+                    waiters.popleft()["go"] = True
+            while len(waiters) > bound:
+                waiters.popleft()["go"] = True
+            sched.notify_all()
+
         def commit_begin():
             with sched:
                 st["committing"] += 1
@@ -1292,20 +1308,19 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
         def commit_end():
             with sched:
                 st["committing"] -= 1
-                sched.notify_all()
+                release()
 
         def before_prove():
             with sched:
                 if not st["on"]:
                     return
-                st["waiting"] += 1
-                sched.notify_all()
-                sched.wait_for(lambda: errors or (st["committing"] == 0 and todo[0] <= 0)
-                               or st["waiting"] >= st["live"])
-                st["waiting"] -= 1
-                sched.notify_all()
+                me = {"go": False}
+                waiters.append(me)
+                release()
+                sched.wait_for(lambda: me["go"] or errors)
 
         wl.hooks.update(commit_begin=commit_begin, commit_end=commit_end, before_prove=before_prove)
+        st["release"] = release
 
     def worker(slot):
         try:
@@ -1335,6 +1350,8 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
         finally:
             with sched:
                 st["live"] -= 1
+                if "release" in st:
+                    st["release"]()
                 sched.notify_all()
 
     if getattr(wl, "reserve", None):
@@ -1389,7 +1406,8 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     out = {
         "metric": wl.metric, "value": value, "unit": wl.unit, "n_gpus": world, "steps": args.steps,
         "warmup": warmup_done, "ms_per_step": 1e3 * elapsed / args.steps, "pipeline": P,
-        **({"prove_order": args.prove_order} if getattr(wl, "hooks", None) is not None else {}),
+        **({"prove_order": args.prove_order, "prove_defer": args.prove_defer}
+           if getattr(wl, "hooks", None) is not None else {}),
         "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": wl.dtype, "data": wl.data,
         "config": dict(wl.config, parallelism=f"replicas x{world} (independent commitments per GPU, {P} in flight, "
