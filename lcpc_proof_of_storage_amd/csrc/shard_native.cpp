@@ -1816,6 +1816,19 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
     if (x) dev->release_stream(x, shard_all_high());
   for (hipStream_t x : hi)
     if (x) dev->release_stream(x, shard_prove_high());
+  // the page-locked blocks of the proofs this rank assembles (host_proof: p_random, p_eval,
+  // columns, paths), one set per polynomial it is the transcript rank of: every proof of a call
+  // is alive until the call returns, so a call at a new depth would otherwise pin them inside it
+  if (!st) {
+    const size_t own = me < (int)n_polys ? (n_polys - (size_t)me + G - 1) / G : 0;
+    const size_t ndt = e->n_degree_tests;
+    std::vector<void *> proof_pins;
+    for (size_t k = 0; k < own; k++)
+      for (size_t b : {ndt * np * wb, np * wb, nco * n_rows * wb, nco * pl * 32})
+        if (b >= PinnedHeap::MIN)
+          if (void *p = g_pinned_heap.get(b)) proof_pins.push_back(p);
+    for (void *p : proof_pins) g_pinned_heap.put(p);
+  }
   return st;
 }
 
