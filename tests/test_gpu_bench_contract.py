@@ -70,6 +70,16 @@ def test_bench_ligero_default_small(gpu):
     assert d["parity_ok"] is True and d["sharded_n1"]["root_equals_replicas"] is True
 
 
+@pytest.mark.parametrize("order", [("--prove-defer", "2"), ("--prove-order", "commits-first")])
+def test_bench_ligero_prove_scheduling_small(gpu, order):
+    """the A/B scheduling options (proofs deferred while commitments run) finish with every
+    step's root right, including with fewer workers than steps (the all-waiting release)"""
+    d = _bench("--steps", "8", "--warmup", "2", "--log-len", "16", "--workers", "3", "--verify-reps", "0",
+               "--sharded-n1", "0", *order)
+    _check_common(d, 8)
+    assert d["steps_agree"] is True and d["parity_root_vs_oracle"] is True and d["parity_ok"] is True
+
+
 def _bench_ranks(world, extra_env, *args, timeout=280):
     env = dict(os.environ, LCPC_BENCH_BACKEND="gloo", LCPC_BENCH_SHARE_GPU="1", **extra_env)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
