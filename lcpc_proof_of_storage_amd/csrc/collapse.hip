@@ -179,16 +179,6 @@ bool use_mfma(int fid, int n_tensors) {
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// (A/B) LCPC_COLLAPSE_WAVES=1: one-wave blocks (4.3 KiB of LDS instead of 17 KiB), which fit
-// beside four encode blocks on a CU (4 x 38 KiB of its 160 KiB)
-int collapse_waves() {
-  static const int v = [] {
-    const char *e = getenv("LCPC_COLLAPSE_WAVES");
-    return e && e[0] == '1' ? 1 : 4;
-  }();
-  return v;
-}
-
 template <int T>
 hipError_t collapse_mfma_t(const uint32_t *coeffs, size_t n_rows, size_t n_per_row, const uint32_t *tensors,
                            uint32_t *out, void *scratch, hipStream_t s) {
@@ -201,15 +191,11 @@ hipError_t collapse_mfma_t(const uint32_t *coeffs, size_t n_rows, size_t n_per_r
   prof::Scope ps("collapse_partial", s);
   hipLaunchKernelGGL((cmfma::k_tensor_digits<F>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, tensors,
                      n_rows, T, hdig);
-  if (collapse_waves() == 1) {
-    dim3 grid((unsigned)((n_per_row + cmfma::COLS_PER_WAVE - 1) / cmfma::COLS_PER_WAVE), (unsigned)splits);
-    hipLaunchKernelGGL((cmfma::k_collapse_mfma<F, T, 1>), grid, dim3(64), 0, s, coeffs, n_rows, n_per_row,
-                       (const uint8_t *)hdig, partial, rps);
-  } else {
-    dim3 grid((unsigned)((n_per_row + 4 * cmfma::COLS_PER_WAVE - 1) / (4 * cmfma::COLS_PER_WAVE)), (unsigned)splits);
-    hipLaunchKernelGGL((cmfma::k_collapse_mfma<F, T>), grid, dim3(256), 0, s, coeffs, n_rows, n_per_row,
-                       (const uint8_t *)hdig, partial, rps);
-  }
+  // (one-wave blocks, whose 4.3 KiB of LDS fit beside four encode blocks on a CU, measured the
+  // same at K = 20: profiles/r05_k20_collapse_waves_ab.json)
+  dim3 grid((unsigned)((n_per_row + 4 * cmfma::COLS_PER_WAVE - 1) / (4 * cmfma::COLS_PER_WAVE)), (unsigned)splits);
+  hipLaunchKernelGGL((cmfma::k_collapse_mfma<F, T>), grid, dim3(256), 0, s, coeffs, n_rows, n_per_row,
+                     (const uint8_t *)hdig, partial, rps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   prof::Scope ps2("collapse_fold", s);

@@ -131,17 +131,17 @@ __device__ __forceinline__ Fe<F> recombine_redc(const int (&Y)[16]) {
   return redc_plus<F>(y, top);
 }
 
-// One wave = 64 columns x the split's rows; W waves per block on adjacent column ranges.
+// One wave = 64 columns x the split's rows; 4 waves per block on adjacent column ranges.
 // partial[(split T + t) n_per_row + c] = sum over the split's rows (a field element).
-template <class F, int T, int W = 4>
-__global__ __launch_bounds__(64 * W) void k_collapse_mfma(const uint32_t *__restrict__ coeffs, size_t n_rows,
-                                                          size_t n_per_row, const uint8_t *__restrict__ hdig,
-                                                          uint32_t *__restrict__ partial, size_t rows_per_split) {
+template <class F, int T>
+__global__ __launch_bounds__(256) void k_collapse_mfma(const uint32_t *__restrict__ coeffs, size_t n_rows,
+                                                       size_t n_per_row, const uint8_t *__restrict__ hdig,
+                                                       uint32_t *__restrict__ partial, size_t rows_per_split) {
   static_assert(F::N == 4, "Ft127 layout");
-  __shared__ int red[W][TILES][16][17];
+  __shared__ int red[4][TILES][16][17];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int grp = lane >> 4, n = lane & 15;
-  const size_t col0 = ((size_t)blockIdx.x * W + wave) * COLS_PER_WAVE;
+  const size_t col0 = ((size_t)blockIdx.x * 4 + wave) * COLS_PER_WAVE;
   const size_t split = blockIdx.y;
   const size_t r0 = split * rows_per_split;
   const size_t r1 = r0 + rows_per_split < n_rows ? r0 + rows_per_split : n_rows;
