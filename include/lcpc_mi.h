@@ -15,8 +15,9 @@
  *   - "host" pointers are caller-owned CPU memory; "device" pointers are HIP device memory
  *     of the current device; handles own their device buffers;
  *   - handles may be used from several threads: each call leases a HIP stream from a
- *     per-device pool (prove/verify from a high-priority pool), so independent calls, e.g.
- *     commitments of different objects, overlap on the device.
+ *     per-device pool (commits / encodes, prove, and the latency-side calls each have their own
+ *     pool; all streams run at one priority unless LCPC_PRIORITY_STREAMS=1), so independent
+ *     calls, e.g. commitments of different objects, overlap on the device.
  * No torch / HIP types appear in the signatures; `void *stream` is an optional hipStream_t.
  */
 #ifndef LCPC_MI_H
@@ -57,7 +58,9 @@ typedef enum lcpc_status {
   LCPC_ERR_DEVICE = 31,
   LCPC_ERR_OUT_OF_MEMORY = 32,
   LCPC_ERR_NO_DEVICE = 33,
-  LCPC_ERR_UNSUPPORTED = 34
+  LCPC_ERR_UNSUPPORTED = 34,
+  /* a caller-owned transcript's callback (lcpc_transcript_ops) returned non-zero */
+  LCPC_ERR_TRANSCRIPT = 35
 } lcpc_status;
 
 typedef enum lcpc_field {
@@ -141,7 +144,9 @@ size_t lcpc_encoding_n_cols(const lcpc_encoding *e);
  * dims; no effect on any other encoding): AUTO (default) = the one-pass row kernel for file images
  * (lcpc_pos_commit_bytes_device) and the four-step pair for element rows, the measured choices
  * (DESIGN.md §4); FOURSTEP / ONEPASS force one kernel for both.  Results are identical either way.
- * No reference counterpart (fffft has one FFT). */
+ * No reference counterpart (fffft has one FFT).  Configuration, not a runtime switch: call it
+ * right after creating the encoding, before any commit / encode / prove uses it (the setting is
+ * read without synchronisation by concurrent calls on the encoding). */
 #define LCPC_ROW_KERNEL_AUTO 0
 #define LCPC_ROW_KERNEL_FOURSTEP 1
 #define LCPC_ROW_KERNEL_ONEPASS 2
@@ -216,6 +221,35 @@ void lcpc_transcript_append_messages(lcpc_transcript *t, const uint8_t *label, s
                                      const uint8_t *msgs, size_t msg_len, size_t n_msgs);
 void lcpc_transcript_challenge_bytes(lcpc_transcript *t, const uint8_t *label, size_t label_len,
                                      uint8_t *dest, size_t dest_len);
+/* A caller-owned transcript.  The reference's prove / verify take the CALLER's transcript,
+ * `tr: &mut merlin::Transcript` (lcpc-2d/src/lib.rs:319-326, 547-556), and the caller keeps using
+ * it afterwards (proof-of-storage/src/tests.rs:223-233, main.rs:47-57; lcpc-2d/src/tests.rs:318-413
+ * continues one transcript over two proofs).  A handle made by lcpc_transcript_from_ops forwards
+ * every absorb and squeeze of prove / verify -- in the reference's order, the only state being the
+ * caller's -- to these functions:
+ *   append_message(ctx, label, msg)          = Transcript::append_message   (merlin 2.0)
+ *   append_messages(ctx, label, msgs, l, n)  = append_message(label, msgs + i * l) for i < n, the
+ *       prover's per-coefficient absorption (:1075-1077, 1096-1098) in one call; may be NULL
+ *       (then append_message is called n times)
+ *   challenge_bytes(ctx, label, dest, n)     = Transcript::challenge_bytes
+ * Labels are always one of "$l//DT", "$l//PR", "$l//PE", "$l//CO" (macros.rs:29-36), so a Rust
+ * shim can map them back to its &'static [u8] constants.  Callbacks run on the calling thread,
+ * inside the prove / verify call; 0 = success, anything else makes the call return
+ * LCPC_ERR_TRANSCRIPT (a sharded prove still completes its exchanges first).  The handle holds no
+ * transcript state of its own: lcpc_transcript_clone refuses it (NULL). */
+typedef struct lcpc_transcript_ops {
+  void *ctx;
+  int (*append_message)(void *ctx, const uint8_t *label, size_t label_len, const uint8_t *msg,
+                        size_t msg_len);
+  int (*append_messages)(void *ctx, const uint8_t *label, size_t label_len, const uint8_t *msgs,
+                         size_t msg_len, size_t n_msgs);
+  int (*challenge_bytes)(void *ctx, const uint8_t *label, size_t label_len, uint8_t *dest,
+                         size_t dest_len);
+} lcpc_transcript_ops;
+/* NULL (lcpc_last_error) if append_message or challenge_bytes is missing; ops is copied */
+lcpc_transcript *lcpc_transcript_from_ops(const lcpc_transcript_ops *ops);
+/* the first non-zero callback return seen by an ops transcript (0: none, or not an ops handle) */
+int lcpc_transcript_status(const lcpc_transcript *t);
 
 /* ------------------------------------------------------------------ LcEvalProof
  * LcCommit::prove (lcpc-2d/src/lib.rs:319-326 -> prove :1034-1123).  outer_tensor: host,
@@ -243,6 +277,14 @@ lcpc_status lcpc_proof_from_parts(lcpc_field f, size_t n_cols, size_t n_per_row,
 lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer_tensor, size_t outer_len,
                         const uint64_t *inner_tensor, size_t inner_len, const lcpc_proof *p,
                         const lcpc_encoding *e, lcpc_transcript *tr, uint64_t *eval_out);
+/* lcpc_prove / lcpc_verify driving the caller's transcript through ops for this one call: the
+ * drop-in for LcCommit::prove(&self, outer, enc, tr: &mut Transcript) (lib.rs:319-326) and
+ * LcEvalProof::verify(.., tr: &mut Transcript) (:547-556) -- see lcpc_transcript_ops above */
+lcpc_status lcpc_prove_ops(const lcpc_commit *c, const uint64_t *outer_tensor, size_t outer_len,
+                           const lcpc_encoding *e, const lcpc_transcript_ops *ops, lcpc_proof **out);
+lcpc_status lcpc_verify_ops(const uint8_t root[32], const uint64_t *outer_tensor, size_t outer_len,
+                            const uint64_t *inner_tensor, size_t inner_len, const lcpc_proof *p,
+                            const lcpc_encoding *e, const lcpc_transcript_ops *ops, uint64_t *eval_out);
 
 /* ------------------------------------------------------------------ free functions */
 /* collapse_columns (lcpc-2d/src/lib.rs:1126-1154) on host arrays: poly[c] += ... is computed

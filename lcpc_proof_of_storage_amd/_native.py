@@ -31,12 +31,22 @@ ALL_GATHER_FN = C.CFUNCTYPE(C.c_int, vp, vp, vp, sz)
 ALL_TO_ALL_V_FN = C.CFUNCTYPE(C.c_int, vp, vp, szp, vp, szp)
 BROADCAST_FN = C.CFUNCTYPE(C.c_int, vp, vp, sz, C.c_int)
 MAKE_TRANSCRIPT_FN = C.CFUNCTYPE(vp, vp, sz, u8p)
+# lcpc_transcript_ops: a caller-owned transcript's absorb / squeeze callbacks
+TR_APPEND_FN = C.CFUNCTYPE(C.c_int, vp, u8p, sz, u8p, sz)
+TR_APPEND_MANY_FN = C.CFUNCTYPE(C.c_int, vp, u8p, sz, u8p, sz, sz)
+TR_CHALLENGE_FN = C.CFUNCTYPE(C.c_int, vp, u8p, sz, u8p, sz)
 
 
 class P2pRecord(C.Structure):
     """lcpc_p2p_record (include/lcpc_mi.h)"""
     _fields_ = [("tick", C.c_uint32), ("pos", C.c_uint32), ("poly", C.c_uint32), ("stage", C.c_uint32),
                 ("is_send", C.c_int32), ("peer", C.c_int32), ("bytes", C.c_uint64)]
+
+
+class TranscriptOps(C.Structure):
+    """lcpc_transcript_ops (include/lcpc_mi.h)"""
+    _fields_ = [("ctx", vp), ("append_message", TR_APPEND_FN), ("append_messages", TR_APPEND_MANY_FN),
+                ("challenge_bytes", TR_CHALLENGE_FN)]
 
 
 class CommOps(C.Structure):
@@ -105,7 +115,11 @@ SIGNATURES = {
     "lcpc_transcript_append_message": (None, [vp, u8p, sz, u8p, sz]),
     "lcpc_transcript_append_messages": (None, [vp, u8p, sz, u8p, sz, sz]),
     "lcpc_transcript_challenge_bytes": (None, [vp, u8p, sz, u8p, sz]),
+    "lcpc_transcript_from_ops": (vp, [C.POINTER(TranscriptOps)]),
+    "lcpc_transcript_status": (i32, [vp]),
     "lcpc_prove": (i32, [vp, u64p, sz, vp, vp, C.POINTER(vp)]),
+    "lcpc_prove_ops": (i32, [vp, u64p, sz, vp, C.POINTER(TranscriptOps), C.POINTER(vp)]),
+    "lcpc_verify_ops": (i32, [u8p, u64p, sz, u64p, sz, vp, vp, C.POINTER(TranscriptOps), u64p]),
     "lcpc_proof_free": (None, [vp]),
     "lcpc_proof_n_cols": (sz, [vp]),
     "lcpc_proof_n_per_row": (sz, [vp]),

@@ -91,7 +91,9 @@ struct HipPoolBackend {
   void drain(Stream s) { (void)hipStreamSynchronize(s); }
 };
 
-enum { POOL_BULK = 0, POOL_HIGH = 1, POOL_PROVER = 2 };
+// The stream pools of a device (a scoped enum: a stray `true` / `false` no longer selects one).
+enum class StreamPool : int { Bulk = 0, High = 1, Prover = 2 };
+constexpr StreamPool POOL_BULK = StreamPool::Bulk, POOL_HIGH = StreamPool::High, POOL_PROVER = StreamPool::Prover;
 
 // A pool of HIP streams and a caching allocator per device.  Every API call leases its own
 // stream, so independent commitments run concurrently (their CPU-side Fiat-Shamir work
@@ -112,8 +114,7 @@ struct Device {
   lcpc_pool::OrderedPool<HipPoolBackend> blocks{pool_backend};
   std::map<void *, size_t> sizes;
 
-  // high-priority streams carry the prover's short latency-critical kernels (row
-  // combinations, conversions, gathers) ahead of other commitments' bulk encode work
+  // (all pools' streams run at one priority by default: see stream_priority below)
   hipStream_t shared_stream = nullptr;  // LCPC_STREAM_MODE=serial: every call on one stream
 
   static bool serial_mode() {
@@ -124,7 +125,7 @@ struct Device {
     return v;
   }
 
-  hipStream_t acquire_stream(int pool) {
+  hipStream_t acquire_stream(StreamPool pool) {
     if (serial_mode()) {
       std::lock_guard<std::mutex> lk(mu);
       if (!shared_stream) {
@@ -136,7 +137,7 @@ struct Device {
     }
     {
       std::lock_guard<std::mutex> lk(mu);
-      auto &idle = idle_streams[pool];
+      auto &idle = idle_streams[(int)pool];
       if (!idle.empty()) {
         hipStream_t s = idle.back();
         idle.pop_back();
@@ -167,10 +168,10 @@ struct Device {
     if (!priority_streams() || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return 0;
     return high ? hi : lo;
   }
-  void release_stream(hipStream_t s, int pool) {
+  void release_stream(hipStream_t s, StreamPool pool) {
     if (serial_mode()) return;
     std::lock_guard<std::mutex> lk(mu);
-    idle_streams[pool].push_back(s);
+    idle_streams[(int)pool].push_back(s);
   }
   static size_t round_bytes(size_t bytes) { return ((bytes ? bytes : 16) + 255) & ~(size_t)255; }
   // a block of at least `bytes`, ordered after every earlier use of it: on stream `s` when given
@@ -310,8 +311,8 @@ struct Lease {
   Device *d;
   hipStream_t s;
   hipStream_t prev;
-  int pool;
-  explicit Lease(Device *dev, int stream_pool = POOL_BULK) : d(dev), s(nullptr), prev(t_stream), pool(stream_pool) {
+  StreamPool pool;
+  explicit Lease(Device *dev, StreamPool stream_pool = POOL_BULK) : d(dev), s(nullptr), prev(t_stream), pool(stream_pool) {
     (void)hipSetDevice(dev->id);
     s = dev->acquire_stream(pool);
     t_stream = s;
@@ -577,9 +578,37 @@ struct lcpc_proof {
   pinned_vector<uint8_t> paths;
 };
 
+// A merlin::Transcript as prove / verify see it: the library's own restatement (t), or the
+// caller's transcript behind lcpc_transcript_ops (lcpc_transcript_from_ops), every absorb and
+// squeeze forwarded.  The reference threads the caller's `&mut Transcript` through prove / verify
+// (lcpc-2d/src/lib.rs:319-326, 547-556); ops let a caller that owns one keep it.
 struct lcpc_transcript {
   Transcript t;
+  lcpc_transcript_ops ops{};
+  bool external = false;
+  int cb_status = 0;  // first non-zero return of an ops callback (the call then fails)
   explicit lcpc_transcript(const uint8_t *l, size_t n) : t(l, n) {}
+  explicit lcpc_transcript(const lcpc_transcript_ops &o)
+      : t(reinterpret_cast<const uint8_t *>(""), 0), ops(o), external(true) {}
+  void append_message(const uint8_t *label, size_t ln, const uint8_t *msg, size_t mn) {
+    if (!external) return t.append_message(label, ln, msg, mn);
+    if (!cb_status) cb_status = ops.append_message(ops.ctx, label, ln, msg, mn);
+  }
+  // append_message(label, msgs + i * ml) for i < n: one callback when the caller batches
+  void append_messages(const uint8_t *label, size_t ln, const uint8_t *msgs, size_t ml, size_t n) {
+    if (!external) return t.append_messages(label, ln, msgs, ml, n);
+    if (cb_status) return;
+    if (ops.append_messages) {
+      cb_status = ops.append_messages(ops.ctx, label, ln, msgs, ml, n);
+      return;
+    }
+    for (size_t i = 0; i < n && !cb_status; i++) cb_status = ops.append_message(ops.ctx, label, ln, msgs + i * ml, ml);
+  }
+  void challenge_bytes(const uint8_t *label, size_t ln, uint8_t *dst, size_t n) {
+    if (!external) return t.challenge_bytes(label, ln, dst, n);
+    if (!cb_status) cb_status = ops.challenge_bytes(ops.ctx, label, ln, dst, n);
+    if (cb_status) std::memset(dst, 0, n);  // (the call fails; keep the bytes defined)
+  }
 };
 
 namespace lcpc_host {
@@ -734,7 +763,7 @@ inline lcpc_status to_repr_host(Device *dev, int fid, const uint32_t *d_elems, s
   return LCPC_OK;
 }
 
-inline void challenge_tensor(Transcript &tr, int fid, size_t n_rows, std::vector<uint64_t> &out) {
+inline void challenge_tensor(lcpc_transcript &tr, int fid, size_t n_rows, std::vector<uint64_t> &out) {
   // lcpc-2d/src/lib.rs:1056-1062 (prove) / :899-907 (verify)
   uint8_t key[32];
   tr.challenge_bytes(LABEL_DT, 6, key, 32);
@@ -744,7 +773,7 @@ inline void challenge_tensor(Transcript &tr, int fid, size_t n_rows, std::vector
   field_random(rng, fi.limbs, fi.num_bits, fi.p, out.data(), n_rows);
 }
 
-inline void challenge_columns(Transcript &tr, size_t n_cols, size_t nco, std::vector<uint64_t> &idx) {
+inline void challenge_columns(lcpc_transcript &tr, size_t n_cols, size_t nco, std::vector<uint64_t> &idx) {
   // lcpc-2d/src/lib.rs:1103-1110 (prove) / :932-941 (verify)
   uint8_t key[32];
   tr.challenge_bytes(LABEL_CO, 6, key, 32);
@@ -754,5 +783,12 @@ inline void challenge_columns(Transcript &tr, size_t n_cols, size_t nco, std::ve
 }
 
 inline Device *current_device(lcpc_status *st) { return get_device(g_device, st); }
+
+// a caller-owned transcript's callback failed during the call: its state is no longer the
+// reference's, so the proof / verdict is void
+inline lcpc_status transcript_status(const lcpc_transcript *tr) {
+  if (!tr || !tr->cb_status) return LCPC_OK;
+  return fail(LCPC_ERR_TRANSCRIPT, "a caller transcript callback failed (status " + std::to_string(tr->cb_status) + ")");
+}
 }  // namespace lcpc_host
 

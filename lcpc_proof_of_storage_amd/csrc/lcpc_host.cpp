@@ -640,19 +640,34 @@ lcpc_status lcpc_open_column(const lcpc_commit *c, size_t column, uint64_t *col_
 lcpc_transcript *lcpc_transcript_new(const uint8_t *label, size_t n) {
   return new lcpc_transcript(label, n);
 }
-lcpc_transcript *lcpc_transcript_clone(const lcpc_transcript *t) { return new lcpc_transcript(*t); }
+lcpc_transcript *lcpc_transcript_from_ops(const lcpc_transcript_ops *ops) {
+  if (!ops || !ops->append_message || !ops->challenge_bytes) {
+    fail(LCPC_ERR_INVALID_ARG, "transcript ops need append_message and challenge_bytes");
+    return nullptr;
+  }
+  return new lcpc_transcript(*ops);
+}
+int lcpc_transcript_status(const lcpc_transcript *t) { return t ? t->cb_status : 0; }
+lcpc_transcript *lcpc_transcript_clone(const lcpc_transcript *t) {
+  if (!t) return nullptr;
+  if (t->external) {  // the caller's state lives on its side of the boundary
+    fail(LCPC_ERR_UNSUPPORTED, "a caller-owned (ops) transcript cannot be cloned here; clone it on the caller's side");
+    return nullptr;
+  }
+  return new lcpc_transcript(*t);
+}
 void lcpc_transcript_free(lcpc_transcript *t) { delete t; }
 void lcpc_transcript_append_message(lcpc_transcript *t, const uint8_t *l, size_t ln,
                                     const uint8_t *m, size_t mn) {
-  t->t.append_message(l, ln, m, mn);
+  t->append_message(l, ln, m, mn);
 }
 void lcpc_transcript_append_messages(lcpc_transcript *t, const uint8_t *l, size_t ln, const uint8_t *msgs,
                                      size_t msg_len, size_t n_msgs) {
-  t->t.append_messages(l, ln, msgs, msg_len, n_msgs);
+  t->append_messages(l, ln, msgs, msg_len, n_msgs);
 }
 void lcpc_transcript_challenge_bytes(lcpc_transcript *t, const uint8_t *l, size_t ln, uint8_t *d,
                                      size_t n) {
-  t->t.challenge_bytes(l, ln, d, n);
+  t->challenge_bytes(l, ln, d, n);
 }
 
 // ---------------------------------------------------------------- prove
@@ -707,7 +722,8 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   for (size_t i = 0; i < ndt; i++) {
     {
       prof::HostScope hs("host_prove_round_issue");
-      challenge_tensor(tr->t, fid, nr, tensor);
+      challenge_tensor(*tr, fid, nr, tensor);
+      if ((st = transcript_status(tr))) return st;
       std::memcpy(h_tens, tensor.data(), nr * wb);
       HIP_TRY(h2d(dtens.p, h_tens, nr * wb, s));
       const int nt = eval_done ? 1 : 2;
@@ -731,8 +747,9 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
     }
     {
       prof::HostScope hs("host_prove_transcript");
-      tr->t.append_messages(LABEL_PR, 6, repr, wb, np);
+      tr->append_messages(LABEL_PR, 6, repr, wb, np);
     }
+    if ((st = transcript_status(tr))) return st;
   }
   const uint32_t *d_eval = dres.as<uint32_t>() + np * limbs * 2;  // second collapse output
   if (!eval_done) {
@@ -750,11 +767,12 @@ lcpc_status lcpc_prove(const lcpc_commit *c, const uint64_t *outer, size_t outer
   if (st) return st;
   {
     prof::HostScope hs("host_prove_transcript");
-    tr->t.append_messages(LABEL_PE, 6, repr, wb, np);
+    tr->append_messages(LABEL_PE, 6, repr, wb, np);
   }
 
   // columns (:1101-1115)
-  challenge_columns(tr->t, c->n_cols, nco, p->col_idx);
+  challenge_columns(*tr, c->n_cols, nco, p->col_idx);
+  if ((st = transcript_status(tr))) return st;
   p->cols.resize(nco * nr * limbs);
   p->paths.resize(nco * p->path_len * 32);
   uint8_t *h_cols = (uint8_t *)p->cols.data();
@@ -850,7 +868,7 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
   if (p->ndt != ndt) return fail(LCPC_VERIFIER_ENCODING_DIMS, "proof has a different number of degree tests");
   const int fid = e->fid, wb = field_bytes(fid), limbs = wb / 8;
   Device *dev = e->dev;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_HIGH);
   HIP_TRY(hipSetDevice(dev->id));
   hipStream_t s = lease.s;
 
@@ -863,7 +881,7 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
   const uint8_t *repr = nullptr;
   lcpc_status st;
   for (size_t i = 0; i < ndt; i++) {
-    challenge_tensor(tr->t, fid, nr, tensor);
+    challenge_tensor(*tr, fid, nr, tensor);
     HIP_TRY(hipMemcpyAsync(dtens.as<uint8_t>() + i * nr * wb, tensor.data(), nr * wb,
                            hipMemcpyHostToDevice, s));
     st = upload(dev, dvec, p->p_random.data() + i * np * limbs, np * wb);
@@ -872,15 +890,17 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
     if (st) return st;
     st = to_repr_host(dev, fid, dvec.as<uint32_t>(), np, &repr);
     if (st) return st;
-    tr->t.append_messages(LABEL_PR, 6, repr, wb, np);
+    tr->append_messages(LABEL_PR, 6, repr, wb, np);
+    if ((st = transcript_status(tr))) return st;
   }
   st = upload(dev, dvec, p->p_eval.data(), np * wb);
   if (st) return st;
   st = to_repr_host(dev, fid, dvec.as<uint32_t>(), np, &repr);
   if (st) return st;
-  tr->t.append_messages(LABEL_PE, 6, repr, wb, np);
+  tr->append_messages(LABEL_PE, 6, repr, wb, np);
   std::vector<uint64_t> idx;
-  challenge_columns(tr->t, nc, nco, idx);
+  challenge_columns(*tr, nc, nco, idx);
+  if ((st = transcript_status(tr))) return st;
   st = encode_rows_any(e, dvec.as<uint32_t>(), np, np, denc.as<uint32_t>() + ndt * nc * limbs * 2, nc, 1, s);
   if (st) return st;
 
@@ -923,6 +943,24 @@ lcpc_status lcpc_verify(const uint8_t root[32], const uint64_t *outer, size_t ou
   }
   if (eval_out) std::memcpy(eval_out, ev.data(), wb);
   return LCPC_OK;
+}
+
+// prove / verify over a caller-owned transcript for the length of one call (the reference's
+// `&mut Transcript` argument, lcpc-2d/src/lib.rs:319-326, 547-556)
+lcpc_status lcpc_prove_ops(const lcpc_commit *c, const uint64_t *outer, size_t outer_len, const lcpc_encoding *e,
+                           const lcpc_transcript_ops *ops, lcpc_proof **out) {
+  if (!ops || !ops->append_message || !ops->challenge_bytes)
+    return fail(LCPC_ERR_INVALID_ARG, "transcript ops need append_message and challenge_bytes");
+  lcpc_transcript tr(*ops);
+  return lcpc_prove(c, outer, outer_len, e, &tr, out);
+}
+lcpc_status lcpc_verify_ops(const uint8_t root[32], const uint64_t *outer, size_t outer_len, const uint64_t *inner,
+                            size_t inner_len, const lcpc_proof *p, const lcpc_encoding *e,
+                            const lcpc_transcript_ops *ops, uint64_t *eval_out) {
+  if (!ops || !ops->append_message || !ops->challenge_bytes)
+    return fail(LCPC_ERR_INVALID_ARG, "transcript ops need append_message and challenge_bytes");
+  lcpc_transcript tr(*ops);
+  return lcpc_verify(root, outer, outer_len, inner, inner_len, p, e, &tr, eval_out);
 }
 
 // ---------------------------------------------------------------- free functions
@@ -1315,7 +1353,7 @@ lcpc_status lcpc_pos_eval_encoded(const lcpc_commit *c, const uint64_t *left, si
   if (n_rows != c->n_rows) return fail(LCPC_ERR_INVALID_ARG, "left vector length != n_rows");
   if (c->col_major) return fail(LCPC_ERR_UNSUPPORTED, "row-major (Ligero) commitments only");
   Device *dev = c->dev;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_HIGH);
   HIP_TRY(hipSetDevice(dev->id));
   const int wb = field_bytes(c->fid);
   DBuf dt, dout, scratch;
@@ -1383,7 +1421,7 @@ lcpc_status lcpc_open_columns(const lcpc_commit *c, const uint64_t *idx, size_t 
     if (idx[k] >= c->n_cols) return fail(LCPC_PROVER_COLUMN_NUMBER, "ProverError::ColumnNumber");
   if (!n) return LCPC_OK;
   Device *dev = c->dev;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_HIGH);
   HIP_TRY(hipSetDevice(dev->id));
   const size_t path_len = log2_np2(c->n_cols);
   const int wb = field_bytes(c->fid);
@@ -1568,7 +1606,7 @@ lcpc_status lcpc_shard_collapse(const lcpc_shard *s, const uint64_t *tensors, si
   const int fid = s->e->fid, wb = field_bytes(fid);
   const size_t np = s->e->n_per_row;
   Device *dev = s->e->dev;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_HIGH);
   HIP_TRY(hipSetDevice(dev->id));
   DBuf dt, dout, scratch;
   lcpc_status st;
@@ -1594,7 +1632,7 @@ lcpc_status lcpc_shard_gather_columns(const lcpc_shard *s, const uint64_t *idx, 
   if (!n || !s->n_rows) return LCPC_OK;
   const int fid = s->e->fid, wb = field_bytes(fid);
   Device *dev = s->e->dev;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_HIGH);
   HIP_TRY(hipSetDevice(dev->id));
   DBuf didx, dcol;
   lcpc_status st;
@@ -1678,7 +1716,7 @@ lcpc_status lcpc_shard_collapse_device(const lcpc_shard *s, const void *d_tensor
   const int fid = s->e->fid, wb = field_bytes(fid);
   const size_t np = s->e->n_per_row;
   Device *dev = s->e->dev;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_HIGH);
   HIP_TRY(hipSetDevice(dev->id));
   if (s->n_rows == 0) {
     HIP_TRY(hipMemsetAsync(d_out, 0, n_tensors * np * wb, lease.s));
@@ -1700,7 +1738,7 @@ lcpc_status lcpc_shard_gather_columns_device(const lcpc_shard *s, const uint64_t
   if (!n || !s->n_rows) return LCPC_OK;
   const int fid = s->e->fid;
   Device *dev = s->e->dev;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_HIGH);
   HIP_TRY(hipSetDevice(dev->id));
   DBuf didx;
   lcpc_status st;
@@ -1736,18 +1774,18 @@ lcpc_status lcpc_challenge_tensor(lcpc_transcript *tr, lcpc_field f, size_t n, u
   // prove / verify degree-test tensor (lcpc-2d/src/lib.rs:1056-1062, 899-907)
   if (!tr || !valid_field(f) || (!out && n)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
   std::vector<uint64_t> t;
-  challenge_tensor(tr->t, f, n, t);
+  challenge_tensor(*tr, f, n, t);
   if (n) std::memcpy(out, t.data(), t.size() * 8);
-  return LCPC_OK;
+  return transcript_status(tr);
 }
 
 lcpc_status lcpc_challenge_columns(lcpc_transcript *tr, size_t n_cols, size_t n, uint64_t *out) {
   // column choice (lcpc-2d/src/lib.rs:1101-1110, 932-941)
   if (!tr || !n_cols || (!out && n)) return fail(LCPC_ERR_INVALID_ARG, "arguments");
   std::vector<uint64_t> idx;
-  challenge_columns(tr->t, n_cols, n, idx);
+  challenge_columns(*tr, n_cols, n, idx);
   if (n) std::memcpy(out, idx.data(), n * 8);
-  return LCPC_OK;
+  return transcript_status(tr);
 }
 
 lcpc_status lcpc_transcript_append_field_elems(lcpc_transcript *tr, const uint8_t *label, size_t ln,
@@ -1758,15 +1796,15 @@ lcpc_status lcpc_transcript_append_field_elems(lcpc_transcript *tr, const uint8_
   lcpc_status st;
   Device *dev = current_device(&st);
   if (!dev) return st;
-  Lease lease(dev, true);
+  Lease lease(dev, POOL_HIGH);
   HIP_TRY(hipSetDevice(dev->id));
   const int wb = field_bytes(f);
   DBuf de;
   if ((st = upload(dev, de, elems, n * wb))) return st;
   const uint8_t *repr = nullptr;
   if ((st = to_repr_host(dev, f, de.as<uint32_t>(), n, &repr))) return st;
-  tr->t.append_messages(label, ln, repr, wb, n);
-  return LCPC_OK;
+  tr->append_messages(label, ln, repr, wb, n);
+  return transcript_status(tr);
 }
 
 }  // extern "C"

@@ -64,6 +64,8 @@ class OrderedPool {
     if (!p) return;
     Entry e;
     e.p = p;
+    Stream to_drain[MAX_STREAMS];
+    int nd = 0;
     {
       std::lock_guard<std::mutex> lk(mu_);
       for (int i = 0; i < n && i < MAX_STREAMS; i++) {
@@ -75,15 +77,23 @@ class OrderedPool {
         if (ev == Event{} || !b_.record(ev, ss[i])) {
           // no event: order the release on the host instead (rare: event creation failed)
           if (ev != Event{}) b_.event_free(ev);
-          b_.drain(ss[i]);
-          syncs_++;
+          to_drain[nd++] = ss[i];
           continue;
         }
         e.st[e.n] = ss[i];
         e.ev[e.n++] = ev;
       }
-      free_.emplace(bytes, std::move(e));
+      if (!nd) {
+        free_.emplace(bytes, std::move(e));
+        return;
+      }
     }
+    // host waits outside the lock (other threads' take / put do not queue behind unrelated GPU
+    // work); the block joins the free list only once they are done
+    for (int i = 0; i < nd; i++) b_.drain(to_drain[i]);
+    std::lock_guard<std::mutex> lk(mu_);
+    syncs_ += nd;
+    free_.emplace(bytes, std::move(e));
   }
 
   // Every cached block (for trimming or teardown), each freed only after its fence has completed

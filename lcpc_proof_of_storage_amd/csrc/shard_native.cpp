@@ -459,10 +459,10 @@ bool shard_prio_streams() { return true; }
 // roots still arrive nearly in order
 constexpr size_t SHARD_BULK_STREAMS = 2;
 size_t shard_bulk_streams() { return SHARD_BULK_STREAMS; }
-// the pool a stream comes from (Device::acquire_stream): the prover's pool, whose priority equals
-// the bulk pool's unless LCPC_PRIORITY_STREAMS=1, for every stream of the driver
-bool shard_all_high() { return true; }
-bool shard_prove_high() { return true; }
+// the pool every stream of the sharded driver comes from (Device::acquire_stream): the
+// latency-side pool POOL_HIGH (verify, openings, this driver), apart from lcpc_prove's POOL_PROVER;
+// its priority equals the bulk pool's unless LCPC_PRIORITY_STREAMS=1
+constexpr StreamPool kShardPool = POOL_HIGH;
 
 struct ShardDeleter {
   void operator()(lcpc_sharded_commit *c) const {
@@ -485,8 +485,8 @@ struct ShardDeleter {
       if (cs) b->use(cs);
     }
     delete c;
-    if (s) d->release_stream(s, shard_all_high());
-    if (sp) d->release_stream(sp, shard_prove_high());
+    if (s) d->release_stream(s, kShardPool);
+    if (sp) d->release_stream(sp, kShardPool);
   }
 };
 using ShardPtr = std::unique_ptr<lcpc_sharded_commit, ShardDeleter>;
@@ -549,9 +549,9 @@ lcpc_status shard_init(const lcpc_encoding *e, lcpc_comm *comm, size_t n_rows, S
   shard_geom(c.get(), e->fid, e->n_per_row, e->n_cols, n_rows, comm->nranks, comm->rank, e->kind == KIND_SDIG);
   HIP_TRY(hipSetDevice(c->dev->id));
   c->own_s = bulk == nullptr;
-  c->s = bulk ? bulk : c->dev->acquire_stream(shard_all_high());
+  c->s = bulk ? bulk : c->dev->acquire_stream(kShardPool);
   if (!c->s) return fail(LCPC_ERR_DEVICE, "no HIP stream");
-  c->sp = shard_prio_streams() ? c->dev->acquire_stream(shard_prove_high()) : c->s;
+  c->sp = shard_prio_streams() ? c->dev->acquire_stream(kShardPool) : c->s;
   if (!c->sp) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   out = std::move(c);
   return ev_need(out.get(), 0, 2);  // (the commit's stages: chaining values, subtrees)
@@ -853,7 +853,7 @@ lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_r
 lcpc_status challenge_first(lcpc_sharded_commit *c) {
   if (c->ndt) {
     std::vector<uint64_t> t;
-    challenge_tensor(c->tr->t, c->fid, c->n_rows, t);
+    challenge_tensor(*c->tr, c->fid, c->n_rows, t);
     std::memcpy(c->h_t.p, t.data(), c->n_rows * c->wb);
   }
   return LCPC_OK;
@@ -957,19 +957,19 @@ lcpc_status host_absorb(lcpc_sharded_commit *c, size_t r) {
       std::memcpy(c->h_repr_eval.p, repr + np * wb, np * wb);
     }
     prof::HostScope hs("host_prove_transcript");
-    c->tr->t.append_messages(LABEL_PR, 6, repr, wb, np);
+    c->tr->append_messages(LABEL_PR, 6, repr, wb, np);
   }
   if (r + 1 < c->rounds) {
     std::vector<uint64_t> t;
-    challenge_tensor(c->tr->t, c->fid, c->n_rows, t);
+    challenge_tensor(*c->tr, c->fid, c->n_rows, t);
     std::memcpy(c->h_t.p, t.data(), c->n_rows * wb);
     return LCPC_OK;
   }
   {
     prof::HostScope hs("host_prove_transcript");
-    c->tr->t.append_messages(LABEL_PE, 6, c->h_repr_eval.p, wb, np);
+    c->tr->append_messages(LABEL_PE, 6, c->h_repr_eval.p, wb, np);
   }
-  challenge_columns(c->tr->t, c->nc, c->nco, c->col_idx);
+  challenge_columns(*c->tr, c->nc, c->nco, c->col_idx);
   std::memcpy(c->h_idx.p, c->col_idx.data(), c->nco * 8);
   return LCPC_OK;
 }
@@ -1042,6 +1042,12 @@ lcpc_status host_proof(lcpc_sharded_commit *c, lcpc_proof **out) {
   if (c->me != c->root_rank) {
     if (out) *out = nullptr;
     return LCPC_OK;
+  }
+  // a caller-owned transcript whose callback failed: every exchange still ran (no rank is left
+  // waiting), but the proof is void
+  if (lcpc_status st = transcript_status(c->tr)) {
+    if (out) *out = nullptr;
+    return st;
   }
   auto p = std::make_unique<lcpc_proof>();
   const size_t wb = c->wb, nco = c->nco, n_rows = c->n_rows;
@@ -1270,7 +1276,7 @@ static lcpc_status comm_common(lcpc_comm *c) {
   HIP_TRY(hipSetDevice(c->dev->id));
   // the comm stream at the priority of the driver's other streams (one priority unless
   // LCPC_PRIORITY_STREAMS=1 asks for the A/B split, Device::stream_priority)
-  HIP_TRY(hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, Device::stream_priority(shard_all_high())));
+  HIP_TRY(hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, Device::stream_priority(kShardPool != POOL_BULK)));
   c->shared->cs = c->cs;
   return LCPC_OK;
 }
@@ -1450,8 +1456,11 @@ lcpc_status lcpc_sharded_pos_request(lcpc_sharded_commit *c, const uint64_t *lef
   } else {
     HIP_TRY(hipMemsetAsync(part.p, 0, nc * wb, c->s));
   }
-  HIP_TRY(hipEventRecord(EV(c, EV_READY, kPosEvalStage), c->s));
+  // the gather's receive buffer is taken BEFORE the READY record: a reused pool block's fence wait
+  // is queued on c->s by the take, and the comm stream's wait on READY then orders RCCL's writes
+  // into `all` after it (taken after the record, the gather could race the block's last owner)
   if (am_root) HIP_TRY(salloc(c, all, (size_t)c->G * nc * wb));
+  HIP_TRY(hipEventRecord(EV(c, EV_READY, kPosEvalStage), c->s));
   if ((st = one_group(c, gather_to_root(c, part.as<uint8_t>(), all.as<uint8_t>(), root,
                                         std::vector<size_t>(c->G, nc * wb), kPosEvalStage),
                       kPosEvalStage, &wd, 0, "partial u^T Enc(M) gather")))
@@ -1556,8 +1565,8 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   const size_t n_bulk = shard_bulk_streams();
   hipStream_t bulks[2] = {nullptr, nullptr};
   for (size_t i = 0; i < n_bulk; i++)
-    if (!(bulks[i] = e->dev->acquire_stream(shard_all_high()))) {
-      if (i) e->dev->release_stream(bulks[0], shard_all_high());
+    if (!(bulks[i] = e->dev->acquire_stream(kShardPool))) {
+      if (i) e->dev->release_stream(bulks[0], kShardPool);
       return fail(LCPC_ERR_DEVICE, "no HIP stream");
     }
   struct BulkRelease {  // (destroyed after cs: returns the streams to the pool)
@@ -1565,7 +1574,7 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
     hipStream_t *s;
     ~BulkRelease() {
       for (int i = 0; i < 2; i++)
-        if (s[i]) d->release_stream(s[i], shard_all_high());
+        if (s[i]) d->release_stream(s[i], kShardPool);
     }
   } bulk_release{e->dev, bulks};
   std::vector<ShardPtr> cs(n_polys);
@@ -1810,12 +1819,12 @@ lcpc_status lcpc_sharded_reserve(const lcpc_encoding *e, size_t n_rows, lcpc_com
   // the streams lcpc_sharded_commit_prove_many acquires: the shared (bulk) encode streams, and a
   // prove stream per polynomial in flight
   std::vector<hipStream_t> lo, hi;
-  for (size_t i = 0; i < shard_bulk_streams(); i++) lo.push_back(dev->acquire_stream(shard_all_high()));
-  for (size_t k = 0; k < depth && shard_prio_streams(); k++) hi.push_back(dev->acquire_stream(shard_prove_high()));
+  for (size_t i = 0; i < shard_bulk_streams(); i++) lo.push_back(dev->acquire_stream(kShardPool));
+  for (size_t k = 0; k < depth && shard_prio_streams(); k++) hi.push_back(dev->acquire_stream(kShardPool));
   for (hipStream_t x : lo)
-    if (x) dev->release_stream(x, shard_all_high());
+    if (x) dev->release_stream(x, kShardPool);
   for (hipStream_t x : hi)
-    if (x) dev->release_stream(x, shard_prove_high());
+    if (x) dev->release_stream(x, kShardPool);
   // the page-locked blocks of the proofs this rank assembles (host_proof: p_random, p_eval,
   // columns, paths), one set per polynomial it is the transcript rank of: every proof of a call
   // is alive until the call returns, so a call at a new depth would otherwise pin them inside it

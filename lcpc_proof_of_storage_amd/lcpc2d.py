@@ -30,6 +30,7 @@ FIELD_NAMES = {FT63: "Ft63", FT127: "Ft127", FT191: "Ft191", FT255: "Ft255", FT2
 
 # status codes (include/lcpc_mi.h)
 PROVER = {1: "TooBig", 2: "Encode", 3: "Commit", 4: "ColumnNumber", 5: "OuterTensor"}
+TRANSCRIPT_CALLBACK = 35  # LCPC_ERR_TRANSCRIPT: a CallerTranscript callback failed
 VERIFIER = {10: "NumColOpens", 11: "ColumnPath", 12: "ColumnEval", 13: "ColumnDegree", 14: "OuterTensor",
             15: "InnerTensor", 16: "EncodingDims", 17: "Encode"}
 FFT = {20: "NotPowerOfTwo", 21: "TooBig", 22: "WrongSizePrecomp"}
@@ -197,6 +198,80 @@ class Transcript:
             N.load().lcpc_transcript_free(self._h)
         except Exception:
             pass
+
+
+class CallerTranscript:
+    """A transcript the CALLER owns, driven by prove / verify through lcpc_transcript_ops.
+
+    The reference's prove / verify mutate the caller's ``&mut merlin::Transcript``
+    (lcpc-2d/src/lib.rs:319-326, 547-556) and the caller goes on using it.  ``obj`` is any object
+    with ``append_message(label, msg)`` and ``challenge_bytes(label, n) -> bytes`` (merlin's
+    methods), optionally ``append_messages(label, msgs, msg_len)`` for the prover's batched
+    per-coefficient absorption; every absorb and squeeze of the call goes to it, in the
+    reference's order.  An exception raised inside a callback fails the call (LCPC_ERR_TRANSCRIPT)
+    and is re-raised from prove / verify."""
+
+    def __init__(self, obj):
+        self.obj = obj
+        self.error: Optional[BaseException] = None
+
+        def guard(fn):
+            def cb(*a):
+                if self.error is not None:
+                    return 1
+                try:
+                    fn(*a)
+                    return 0
+                except BaseException as e:  # noqa: BLE001 -- handed back to the caller after the C call
+                    self.error = e
+                    return 1
+            return cb
+
+        def am(ctx, lp, ln, mp, mn):
+            obj.append_message(C.string_at(lp, ln), C.string_at(mp, mn))
+
+        def ams(ctx, lp, ln, mp, ml, n):
+            label, data = C.string_at(lp, ln), C.string_at(mp, ml * n)
+            obj.append_messages(label, data, ml)
+
+        def ch(ctx, lp, ln, dp, n):
+            out = bytes(obj.challenge_bytes(C.string_at(lp, ln), n))
+            if len(out) != n:
+                raise ValueError(f"challenge_bytes returned {len(out)} bytes, {n} asked")
+            C.memmove(dp, out, n)
+
+        many = N.TR_APPEND_MANY_FN(guard(ams)) if hasattr(obj, "append_messages") else N.TR_APPEND_MANY_FN()
+        self._cbs = (N.TR_APPEND_FN(guard(am)), many, N.TR_CHALLENGE_FN(guard(ch)))
+        self._ops = N.TranscriptOps(None, *self._cbs)
+        self._h = N.load().lcpc_transcript_from_ops(C.byref(self._ops))
+        if not self._h:
+            raise LcpcError(30, N.last_error())
+
+    def reraise(self, code: int):
+        """after a failed call: the callback's own exception if it caused the failure"""
+        if code == 35 and self.error is not None:
+            err, self.error = self.error, None
+            raise err
+
+    def __del__(self):
+        try:
+            N.load().lcpc_transcript_free(self._h)
+        except Exception:
+            pass
+
+
+def _transcript(tr):
+    """the library's Transcript as is; any other transcript object behind CallerTranscript"""
+    if isinstance(tr, (Transcript, CallerTranscript)):
+        return tr
+    return CallerTranscript(tr)
+
+
+def _call_with_transcript(tr, fn):
+    rc = fn(tr._h)
+    if isinstance(tr, CallerTranscript):
+        tr.reraise(rc)
+    _raise(rc)
 
 
 # ---------------------------------------------------------------- encodings
@@ -471,10 +546,14 @@ class LcCommit:
         return [LcColumn(cols[k].copy(), [pb[32 * (k * pl + i):32 * (k * pl + i + 1)] for i in range(pl)])
                 for k in range(n)]
 
-    def prove(self, outer_tensor: np.ndarray, enc: LcEncoding, tr: Transcript) -> "LcEvalProof":
+    def prove(self, outer_tensor: np.ndarray, enc: LcEncoding, tr) -> "LcEvalProof":
+        """LcCommit::prove (lib.rs:319-326).  tr: the library's Transcript, or the caller's own
+        transcript object (CallerTranscript: every absorb / squeeze goes to it)."""
         o = _elems(outer_tensor, self.field)
         h = C.c_void_p()
-        _raise(N.load().lcpc_prove(self._h, _p64(o), o.shape[0], enc._h, tr._h, C.byref(h)))
+        tr = _transcript(tr)
+        _call_with_transcript(tr, lambda th: N.load().lcpc_prove(self._h, _p64(o), o.shape[0], enc._h, th,
+                                                                 C.byref(h)))
         return LcEvalProof(h.value)
 
 
@@ -666,12 +745,15 @@ class LcEvalProof:
                                               C.byref(h)))
         return cls(h.value)
 
-    def verify(self, root: bytes, outer_tensor, inner_tensor, enc: LcEncoding, tr: Transcript) -> np.ndarray:
+    def verify(self, root: bytes, outer_tensor, inner_tensor, enc: LcEncoding, tr) -> np.ndarray:
+        """LcEvalProof::verify (lib.rs:547-556); tr as for LcCommit.prove."""
         o = _elems(outer_tensor, self.field)
         i = _elems(inner_tensor, self.field)
         rp, keep = _bytes_ptr(root)
         out = np.zeros(limbs(self.field), np.uint64)
-        _raise(N.load().lcpc_verify(rp, _p64(o), o.shape[0], _p64(i), i.shape[0], self._h, enc._h, tr._h, _p64(out)))
+        tr = _transcript(tr)
+        _call_with_transcript(tr, lambda th: N.load().lcpc_verify(rp, _p64(o), o.shape[0], _p64(i), i.shape[0],
+                                                                  self._h, enc._h, th, _p64(out)))
         return out
 
 

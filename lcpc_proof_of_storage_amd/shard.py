@@ -673,12 +673,17 @@ class ShardedCommit:
         return bytes(out)
 
     def prove(self, outer, tr=None, root: int = 0):
-        """Collective; returns the LcEvalProof on rank `root` (which passes the transcript)."""
-        from .lcpc2d import LcEvalProof, _elems
+        """Collective; returns the LcEvalProof on rank `root` (which passes the transcript: the
+        library's Transcript or the caller's own, as LcCommit.prove)."""
+        from .lcpc2d import CallerTranscript, LcEvalProof, _elems, _transcript
         o = np.ascontiguousarray(_elems(outer, self.enc.field))
         h = C.c_void_p()
-        _check(_lib().lcpc_sharded_prove(self._h, o.ctypes.data_as(C.POINTER(C.c_uint64)), o.shape[0], self.enc._h,
-                                         tr._h if tr is not None else None, root, C.byref(h)))
+        tr = _transcript(tr) if tr is not None else None
+        rc = _lib().lcpc_sharded_prove(self._h, o.ctypes.data_as(C.POINTER(C.c_uint64)), o.shape[0], self.enc._h,
+                                       tr._h if tr is not None else None, root, C.byref(h))
+        if isinstance(tr, CallerTranscript):
+            tr.reraise(rc)
+        _check(rc)
         return LcEvalProof(h.value) if h.value else None
 
 
