@@ -28,7 +28,6 @@ events on the launching stream, on serial launches after the timed region) and a
 N = 1: warm-up + median of 5, which doubles as the bit-exactness check of the root).
 """
 import argparse
-import collections
 import glob
 import json
 import os
@@ -110,16 +109,17 @@ def parse():
                          "Commits then finish in order and each proof's serial host "
                          "transcript starts while later commits run, instead of every commit of a wave "
                          "finishing together at its end")
-    ap.add_argument("--workers", type=int, default=0,
-                    help="replicas: host worker threads (steps in flight) exactly; 0: --pipeline's rule")
-    ap.add_argument("--prove-defer", type=int, default=0,
-                    help="replicas (ligero / sdig), timed steps: up to this many finished commitments' proofs "
-                         "wait (first in, first out) while commitments are queued or running (0: none)")
-    ap.add_argument("--prove-order", choices=("interleaved", "commits-first"), default="interleaved",
-                    help="replicas (ligero / sdig), timed steps: a proof starts right after its commitment "
-                         "(interleaved), or waits until no commitment is queued or running and no step is "
-                         "left to start (or every worker waits), so the commitments run back to back and "
-                         "the proofs' kernels fill the GPU while the last transcripts run")
+    ap.add_argument("--input", choices=("device", "host", "host-pinned"), default="device",
+                    help="replicas (ligero / sdig / pos): where each step's input is when it starts.  device "
+                         "(default, the headline): resident in HBM.  host: pageable host memory, the caller's "
+                         "&[F] of LcCommit::commit (lcpc-2d/src/lib.rs:651) or the file image a PoS server read "
+                         "from disk (networking/server.rs:670-679) -- lcpc_commit_new / lcpc_pos_commit_bytes "
+                         "move it across PCIe inside the timed step.  host-pinned: the same from page-locked "
+                         "memory (the DMA engine reads it directly)")
+    ap.add_argument("--transcript", choices=("library", "caller"), default="library",
+                    help="ligero / sdig replicas: prove with the library's own Merlin transcript, or with a "
+                         "caller-owned one driven through lcpc_transcript_ops (CallerTranscript over a "
+                         "library transcript: every absorb / squeeze crosses the callback boundary)")
     ap.add_argument("--timeline", default=None,
                     help="replicas (ligero / sdig): write every timed step's gate / commit / prove "
                          "times (s, from the start of the timed region) to this JSON file")
@@ -189,6 +189,51 @@ def max_over_ranks(dist, x, device="cpu"):
 def replica_seed(rank):
     """Each replica commits its own polynomial (independent objects, no data-path collective)."""
     return SEED + rank
+
+
+# the variables of the one-GPU rehearsals of N ranks (LCPC_BENCH_SHARE_GPU: every rank on GPU 0;
+# LCPC_BENCH_BACKEND=gloo: host-staged exchanges; LCPC_BENCH_RCCL_SAME_GPU / NCCL_HOSTID: RCCL over
+# loopback sockets).  A plain `--gpus N` run sets none of them.
+REHEARSAL_VARS = ("LCPC_BENCH_BACKEND", "LCPC_BENCH_SHARE_GPU", "LCPC_BENCH_RCCL_SAME_GPU", "NCCL_HOSTID")
+COMM_INFO = {}  # the library communicator of this rank's sharded run (nranks, is_rccl), when one exists
+
+
+def device_binding(local_rank):
+    """(the HIP device this rank binds, the rehearsal variables set): one GPU per rank, device =
+    LOCAL_RANK, unless the one-GPU rehearsal puts every rank on GPU 0"""
+    share = os.environ.get("LCPC_BENCH_SHARE_GPU") == "1"
+    return (0 if share else local_rank), {k: os.environ[k] for k in REHEARSAL_VARS if k in os.environ}
+
+
+def rank_identity(rank, local_rank, device_idx, torch=None):
+    """what this rank ran on: its device index and, with a GPU, the device's UUID and PCI bus
+    (distinct per physical GPU), the rehearsal variables, and the library communicator"""
+    ident = {"rank": rank, "local_rank": local_rank, "device": device_idx,
+             "rehearsal_env": device_binding(local_rank)[1],
+             "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")}
+    if torch is not None:
+        props = torch.cuda.get_device_properties(device_idx)
+        ident["device_uuid"] = str(getattr(props, "uuid", "") or "")
+        ident["pci_bus_id"] = getattr(props, "pci_bus_id", None)
+    if COMM_INFO:
+        ident["comm_nranks"] = COMM_INFO.get("nranks")
+        ident["comm_is_rccl"] = COMM_INFO.get("is_rccl")
+    return ident
+
+
+def fold_identities(dist, ident):
+    """every rank's identity on every rank (a collective), and the summary rank 0 prints: the
+    devices the ranks bound, how many distinct GPUs those are, the communicator's rank count when
+    the exchanges ran over RCCL, and whether any rank ran a one-GPU rehearsal"""
+    ids = [ident]
+    if dist is not None:
+        ids = [None] * dist.get_world_size()
+        dist.all_gather_object(ids, ident)
+    uu = [i.get("device_uuid") or f"index:{i['device']}" for i in ids]
+    rccl = [i.get("comm_nranks") for i in ids if i.get("comm_is_rccl")]
+    return {"devices": [i["device"] for i in ids], "distinct_gpus": len(set(uu)),
+            "rccl_nranks": rccl[0] if rccl and len(rccl) == len(ids) else None,
+            "rehearsal": any(i["rehearsal_env"] for i in ids), "ranks": ids}
 
 
 def cgroup_throttle():
@@ -262,6 +307,13 @@ class Workload:
         self.__dict__.update(kw)
 
 
+INPUT_NOTE = {"device": "resident in HBM",
+              "host": "in pageable host memory (numpy; crossed to HBM inside every timed step)",
+              "host-pinned": "in page-locked host memory (torch pin_memory; crossed to HBM inside every timed step)"}
+INPUT_WORKLOAD = {"device": "", "host": ", host-resident input (pageable)",
+                  "host-pinned": ", host-resident input (page-locked)"}
+
+
 def rho_note(args):
     """the metric name of a non-default rate (the BASELINE metric is rho = 1/2)"""
     return "" if args.rho == "1/2" else f", rho={args.rho}"
@@ -280,37 +332,44 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
     # synthetic inputs (host RNG of the product library), then resident in HBM
     coeffs = L.field_random(fid, n, replica_seed(rank))
     outer = L.field_random(fid, n_rows, 7)  # prove accepts any outer tensor of n_rows elements
-    d_coeffs = torch.from_numpy(coeffs.view(np.int64)).to(f"cuda:{local_rank}")
+    host_src = None
+    if args.input == "device":
+        d_coeffs = torch.from_numpy(coeffs.view(np.int64)).to(f"cuda:{local_rank}")
+
+        def commit():
+            return L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+    else:
+        # the caller's coefficients in host memory: LcCommit::commit(&[F]) (lib.rs:651-682)
+        host_src = (torch.from_numpy(coeffs.view(np.int64)).pin_memory().numpy().view(np.uint64)
+                    if args.input == "host-pinned" else coeffs)
+
+        def commit():
+            return L.LcCommit.commit(host_src, enc)
 
     gate = threading.Semaphore(args.commit_slots) if args.commit_slots > 0 else None
 
     timeline = []  # (slot, t_gate, t_commit_start, t_commit_end, t_prove_end) with --timeline
 
-    hooks = {}  # the runner's scheduling hooks (--prove-order)
-
-    def step(slot):
-        t_a = time.perf_counter()
-        if "commit_begin" in hooks:
-            hooks["commit_begin"]()
-        try:
-            if gate is not None:
-                with gate:
-                    t_b = time.perf_counter()
-                    c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
-            else:
-                t_b = t_a
-                c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
-        finally:
-            if "commit_end" in hooks:
-                hooks["commit_end"]()
-        t_c = time.perf_counter()
-        root = c.get_root()
-        if "before_prove" in hooks:
-            hooks["before_prove"]()
+    def transcript(root):
         tr = L.Transcript(b"test transcript")
         tr.append_message(b"polycommit", root)
         tr.append_message(b"ncols", nco.to_bytes(8, "big"))
-        c.prove(outer, enc, tr)
+        # --transcript caller: the caller owns the transcript and prove drives it through
+        # lcpc_transcript_ops (here a library transcript behind Python callbacks)
+        return L.CallerTranscript(tr) if args.transcript == "caller" else tr
+
+    def step(slot):
+        t_a = time.perf_counter()
+        if gate is not None:
+            with gate:
+                t_b = time.perf_counter()
+                c = commit()
+        else:
+            t_b = t_a
+            c = commit()
+        t_c = time.perf_counter()
+        root = c.get_root()
+        c.prove(outer, enc, transcript(root))
         if args.timeline:
             timeline.append((slot, t_a, t_b, t_c, time.perf_counter()))
         return root
@@ -324,19 +383,17 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
         for _ in range(reps):
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+            c = commit()
             root = c.get_root()
             t2 = time.perf_counter()
-            tr = L.Transcript(b"test transcript")
-            tr.append_message(b"polycommit", root)
-            tr.append_message(b"ncols", nco.to_bytes(8, "big"))
-            c.prove(outer, enc, tr)
+            c.prove(outer, enc, transcript(root))
             cs.append(1e3 * (t2 - t1))
             ps.append(1e3 * (time.perf_counter() - t2))
         cs.sort()
         ps.sort()
         return {"commit_ms": cs[len(cs) // 2], "prove_ms": ps[len(ps) // 2],
-                "what": f"one commitment, serial: LcCommit::commit_device and LcCommit::prove (median of {reps})"}
+                "what": f"one commitment, serial: LcCommit::{'commit_device' if args.input == 'device' else 'commit'} "
+                        f"and LcCommit::prove (median of {reps})"}
 
     def cpu_baseline(O):
         o_enc = (O.Encoding.sdig(fid, n_per_row, seed=0, code_id=3) if sdig
@@ -355,7 +412,7 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
     def verify_bench(reps):
         """LcEvalProof::verify (lcpc-2d/src/lib.rs:862-982) of one proof of this workload: the
         verifier's encodes of p_random / p_eval and the column checks, timed over `reps` calls."""
-        c = L.LcCommit.commit_device(d_coeffs.data_ptr(), n, enc)
+        c = commit()
         root = c.get_root()
 
         def tr():
@@ -379,12 +436,12 @@ def ligero_or_sdig(args, L, torch, rank, local_rank):
         metric=("committed field-elements/s (commit+open), 2^24-coeff Brakedown (cfg4)" if sdig else
                 "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU" + rho_note(args)),
         dtype=f"u64x{nl} ({args.field} Montgomery limbs)",
-        data=f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), resident in HBM",
+        data=f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x} + rank)), " + INPUT_NOTE[args.input],
         config={"workload": name + f"{n_rows}x{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, "
-                                   f"BLAKE3 Merkle",
+                                   f"BLAKE3 Merkle" + INPUT_WORKLOAD[args.input],
                 "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                 "n_col_opens": nco, "n_degree_tests": ndt},
-        step=step, hooks=hooks, cpu_baseline=cpu_baseline, verify_bench=verify_bench, cpu_verify=cpu_verify,
+        step=step, cpu_baseline=cpu_baseline, input_bytes=n * B, verify_bench=verify_bench, cpu_verify=cpu_verify,
         latency=latency,
         prepare=lambda: enc.prepare_thread(n_rows), reserve=lambda count: enc.reserve(n, count),
         timeline=timeline,
@@ -545,7 +602,12 @@ def pos_workload(args, L, torch, rank, local_rank):
     rng = np.random.default_rng(1 + rank)
     host = rng.integers(0, 256, n_bytes, dtype=np.uint8)
     dev = f"cuda:{local_rank}"
-    d_bytes = torch.from_numpy(host).to(dev)
+    if args.input == "device":
+        d_bytes = torch.from_numpy(host).to(dev)
+    elif args.input == "host-pinned":
+        host_img = torch.from_numpy(host).pin_memory().numpy()
+    else:
+        host_img = host
     # element buffers of whole-row capacity whose tail past n_el stays zero: commit pads the last
     # row with zeros (lcpc-2d/src/lib.rs:665-674), so committing the n_rows x n_per_row buffer is
     # the same commitment, and the ragged row needs no separate one-row encode
@@ -560,6 +622,8 @@ def pos_workload(args, L, torch, rank, local_rank):
     gate = threading.Semaphore(args.commit_slots) if args.commit_slots > 0 else None
 
     def commit(slot):
+        if args.input != "device":  # the file the server just read: lcpc_pos_commit_bytes from host memory
+            return L.LcCommit.commit_pos_bytes(host_img, enc)
         if args.pos_commit == "bytes":  # lcpc_pos_commit_bytes_device: the file image in one call
             return L.LcCommit.commit_pos_bytes_device(d_bytes.data_ptr(), n_bytes, enc)
         d_el = slots[slot]
@@ -599,19 +663,21 @@ def pos_workload(args, L, torch, rank, local_rank):
         opened = c.open_columns(cols)
         return pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, c.get_root(), ev, opened)
 
-    fi = args.pos_commit == "bytes"  # the file-image commit (its own row-kernel default)
+    fi = args.pos_commit == "bytes" or args.input != "device"  # the file-image commit (its own row-kernel default)
     return Workload(
         units=n_el, unit="field-elements/s", bytes_per_unit=8,
         metric="proof-of-storage server request: committed field-elements/s (pack+commit+eval+256-col open), "
                f"{n_bytes / 2**30:g} GiB file",
         dtype="u64 (WriteableFt63 Montgomery limbs)",
-        data=f"synthetic: {n_bytes} random bytes (numpy default_rng(1 + rank)), resident in HBM",
+        data=f"synthetic: {n_bytes} random bytes (numpy default_rng(1 + rank)), " + INPUT_NOTE[args.input],
         config={"workload": f"PoS request on a {n_bytes}-byte file: {n_el} WriteableFt63 elements, default "
-                            f"dims {n_rows}x{np_}->{nc}, u^T Enc(M) at a point, 256 opened columns",
+                            f"dims {n_rows}x{np_}->{nc}, u^T Enc(M) at a point, 256 opened columns"
+                            + INPUT_WORKLOAD[args.input],
                 "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd,
-                "commit_call": ("lcpc_pos_commit_bytes_device (file image in one call)" if args.pos_commit == "bytes"
+                "commit_call": ("lcpc_pos_commit_bytes (host file image, pipelined upload)" if args.input != "device"
+                                else "lcpc_pos_commit_bytes_device (file image in one call)" if args.pos_commit == "bytes"
                                 else "lcpc_pos_bytes_to_field_device + lcpc_commit_new_device")},
-        step=step, cpu_baseline=cpu_baseline, parity=parity,
+        step=step, cpu_baseline=cpu_baseline, parity=parity, input_bytes=n_bytes,
         enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small", "ntt_row1"),
         enc_kernel_desc=(f"ntt_encode = ntt_row1 (one launch per commit, all {n_rows} rows)" if row1_active(nc, fi) else
                          f"ntt_encode = ntt_pass_a + ntt_pass_b (one launch each per commit, all {n_rows} rows)"),
@@ -661,10 +727,12 @@ def plumbing_check(args, rank, world):
     time.sleep(0.01 * (1 + rank))
     sync_barrier(dist)
     elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    _, local_rank, _ = dist_env()
+    ids = fold_identities(dist, rank_identity(rank, local_rank, device_binding(local_rank)[0]))
     if rank == 0:
         print(json.dumps({"metric": "plumbing check", "value": None, "unit": None, "n_gpus": formed,
                           "world_formed": formed, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": 1e3 * elapsed / max(args.steps, 1), "plumbing_only": True}))
+                          "ms_per_step": 1e3 * elapsed / max(args.steps, 1), "plumbing_only": True, **ids}))
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
@@ -751,6 +819,32 @@ def roofline_objects(wl, iso, stats, args, traffic_rows_frac=1.0):
     return out
 
 
+def h2d_copy_rates(torch, nbytes, device, reps=5):
+    """GB/s of one host -> HBM copy of nbytes from page-locked and from pageable memory (torch
+    copy_ on the current stream, HIP events; best of reps): the PCIe ceilings a host-input line is
+    held against"""
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    out = {}
+    for kind in ("pinned", "pageable"):
+        src = torch.empty(nbytes, dtype=torch.uint8)
+        if kind == "pinned":
+            src = src.pin_memory()
+        src.fill_(1)
+        best = None
+        for _ in range(reps + 1):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            dst.copy_(src, non_blocking=(kind == "pinned"))
+            b.record()
+            b.synchronize()
+            ms = a.elapsed_time(b)
+            best = ms if best is None else min(best, ms)
+        out[kind] = nbytes / (best * 1e-3) / 1e9
+        del src
+    del dst
+    return out
+
+
 def time_cpu_baseline(wl, O, cores, reps):
     """one warm-up, then the median of `reps` timed runs on `cores` threads"""
     O.lib().of_set_threads(cores)
@@ -795,6 +889,7 @@ def ligero_sharded(args, L, torch, dist, rank, world, device, backend, share):
     else:
         comm, comm_kind = shard.NativeComm.host(dist), "host-staged gloo collectives (ranks share one GPU)"
     assert comm.world == world and comm.rank == rank, (comm.world, comm.rank)
+    COMM_INFO.update(nranks=comm.world, is_rccl=comm.is_rccl)
 
     def make_tr(i, root):
         tr = L.Transcript(b"test transcript")
@@ -845,13 +940,13 @@ def main():
     # one-GPU box; the exchanges then go over host-staged gloo collectives); the default is one
     # rank per GPU over RCCL
     backend = os.environ.get("LCPC_BENCH_BACKEND", "nccl")
+    device_idx, _ = device_binding(local_rank)
     share = os.environ.get("LCPC_BENCH_SHARE_GPU") == "1"
     # LCPC_BENCH_RCCL_SAME_GPU=1 (with the two above): the ranks share GPU 0 but the library's
     # exchanges still go through RCCL -- a distinct NCCL_HOSTID per rank makes RCCL treat them as
     # separate nodes (loopback sockets), so its multi-rank send / receive groups run on one GPU
     if os.environ.get("LCPC_BENCH_RCCL_SAME_GPU") == "1" and share:
         os.environ.update(NCCL_HOSTID=f"lcpc-bench-rank-{rank}", NCCL_IB_DISABLE="1", NCCL_SOCKET_IFNAME="lo")
-    device_idx = 0 if share else local_rank
     dist = init_dist(world, device_idx, backend=backend)
     formed = dist.get_world_size() if dist is not None else 1
     if formed != args.gpus:
@@ -890,8 +985,11 @@ def main():
                                  "what": "the row-sharded engine (--mode sharded, the N > 1 default) at N = 1, same "
                                          "workload, steps and warm-up: divide an N > 1 line's value by this for its "
                                          "speed-up on one engine"}
+    # every rank's device and communicator, folded into the line (a collective: all ranks)
+    ids = fold_identities(dist, rank_identity(rank, local_rank, device_idx, torch))
     if rank == 0:
         out["world_formed"] = formed
+        out.update(ids)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
@@ -1155,6 +1253,7 @@ def run_pos_sharded(args, L, torch, dist, rank, world, device, backend, share):
                            "RCCL with the ranks sharing one GPU (per-rank NCCL_HOSTID: socket transport over loopback)")
     else:
         comm, comm_kind = shard.NativeComm.host(dist), "host-staged gloo collectives (ranks share one GPU)"
+    COMM_INFO.update(nranks=comm.world, is_rccl=comm.is_rccl)
 
     def step():
         if hi > lo:
@@ -1270,7 +1369,7 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     # in-flight depth: --pipeline workers pull steps from one counter; with the commit gate there
     # are no waves to align (a K = 20 sweep on the box: 16 workers 11.7-11.8 G/s, 20 workers
     # 10.5-11.2, 10 workers 10.6-11.8, gpurun_out/r02v)
-    P = args.workers if args.workers > 0 else max(1, min(args.pipeline, args.steps))
+    P = max(1, min(args.pipeline, args.steps))
     n_workers = P
     warm_left = [max(0, args.warmup)]  # exactly --warmup untimed steps, over whichever workers
     warmup_done = warm_left[0]
@@ -1283,45 +1382,6 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     roots, errors = [], []
     ready = threading.Barrier(n_workers + 1)
     start = threading.Event()
-    # --prove-order commits-first / --prove-defer M (timed steps only): a finished commitment's
-    # proof joins a FIFO and waits while commitments are queued or running; the oldest waiter is
-    # released whenever more than M wait (commits-first: no bound), and all of them once no
-    # commitment is running and no step is left to start -- or every live worker waits, so a run
-    # with fewer workers than steps cannot stall
-    sched = threading.Condition()
-    st = {"committing": 0, "live": n_workers, "on": False}
-    waiters = collections.deque()
-    bound = args.steps if args.prove_order == "commits-first" else args.prove_defer
-    if bound > 0 and getattr(wl, "hooks", None) is not None:
-        def release():  # (under sched)
-            if (st["committing"] == 0 and todo[0] <= 0) or len(waiters) >= st["live"]:
-                while waiters:
-                    waiters.popleft()["go"] = True
-            while len(waiters) > bound:
-                waiters.popleft()["go"] = True
-            sched.notify_all()
-
-        def commit_begin():
-            with sched:
-                st["committing"] += 1
-
-        def commit_end():
-            with sched:
-                st["committing"] -= 1
-                release()
-
-        def before_prove():
-            with sched:
-                if not st["on"]:
-                    return
-                me = {"go": False}
-                waiters.append(me)
-                release()
-                sched.wait_for(lambda: me["go"] or errors)
-
-        wl.hooks.update(commit_begin=commit_begin, commit_end=commit_end, before_prove=before_prove)
-        st["release"] = release
-
     def worker(slot):
         try:
             if getattr(wl, "prepare", None):
@@ -1336,23 +1396,16 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
             errors.append(e)
         ready.wait()
         start.wait()
-        try:
-            while not errors:
-                with lock:
-                    if todo[0] <= 0:
-                        return
-                    todo[0] -= 1
-                try:
-                    roots.append(wl.step(slot))
-                except Exception as e:
-                    errors.append(e)
+        while not errors:
+            with lock:
+                if todo[0] <= 0:
                     return
-        finally:
-            with sched:
-                st["live"] -= 1
-                if "release" in st:
-                    st["release"]()
-                sched.notify_all()
+                todo[0] -= 1
+            try:
+                roots.append(wl.step(slot))
+            except Exception as e:
+                errors.append(e)
+                return
 
     if getattr(wl, "reserve", None):
         wl.reserve(n_workers + 1)  # device pool blocks and streams of every concurrent step (not steps)
@@ -1365,14 +1418,12 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     L.prof_enable(prof and args.prof_timed)
     L.prof_reset()
     barrier()
-    st["on"] = True
     t0 = time.perf_counter()
     t0_mono_ns = time.clock_gettime_ns(time.CLOCK_MONOTONIC)  # (--timeline: aligns with a rocprofv3 trace)
     c0, th0 = os.times(), cgroup_throttle()
     start.set()
     for w in workers:
         w.join()
-    st["on"] = False
     if errors:
         raise errors[0]
     root = roots[-1] if roots else None
@@ -1406,8 +1457,6 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     out = {
         "metric": wl.metric, "value": value, "unit": wl.unit, "n_gpus": world, "steps": args.steps,
         "warmup": warmup_done, "ms_per_step": 1e3 * elapsed / args.steps, "pipeline": P,
-        **({"prove_order": args.prove_order, "prove_defer": args.prove_defer}
-           if getattr(wl, "hooks", None) is not None else {}),
         "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": wl.dtype, "data": wl.data,
         "config": dict(wl.config, parallelism=f"replicas x{world} (independent commitments per GPU, {P} in flight, "
@@ -1416,6 +1465,18 @@ def run_replicas(args, L, torch, dist, rank, world, device_idx, backend):
     }
     if lat:
         out["latency"] = lat
+    if args.input != "device":
+        from lcpc_proof_of_storage_amd import _native
+        ib = wl.input_bytes
+        rates = h2d_copy_rates(torch, ib, f"cuda:{device_idx}")
+        ach = ib * args.steps * (world if scaling == "weak" else 1) / elapsed / 1e9
+        out["pcie"] = {
+            "input": args.input, "bytes_per_step": ib, "achieved_gbs": ach,
+            "pinned_copy_peak_gbs": rates["pinned"], "pageable_copy_gbs": rates["pageable"],
+            "frac_of_pinned_peak": ach / rates["pinned"] if rates["pinned"] else None,
+            "library_read_pinned_source": bool(_native.load().lcpc_last_upload_pinned()),
+            "what": "input bytes of the timed steps / the timed region, against one whole-buffer torch copy_ of "
+                    "the same size to HBM from page-locked and from pageable memory (HIP events, best of 5)"}
     out["host_cpu"] = host_cpu_use(c0, c1, elapsed)
     if th0 and th1:
         out["host_cpu"]["cgroup_throttled"] = {k: th1[k] - th0[k] for k in th0 if k in th1}

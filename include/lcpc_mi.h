@@ -175,9 +175,15 @@ lcpc_status lcpc_encode_rows_device(const lcpc_encoding *e, const void *d_src, s
 
 /* ------------------------------------------------------------------ LcCommit
  * LcCommit::commit (lcpc-2d/src/lib.rs:314-316 -> commit :651-700).  The commitment (coeffs,
- * encoded matrix, Merkle hashes) stays resident in HBM; `len` elements. */
+ * encoded matrix, Merkle hashes) stays resident in HBM; `len` elements of host memory.  The rows
+ * cross PCIe in ~8 MiB blocks on a copy stream, each block encoded as soon as it has landed;
+ * page-locked memory (hipHostMalloc / hipHostRegister) is read by the DMA engine directly,
+ * pageable memory (a Rust Vec) through two page-locked staging slots of the calling thread. */
 lcpc_status lcpc_commit_new(const lcpc_encoding *e, const uint64_t *coeffs, size_t len,
                             lcpc_commit **out);
+/* 1 if the calling thread's last host-input commit read a page-locked source directly, 0 if it
+ * staged pageable memory (diagnostic) */
+int lcpc_last_upload_pinned(void);
 /* Same with the coefficients already in device memory (no PCIe transfer). */
 lcpc_status lcpc_commit_new_device(const lcpc_encoding *e, const void *d_coeffs, size_t len,
                                    lcpc_commit **out);
@@ -321,6 +327,13 @@ lcpc_status lcpc_pos_bytes_to_field_device(const void *d_bytes, size_t n_bytes, 
  * be 8-byte aligned; WriteableFt63 (LCPC_FT63) encodings only. */
 lcpc_status lcpc_pos_commit_bytes_device(const lcpc_encoding *e, const void *d_bytes, size_t n_bytes,
                                          lcpc_commit **out);
+/* The same commitment from a file image in HOST memory -- what the server has after reading the
+ * file from disk on every proof request (networking/server.rs:670-679): the image crosses PCIe in
+ * blocks of whole rows, and at the default dims each block is unpacked and encoded by the
+ * one-pass kernel as soon as it has landed (pageable images through page-locked staging, as
+ * lcpc_commit_new).  Any alignment. */
+lcpc_status lcpc_pos_commit_bytes(const lcpc_encoding *e, const uint8_t *bytes, size_t n_bytes,
+                                  lcpc_commit **out);
 /* DataField::field_vec_to_byte_vec truncated to expected_len (data_field.rs:57-62,
  * fields.rs:115-121) */
 lcpc_status lcpc_pos_field_to_bytes(const uint64_t *elems, size_t n, uint8_t *out,

@@ -83,6 +83,102 @@ lcpc_status make_sdig_encoding(int fid, int code, size_t n_per_row, size_t want_
   return LCPC_OK;
 }
 
+// Host -> device upload of `bytes` bytes in blocks of `block` bytes on a copy stream of its own,
+// each block handed to on_block(off, n) -- which queues the block's compute on `s` -- as soon as s
+// has been ordered after the block's copy: the DMA of block k + 1 overlaps the kernels of block k.
+// A page-locked source (hipHostMalloc / registered) is read by the DMA engine directly; a pageable
+// one goes through two of this thread's page-locked staging slots, the host filling one while the
+// engine drains the other (lcpc_commit_new's source is the caller's &[F], lcpc-2d/src/lib.rs:651:
+// normally pageable).  Returns with the copies queued; s is ordered after all of them.
+struct UploadStats {
+  bool pinned = false;
+  size_t blocks = 0;
+};
+inline thread_local UploadStats t_last_upload;
+// this thread's upload events (2 "block landed" + 2 "staging slot free"), per current device
+struct UploadEvents {
+  hipEvent_t e[4] = {};
+  int dev = -1;
+  ~UploadEvents() { reset(); }
+  void reset() {
+    for (hipEvent_t &x : e) {
+      if (x) (void)hipEventDestroy(x);
+      x = nullptr;
+    }
+  }
+  bool ready() {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return false;
+    if (cur != dev) {
+      reset();
+      dev = cur;
+    }
+    for (hipEvent_t &x : e)
+      if (!x && hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
+        x = nullptr;
+        return false;
+      }
+    return true;
+  }
+};
+inline thread_local UploadEvents t_upload_ev;
+
+template <class OnBlock>
+lcpc_status h2d_blocks(Device *dev, uint8_t *d_dst, const uint8_t *h_src, size_t bytes, size_t block,
+                       hipStream_t s, OnBlock &&on_block) {
+  t_last_upload = {};
+  if (!bytes) return LCPC_OK;
+  block = std::max<size_t>(block, 4096);
+  const bool pinned = host_dev_ptr(h_src) != nullptr;
+  t_last_upload.pinned = pinned;
+  uint8_t *stg[2] = {nullptr, nullptr};
+  if (!pinned) {
+    const size_t slot = std::min(block, bytes);
+    stg[0] = (uint8_t *)t_pin[PIN_STAGE].get(slot);
+    stg[1] = (uint8_t *)t_pin[PIN_STAGE2].get(slot);
+    if (!stg[0] || !stg[1]) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
+  }
+  if (!t_upload_ev.ready()) return fail(LCPC_ERR_DEVICE, "hipEventCreate");
+  hipEvent_t *landed = t_upload_ev.e, *slot_free = t_upload_ev.e + 2;
+  hipStream_t cs = dev->acquire_stream(POOL_BULK);
+  if (!cs) return fail(LCPC_ERR_DEVICE, "no HIP stream");
+  // (the copies stay queued on cs, and s waits on them: the stream goes back to the pool at once,
+  // work still queued on it ordered like any pooled stream's; the staging slots and events are
+  // this thread's, reused only after its caller drains s)
+  struct Release {
+    Device *dev;
+    hipStream_t cs;
+    ~Release() { dev->release_stream(cs, POOL_BULK); }
+  } rel{dev, cs};
+  bool used[2] = {false, false};
+  size_t k = 0;
+  for (size_t off = 0; off < bytes; off += block, k++) {
+    const size_t n = std::min(block, bytes - off);
+    const int j = (int)(k & 1);
+    if (pinned) {
+      HIP_TRY(hipMemcpyAsync(d_dst + off, h_src + off, n, hipMemcpyHostToDevice, cs));
+    } else {
+      if (used[j]) HIP_TRY(hipEventSynchronize(slot_free[j]));  // its previous DMA has drained
+      std::memcpy(stg[j], h_src + off, n);
+      HIP_TRY(hipMemcpyAsync(d_dst + off, stg[j], n, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipEventRecord(slot_free[j], cs));
+      used[j] = true;
+    }
+    HIP_TRY(hipEventRecord(landed[j], cs));
+    HIP_TRY(hipStreamWaitEvent(s, landed[j], 0));
+    lcpc_status st = on_block(off, n);
+    if (st) return st;
+  }
+  t_last_upload.blocks = k;
+  return LCPC_OK;
+}
+
+// upload block: about 8 MiB, whole rows of `row_bytes` (at least one)
+inline size_t upload_block(size_t row_bytes) {
+  const size_t target = (size_t)8 << 20;
+  return std::max<size_t>(1, target / std::max<size_t>(row_bytes, 1)) * row_bytes;
+}
+
 // src_bytes != 0: d_src is a device proof-of-storage file image of src_bytes bytes, 7 per
 // WriteableFt63 element (len = ceil(src_bytes / 7)), packed as DataField::from_byte_vec does
 // (fields/data_field.rs:38-46) -- at the PoS default dims straight into the one-pass encode
@@ -104,12 +200,31 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   hipStream_t s = lease.s;
   const int fid = e->fid, wb = field_bytes(fid);
   DBuf packed;  // bytes off the fused path: the element image (at function scope: no block-exit drain)
+  DBuf image;   // a host file image's device copy
   const uint8_t *src_b = nullptr;
+  bool host_image = false;  // src_b fills block by block from the host (encoded as blocks land)
   if (src_bytes) {
-    if (fid != LCPC_FT63 || src_is_host) return fail(LCPC_ERR_INVALID_ARG, "file image: device WriteableFt63 only");
-    if (e->kind != KIND_SDIG && ntt_row1_bytes(e->plan) && ntt_rows_pos_bytes_ok(e->plan, np) && !((uintptr_t)d_src & 15)) {
+    if (fid != LCPC_FT63) return fail(LCPC_ERR_INVALID_ARG, "file image: WriteableFt63 only");
+    const bool fuse = e->kind != KIND_SDIG && ntt_row1_bytes(e->plan) && ntt_rows_pos_bytes_ok(e->plan, np);
+    if (src_is_host) {
+      const size_t padded = (src_bytes + 15) / 16 * 16 + 16;
+      HIP_TRY(image.alloc(dev, padded));
+      // (only the padding past the file: the upload writes the rest on its own stream)
+      HIP_TRY(hipMemsetAsync(image.as<uint8_t>() + src_bytes, 0, padded - src_bytes, s));
+      if (fuse) {
+        src_b = image.as<uint8_t>();
+        host_image = true;
+      } else {
+        lcpc_status st = h2d_blocks(dev, image.as<uint8_t>(), (const uint8_t *)d_src, src_bytes, (size_t)8 << 20, s,
+                                    [](size_t, size_t) { return LCPC_OK; });
+        if (st) return st;
+        d_src = image.p;
+      }
+      src_is_host = false;
+    } else if (fuse && !((uintptr_t)d_src & 15)) {
       src_b = (const uint8_t *)d_src;
-    } else {
+    }
+    if (!src_b) {
       HIP_TRY(packed.alloc(dev, len * 8));
       HIP_TRY(pos_pack7((const uint8_t *)d_src, src_bytes, packed.as<uint64_t>(), s));
       d_src = packed.p;
@@ -139,7 +254,9 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
     c->col_major = true;
     c->canon = true;
     if (src_is_host) {
-      HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb, hipMemcpyHostToDevice, s));
+      lcpc_status st = h2d_blocks(dev, cf, (const uint8_t *)d_src, len * wb, (size_t)8 << 20, s,
+                                  [](size_t, size_t) { return LCPC_OK; });
+      if (st) return st;
       if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
       HIP_TRY(transpose_elems(fid, (const uint32_t *)cf, n_rows, np, np, np, (uint32_t *)cm, n_rows, s,
                               TR_FROM_MONT));
@@ -152,10 +269,36 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
     HIP_TRY(tmp.alloc(dev, e->sdig.tmp_elems * n_rows * wb));
     HIP_TRY(sdig_encode_cm(e->sdig, (uint32_t *)cm, n_rows, tmp.as<uint32_t>(), s));
   } else if (src_is_host) {
+    // the caller's rows land in the commitment's coefficient matrix block by block, each block's
+    // rows encoded as soon as they are there (the copy of the next block overlaps)
     c->canon = true;
-    HIP_TRY(hipMemcpyAsync(cf, d_src, len * wb, hipMemcpyHostToDevice, s));
-    if (n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + len * wb, 0, (n_rows * np - len) * wb, s));
-    HIP_TRY(ntt_rows(e->plan, (const uint32_t *)cf, np, np, (uint32_t *)cm, nc, n_rows, s, nullptr, 0, true));
+    const size_t row_b = np * wb, total = len * wb;
+    lcpc_status st = h2d_blocks(dev, cf, (const uint8_t *)d_src, total, upload_block(row_b), s,
+                                [&](size_t off, size_t n) -> lcpc_status {
+      const bool last = off + n == total;
+      const size_t r0 = off / row_b, r1 = last ? n_rows : (off + n) / row_b;
+      if (last && n_rows * np > len) HIP_TRY(hipMemsetAsync(cf + total, 0, (n_rows * np - len) * wb, s));
+      if (r1 > r0)
+        HIP_TRY(ntt_rows(e->plan, (const uint32_t *)(cf + r0 * row_b), np, np, (uint32_t *)(cm + r0 * nc * wb), nc,
+                         r1 - r0, s, nullptr, 0, true));
+      return LCPC_OK;
+    });
+    if (st) return st;
+  } else if (host_image) {
+    // a host file image: uploaded block by block (whole rows of 7 n_per_row bytes), each block's
+    // rows unpacked and encoded by the one-pass kernel as soon as they are there
+    c->canon = true;
+    const size_t row_b = 7 * np;
+    lcpc_status st = h2d_blocks(dev, image.as<uint8_t>(), (const uint8_t *)d_src, src_bytes, upload_block(row_b), s,
+                                [&](size_t off, size_t n) -> lcpc_status {
+      const bool last = off + n == src_bytes;
+      const size_t r0 = off / row_b, r1 = last ? n_rows : (off + n) / row_b;
+      if (r1 > r0)
+        HIP_TRY(ntt_rows_pos_bytes(e->plan, src_b + r0 * row_b, src_bytes - r0 * row_b,
+                                   (uint32_t *)(cm + r0 * nc * wb), nc, r1 - r0, s, (uint32_t *)(cf + r0 * np * wb), np));
+      return LCPC_OK;
+    });
+    if (st) return st;
   } else if (src_b) {
     // the file image, unpacked inside the encode, which also writes the coefficient matrix
     c->canon = true;
@@ -196,6 +339,7 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   tmp.settle();
   scratch.settle();
   packed.settle();
+  image.settle();
   std::memcpy(c->root, h_root, 32);
   c->coeffs.settle();
   c->comm.settle();
@@ -538,6 +682,13 @@ lcpc_status lcpc_pos_commit_bytes_device(const lcpc_encoding *e, const void *d_b
   if ((uintptr_t)d_bytes & 7) return fail(LCPC_ERR_INVALID_ARG, "device file image must be 8-byte aligned");
   return commit_device(e, d_bytes, false, (n_bytes + 6) / 7, out, n_bytes);  // 7 data bytes per element
 }
+
+lcpc_status lcpc_pos_commit_bytes(const lcpc_encoding *e, const uint8_t *bytes, size_t n_bytes, lcpc_commit **out) {
+  if (!bytes || !n_bytes) return fail(LCPC_ERR_INVALID_ARG, "null or empty file image");
+  return commit_device(e, bytes, true, (n_bytes + 6) / 7, out, n_bytes);
+}
+
+int lcpc_last_upload_pinned(void) { return t_last_upload.pinned ? 1 : 0; }
 
 void lcpc_commit_free(lcpc_commit *c) {
   if (!c) return;

@@ -484,6 +484,16 @@ class LcCommit:
         _raise(N.load().lcpc_pos_commit_bytes_device(enc._h, d_bytes, n_bytes, C.byref(h)))
         return cls(h.value, enc.field)
 
+    @classmethod
+    def commit_pos_bytes(cls, data, enc: LcEncoding) -> "LcCommit":
+        """the same commitment from a file image in host memory (lcpc_pos_commit_bytes: the
+        server's per-request commit of the file it just read, networking/server.rs:670-679);
+        data: bytes or a uint8 array"""
+        a = np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, np.uint8)
+        h = C.c_void_p()
+        _raise(N.load().lcpc_pos_commit_bytes(enc._h, a.ctypes.data_as(N.u8p), a.size, C.byref(h)))
+        return cls(h.value, enc.field)
+
     def get_root(self) -> bytes:
         out = (C.c_uint8 * 32)()
         _raise(N.load().lcpc_commit_get_root(self._h, C.cast(out, N.u8p)))

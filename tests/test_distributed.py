@@ -60,16 +60,47 @@ def test_bench_plumbing_world2():
 def test_bench_gpus2_spawns_two_ranks():
     """`bench.py --gpus 2` outside torch.distributed.run launches 2 ranks itself (before any torch
     import) and the rank-0 line reports the world they formed."""
+    d = _spawn_plumbing({})
+    assert d["n_gpus"] == 2 and d["world_formed"] == 2 and d["plumbing_only"] is True
+    # a plain --gpus N spawn: rank k binds device k (LOCAL_RANK), and no rank carries a one-GPU
+    # rehearsal variable -- what lets a SCALE record show N ranks on N distinct GPUs
+    assert d["devices"] == [0, 1] and d["distinct_gpus"] == 2 and d["rehearsal"] is False
+    assert [i["rank"] for i in d["ranks"]] == [0, 1]
+    assert all(i["rehearsal_env"] == {} for i in d["ranks"])
+
+
+def _spawn_plumbing(extra_env):
     import json
     import subprocess
-    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    sys.path.insert(0, ROOT)
+    import bench
+    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK") + bench.REHEARSAL_VARS
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.update(extra_env)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
                         "--plumbing-only"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=220)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
-    d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["world_formed"] == 2 and d["plumbing_only"] is True
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(240)
+def test_bench_rehearsal_is_reported():
+    """the one-GPU rehearsal (every rank on GPU 0) is visible in the line, rank by rank"""
+    d = _spawn_plumbing({"LCPC_BENCH_SHARE_GPU": "1", "LCPC_BENCH_BACKEND": "gloo"})
+    assert d["devices"] == [0, 0] and d["distinct_gpus"] == 1 and d["rehearsal"] is True
+    assert all(i["rehearsal_env"].get("LCPC_BENCH_SHARE_GPU") == "1" for i in d["ranks"])
+
+
+def test_device_binding_is_local_rank(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    for k in bench.REHEARSAL_VARS:
+        monkeypatch.delenv(k, raising=False)
+    assert bench.device_binding(3) == (3, {})
+    monkeypatch.setenv("LCPC_BENCH_SHARE_GPU", "1")
+    assert bench.device_binding(3) == (0, {"LCPC_BENCH_SHARE_GPU": "1"})
 
 
 @pytest.mark.timeout(120)

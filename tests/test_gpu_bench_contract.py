@@ -70,14 +70,35 @@ def test_bench_ligero_default_small(gpu):
     assert d["parity_ok"] is True and d["sharded_n1"]["root_equals_replicas"] is True
 
 
-@pytest.mark.parametrize("order", [("--prove-defer", "2"), ("--prove-order", "commits-first")])
-def test_bench_ligero_prove_scheduling_small(gpu, order):
-    """the A/B scheduling options (proofs deferred while commitments run) finish with every
-    step's root right, including with fewer workers than steps (the all-waiting release)"""
-    d = _bench("--steps", "8", "--warmup", "2", "--log-len", "16", "--workers", "3", "--verify-reps", "0",
-               "--sharded-n1", "0", *order)
-    _check_common(d, 8)
-    assert d["steps_agree"] is True and d["parity_root_vs_oracle"] is True and d["parity_ok"] is True
+@pytest.mark.parametrize("source", ["host", "host-pinned"])
+def test_bench_ligero_host_input_small(gpu, source):
+    """--input host / host-pinned: every timed step commits from host memory (lcpc_commit_new,
+    the reference's commit(&[F])); the line carries the PCIe figures and stays right"""
+    d = _bench("--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1", "--sharded-n1", "0",
+               "--input", source)
+    _check_common(d, 4)
+    assert d["parity_ok"] is True and d["steps_agree"] is True
+    pc = d["pcie"]
+    assert pc["input"] == source and pc["bytes_per_step"] == (1 << 16) * 16
+    assert pc["achieved_gbs"] > 0 and pc["pinned_copy_peak_gbs"] > 0 and pc["pageable_copy_gbs"] > 0
+    assert pc["library_read_pinned_source"] is (source == "host-pinned")
+    assert "host" in d["data"] and "host-resident" in d["config"]["workload"]
+
+
+def test_bench_ligero_caller_transcript_small(gpu):
+    """--transcript caller: prove drives a caller-owned transcript through lcpc_transcript_ops;
+    same roots, the oracle's proof and verifier value"""
+    d = _bench("--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1", "--sharded-n1", "0",
+               "--transcript", "caller")
+    _check_common(d, 4)
+    assert d["parity_ok"] is True and d["verify"]["parity_vs_oracle"] is True
+
+
+def test_bench_pos_host_input_small(gpu):
+    d = _bench("--code", "pos", "--steps", "2", "--warmup", "2", "--pos-bytes", str(1 << 20), "--input", "host")
+    _check_common(d, 2)
+    assert d["parity_ok"] is True and d["pcie"]["bytes_per_step"] == 1 << 20
+    assert "lcpc_pos_commit_bytes" in d["config"]["commit_call"]
 
 
 def _bench_ranks(world, extra_env, *args, timeout=280):
@@ -96,6 +117,8 @@ def _check_self_checking(d, world):
     """an N > 1 line carries its own evidence of a right answer: the oracle's root against every
     warm-up and timed step, the kept proof and the verifier's value (the timed cpu_baseline is the
     N = 1 line's: at N > 1 the oracle runs once, as the checker)"""
+    # one GPU box: the ranks share GPU 0 (the rehearsal), and the line says so rank by rank
+    assert d["devices"] == [0] * world and d["rehearsal"] is True and len(d["ranks"]) == world
     assert d["n_gpus"] == world and d["world_formed"] == world and d["scaling"] == "strong"
     assert d["parity_root_vs_oracle"] is True and d["parity_proof_vs_oracle"] is True
     ps = d["parity_steps_vs_oracle"]
