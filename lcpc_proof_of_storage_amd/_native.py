@@ -12,7 +12,9 @@ import re
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "liblcpc_mi.so")
+# LCPC_MI_LIB: another in-tree build of the same sources (e.g. an FFT-convention variant,
+# tools/gpu/fft_variant_check.sh); the default is the shipped library
+LIB_PATH = os.environ.get("LCPC_MI_LIB") or os.path.join(PKG_DIR, "liblcpc_mi.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "lcpc_mi.h")
 
 _lib = None

@@ -5,6 +5,8 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "../../include/lcpc_fft_convention.h"
+
 namespace lcpc {
 
 // Bytes per element of field `fid` (8, 16, 24, 32) and 32-bit words per element.
@@ -24,6 +26,8 @@ bool no_mfma();
 struct NttPlan {
   int fid = -1;
   int log_n = 0, l1 = 0, l2 = 0;
+  // an ifft_oi plan (its rows are the inner DIF of the inverse: never reordered by ntt_rows)
+  bool inverse = false;
   uint32_t *d_tw = nullptr;        // w^e, e in [0, n): n elements (Montgomery)
   uint32_t *d_tw_canon = nullptr;  // forward plans: the same values' canonical words (below)
   // pass A's inter-pass twiddles w^(c * bitrev_l1(t)) laid out [t][c] (t < 2^l1, c < 2^l2): the
@@ -51,9 +55,13 @@ void ntt_plan_free(NttPlan &p);
 // canonical words of w^e (d_tw_canon) -- at no extra cost, and every output's Montgomery words
 // become its canonical value: commitments hash their codeword without a per-element
 // conversion (the Merkle leaves are over canonical bytes).
+// Forward plans follow include/lcpc_fft_convention.h: with LCPC_FFT_OUTPUT_BITREV = 0 the rows are
+// reordered to natural order after the transform (bitrev_rows_inplace).
 hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
                     uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s,
                     uint32_t *copy = nullptr, size_t copy_stride = 0, bool canon_out = false);
+// m[r][j] <-> m[r][bitrev_log_n(j)] in place, rows r < n_rows of stride `stride` elements
+hipError_t bitrev_rows_inplace(int fid, uint32_t *m, size_t stride, int log_n, size_t n_rows, hipStream_t s);
 // The proof-of-storage file image encoded straight into a commitment (ntt_row1.hpp BYTES): row r
 // = WriteableFt63 elements [n_per_row r, n_per_row (r + 1)) of the n_bytes-byte image, 7 bytes per
 // element (zero padded); canonical output, the coefficient matrix written to copy.  Only at the

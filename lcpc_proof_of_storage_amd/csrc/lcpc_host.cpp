@@ -1555,10 +1555,16 @@ lcpc_status lcpc_ifft_oi_rows(lcpc_field f, uint64_t *rows, size_t n_rows, size_
   HIP_TRY(b.alloc(dev, n_rows * len * wb));
   uint32_t inv[8] = {0};
   inv_pow2_canon(f, log_n, inv);
-  HIP_TRY(bitrev_scale(f, a.as<uint32_t>(), b.as<uint32_t>(), log_n, n_rows, nullptr, lease.s));
-  HIP_TRY(ntt_rows(plan, b.as<uint32_t>(), len, len, a.as<uint32_t>(), len, n_rows, lease.s));
-  HIP_TRY(bitrev_scale(f, a.as<uint32_t>(), b.as<uint32_t>(), log_n, n_rows, inv, lease.s));
-  HIP_TRY(hipMemcpyAsync(rows, b.p, n_rows * len * wb, hipMemcpyDeviceToHost, lease.s));
+  // ifft_oi = reorder the evaluations to natural order (bit-reversed ones: include/
+  // lcpc_fft_convention.h), DIF with the inverse root, bit-reverse back and scale by len^-1
+  uint32_t *x = a.as<uint32_t>(), *y = b.as<uint32_t>();
+  if (LCPC_FFT_OUTPUT_BITREV) {
+    HIP_TRY(bitrev_scale(f, x, y, log_n, n_rows, nullptr, lease.s));
+    std::swap(x, y);
+  }
+  HIP_TRY(ntt_rows(plan, x, len, len, y, len, n_rows, lease.s));
+  HIP_TRY(bitrev_scale(f, y, x, log_n, n_rows, inv, lease.s));
+  HIP_TRY(hipMemcpyAsync(rows, x, n_rows * len * wb, hipMemcpyDeviceToHost, lease.s));
   HIP_TRY(hipStreamSynchronize(lease.s));
   return LCPC_OK;
 }
@@ -2500,12 +2506,17 @@ lcpc_status lcpc_pos_decode_porenc(const uint8_t *porenc, size_t pre, size_t enc
     // [enc][B] canonical -> [B][enc] Montgomery (get_encoded_row + raw_bytes_to_field_vec)
     HIP_TRY(transpose_elems(fid, a.as<uint32_t>(), enc, B, B, B, b.as<uint32_t>(), enc, s, TR_TO_MONT,
                             dbad.as<uint32_t>()));
-    HIP_TRY(bitrev_scale(fid, b.as<uint32_t>(), a.as<uint32_t>(), log_n, B, nullptr, s));
-    HIP_TRY(ntt_rows(plan, a.as<uint32_t>(), enc, enc, b.as<uint32_t>(), enc, B, s));
-    HIP_TRY(bitrev_scale(fid, b.as<uint32_t>(), a.as<uint32_t>(), log_n, B, inv, s));
+    // ifft_oi (see lcpc_ifft_oi_rows): the decoded rows end in x, y is free
+    uint32_t *x = b.as<uint32_t>(), *y = a.as<uint32_t>();
+    if (LCPC_FFT_OUTPUT_BITREV) {
+      HIP_TRY(bitrev_scale(fid, x, y, log_n, B, nullptr, s));
+      std::swap(x, y);
+    }
+    HIP_TRY(ntt_rows(plan, x, enc, enc, y, enc, B, s));
+    HIP_TRY(bitrev_scale(fid, y, x, log_n, B, inv, s));
     // decoded_row.drain(pre..) then field_vec_to_byte_vec
-    HIP_TRY(hipMemcpy2DAsync(b.p, pre * POS_WB, a.p, enc * POS_WB, pre * POS_WB, B, hipMemcpyDeviceToDevice, s));
-    HIP_TRY(pos_unpack7(b.as<uint64_t>(), B * pre, dbytes.as<uint8_t>(), B * pre * POS_DB, s));
+    HIP_TRY(hipMemcpy2DAsync(y, pre * POS_WB, x, enc * POS_WB, pre * POS_WB, B, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(pos_unpack7(reinterpret_cast<const uint64_t *>(y), B * pre, dbytes.as<uint8_t>(), B * pre * POS_DB, s));
     if (k >= 2) HIP_TRY(hipEventSynchronize(out_ev.e[slot]));
     HIP_TRY(hipMemcpyAsync(ostg[slot].p, dbytes.p, B * pre * POS_DB, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(out_ev.e[slot], s));

@@ -48,6 +48,10 @@ hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream
     return hipErrorInvalidValue;
   p.fid = fid;
   p.log_n = log_n;
+  p.inverse = inverse;
+  // include/lcpc_fft_convention.h: the forward transform's root is omega or omega^-1, the
+  // inverse's the other one
+  const bool inv_root = inverse != (LCPC_FFT_OMEGA_INVERSE != 0);
   // Ft63 at 2^15 (the PoS default n_cols): the l1 = 8 split measured 5 % faster than l1 = 7
   // (tools/microbench/nttbench.hip mode 5, 9363 rows); every other shape splits evenly.
   p.l1 = fid == 0 && log_n == 15 ? 8 : log_n / 2;
@@ -56,11 +60,11 @@ hipError_t ntt_plan_init(NttPlan &p, int fid, int log_n, bool inverse, hipStream
   hipError_t e = hipMalloc(&p.d_tw, n * field_bytes(fid));
   if (e != hipSuccess) return e;
   switch (fid) {
-    case 0: e = ntt_tw_table_ft63(p.d_tw, log_n, inverse, s); break;
-    case 1: e = ntt_tw_table_ft127(p.d_tw, log_n, inverse, s); break;
-    case 2: e = ntt_tw_table_ft191(p.d_tw, log_n, inverse, s); break;
-    case 3: e = ntt_tw_table_ft255(p.d_tw, log_n, inverse, s); break;
-    default: e = ntt_tw_table_ft253(p.d_tw, log_n, inverse, s); break;
+    case 0: e = ntt_tw_table_ft63(p.d_tw, log_n, inv_root, s); break;
+    case 1: e = ntt_tw_table_ft127(p.d_tw, log_n, inv_root, s); break;
+    case 2: e = ntt_tw_table_ft191(p.d_tw, log_n, inv_root, s); break;
+    case 3: e = ntt_tw_table_ft255(p.d_tw, log_n, inv_root, s); break;
+    default: e = ntt_tw_table_ft253(p.d_tw, log_n, inv_root, s); break;
   }
   if (e != hipSuccess) return e;
   if (log_n > 12) {  // the pass-A kernels' [t][c] inter-pass twiddles
@@ -93,14 +97,19 @@ void ntt_plan_free(NttPlan &p) {
 hipError_t ntt_rows(const NttPlan &p, const uint32_t *src, size_t src_stride, size_t n_valid,
                     uint32_t *dst, size_t dst_stride, size_t n_rows, hipStream_t s, uint32_t *copy,
                     size_t copy_stride, bool canon) {
+  hipError_t e;
   switch (p.fid) {
-    case 0: return ntt_rows_ft63(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
-    case 1: return ntt_rows_ft127(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
-    case 2: return ntt_rows_ft191(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
-    case 3: return ntt_rows_ft255(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
-    case 4: return ntt_rows_ft253(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon);
+    case 0: e = ntt_rows_ft63(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon); break;
+    case 1: e = ntt_rows_ft127(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon); break;
+    case 2: e = ntt_rows_ft191(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon); break;
+    case 3: e = ntt_rows_ft255(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon); break;
+    case 4: e = ntt_rows_ft253(p, src, src_stride, n_valid, dst, dst_stride, n_rows, s, copy, copy_stride, canon); break;
     default: return hipErrorInvalidValue;
   }
+#if !LCPC_FFT_OUTPUT_BITREV
+  if (e == hipSuccess && !p.inverse) e = bitrev_rows_inplace(p.fid, dst, dst_stride, p.log_n, n_rows, s);
+#endif
+  return e;
 }
 
 }  // namespace lcpc

@@ -16,7 +16,11 @@ hipError_t ntt_rows_pos_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_b
   if (!ntt_rows_pos_bytes_ok(p, (size_t)1 << (ntt_row1::LOG_N - 1)) || ((uintptr_t)bytes & 15) || !copy)
     return hipErrorInvalidValue;
   if (n_rows == 0) return hipSuccess;
-  return ntt_row1::launch_bytes<Ft63>(p, bytes, n_bytes, dst, dst_stride, n_rows, s, copy, copy_stride);
+  hipError_t e = ntt_row1::launch_bytes<Ft63>(p, bytes, n_bytes, dst, dst_stride, n_rows, s, copy, copy_stride);
+#if !LCPC_FFT_OUTPUT_BITREV
+  if (e == hipSuccess) e = bitrev_rows_inplace(p.fid, dst, dst_stride, p.log_n, n_rows, s);
+#endif
+  return e;
 }
 hipError_t ntt_tw_table_ft63(uint32_t *tw, int log_n, bool inverse, hipStream_t s) {
   const size_t n = (size_t)1 << log_n;

@@ -125,6 +125,21 @@ __global__ __launch_bounds__(256) void k_bitrev_scale(const uint32_t *__restrict
   fe_store<F>(out, r * n + j, v);
 }
 
+// m[r][j] <-> m[r][bitrev(j)], one thread per pair end j (the one with j < bitrev(j) swaps)
+template <class F>
+__global__ __launch_bounds__(256) void k_bitrev_inplace(uint32_t *__restrict__ m, size_t stride, int log_n,
+                                                        size_t n_rows) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t n = (size_t)1 << log_n;
+  if (t >= n * n_rows) return;
+  const size_t r = t >> log_n, i = t & (n - 1);
+  const size_t j = log_n ? (size_t)(__builtin_bitreverse64((uint64_t)i) >> (64 - log_n)) : 0;
+  if (i >= j) return;
+  const Fe<F> a = fe_load<F>(m, r * stride + i), b = fe_load<F>(m, r * stride + j);
+  fe_store<F>(m, r * stride + i, b);
+  fe_store<F>(m, r * stride + j, a);
+}
+
 // dst[i] = base^(i * step_exp)  for i < n  (Montgomery)
 template <class F>
 __global__ __launch_bounds__(256) void k_powers(const uint32_t *__restrict__ base, uint64_t step_exp,
@@ -166,6 +181,16 @@ hipError_t bitrev_scale(int fid, const uint32_t *in, uint32_t *out, int log_n, s
       for (int i = 0; i < F::N; i++) sc.v[i] = scale_canon_words[i];
     hipLaunchKernelGGL((k_bitrev_scale<F>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, in,
                        out, log_n, n_rows, sc, scale_canon_words ? 1 : 0);
+    return hipGetLastError();
+  });
+}
+
+hipError_t bitrev_rows_inplace(int fid, uint32_t *m, size_t stride, int log_n, size_t n_rows, hipStream_t s) {
+  const size_t total = ((size_t)1 << log_n) * n_rows;
+  if (!total || log_n == 0) return hipSuccess;
+  return dispatch_field(fid, [&]<class F>() {
+    hipLaunchKernelGGL((k_bitrev_inplace<F>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, m, stride,
+                       log_n, n_rows);
     return hipGetLastError();
   });
 }

@@ -17,15 +17,33 @@
  *   - ifft_oi: decimation in time with omega^-1 roots, bit-reversed input, natural output,
  *     then every element multiplied by len^-1.
  * The butterfly order cannot change any output bit (field arithmetic is exact); the two
- * choices that can -- which root and which output order -- are pinned by the reference's
+ * choices that can -- which root and which output order -- are NOT pinned by the reference's
  * own invariant tests (lcpc-2d/src/tests.rs:193-234 commit test: ifft_oi inverts encode and
- * the encoded rows are R-S evaluations) which tests/test_oracle_invariants.py ports.
+ * the encoded rows are R-S evaluations, ported by tests/test_oracle_invariants.py), which hold
+ * under either.  They are the switches of include/lcpc_fft_convention.h, shared with the
+ * product's NTT plans; the defaults are the restatement above.
  */
 #include <stdlib.h>
 #include <string.h>
 
+#include "../include/lcpc_fft_convention.h"
 #include "oracle.h"
 #include "of_internal.h"
+
+/* x[j] <-> x[bitrev_lg(j)] (the LCPC_FFT_OUTPUT_BITREV = 0 convention's reordering) */
+static void bitrev_permute(uint64_t *x, int lg, int nl) {
+  const size_t n = (size_t)1 << lg;
+  for (size_t j = 0; j < n; j++) {
+    size_t r = 0;
+    for (int b = 0; b < lg; b++) r |= ((j >> b) & 1) << (lg - 1 - b);
+    if (j < r)
+      for (int k = 0; k < nl; k++) {
+        const uint64_t t = x[j * nl + k];
+        x[j * nl + k] = x[r * nl + k];
+        x[r * nl + k] = t;
+      }
+  }
+}
 
 static int log2_exact(size_t len, int *lg) {
   if (len == 0 || (len & (len - 1))) return 0;
@@ -40,6 +58,11 @@ void of_ntt_omega(int fid, int log_len, uint64_t *out) {
   uint64_t w[OF_MAXL];
   memcpy(w, f->root, sizeof(w));
   for (uint32_t i = 0; i < f->s - (uint32_t)log_len; i++) of_mont_mul(f, w, w, w);
+#if LCPC_FFT_OMEGA_INVERSE
+  uint64_t wi[OF_MAXL];
+  of_inv(fid, w, wi);
+  memcpy(w, wi, sizeof(w));
+#endif
   memcpy(out, w, sizeof(uint64_t) * f->nl);
 }
 
@@ -77,6 +100,9 @@ int of_fft_io(int fid, uint64_t *x, size_t len) {
     }
   }
   free(roots);
+#if !LCPC_FFT_OUTPUT_BITREV
+  bitrev_permute(x, lg, nl);
+#endif
   return 0;
 }
 
@@ -92,6 +118,9 @@ int of_ifft_oi(int fid, uint64_t *x, size_t len) {
   of_inv(fid, w, wi);
   uint64_t *roots = roots_table(f, lg, wi);
   uint64_t a[OF_MAXL], b[OF_MAXL];
+#if !LCPC_FFT_OUTPUT_BITREV
+  bitrev_permute(x, lg, nl);  /* natural-order evaluations in: the DIT below reads bit-reversed */
+#endif
   for (size_t gap = 1; gap < len; gap *= 2) {
     size_t nchunks = len / (2 * gap);
     for (size_t c = 0; c < nchunks; c++) {

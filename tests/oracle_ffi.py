@@ -14,7 +14,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-LIB_PATH = os.path.join(ORACLE_DIR, "build", "liblcpc_oracle.so")
+# LCPC_ORACLE_LIB: an oracle variant (build_variant below) for a whole test run
+LIB_PATH = os.environ.get("LCPC_ORACLE_LIB") or os.path.join(ORACLE_DIR, "build", "liblcpc_oracle.so")
 
 FIELDS = {"Ft63": 0, "Ft127": 1, "Ft191": 2, "Ft255": 3, "Ft253_192": 4}
 LABEL = {"DT": b"$l//DT", "PR": b"$l//PR", "PE": b"$l//PE", "CO": b"$l//CO"}
@@ -34,6 +35,34 @@ def lib():
         _lib = C.CDLL(LIB_PATH)
         _setup(_lib)
     return _lib
+
+
+def build_variant(name: str, flags: str) -> str:
+    """an oracle built with other compile-time switches (e.g. the FFT conventions of
+    include/lcpc_fft_convention.h) into oracle/build/<name>/; returns the library path"""
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "variant", f"VARIANT={name}", f"VARIANT_FLAGS={flags}"],
+                   check=True)
+    return os.path.join(ORACLE_DIR, "build", name, "liblcpc_oracle.so")
+
+
+class use_lib:
+    """with use_lib(path): every wrapper in this module calls that oracle build instead"""
+
+    def __init__(self, path: str):
+        self.path = path
+
+    def __enter__(self):
+        global _lib
+        self.prev = lib()
+        v = C.CDLL(self.path)
+        _setup(v)
+        _lib = v
+        return v
+
+    def __exit__(self, *exc):
+        global _lib
+        _lib = self.prev
+        return False
 
 
 u64p = C.POINTER(C.c_uint64)

@@ -46,11 +46,14 @@ def bitrev(x: int, bits: int) -> int:
     return int(format(x, f"0{bits}b")[::-1], 2) if bits else 0
 
 
-def fft_io_naive(f: Field, xs):
-    """out[bitrev(j)] = sum_i x_i w^(ij) on canonical values."""
+def fft_io_naive(f: Field, xs, omega_inverse: bool = False, bitrev_out: bool = True):
+    """out[bitrev(j)] = sum_i x_i w^(ij) on canonical values (the two switches of
+    include/lcpc_fft_convention.h: w^-1 instead of w; natural instead of bit-reversed output)."""
     n = len(xs)
     lg = n.bit_length() - 1
     w = f.omega(lg)
+    if omega_inverse:
+        w = pow(w, -1, f.p)
     out = [0] * n
     for j in range(n):
         wj = pow(w, j, f.p)
@@ -58,7 +61,7 @@ def fft_io_naive(f: Field, xs):
         for x in xs:
             acc = (acc + x * pw) % f.p
             pw = pw * wj % f.p
-        out[bitrev(j, lg)] = acc
+        out[bitrev(j, lg) if bitrev_out else j] = acc
     return out
 
 
