@@ -196,6 +196,23 @@ static void basic_cases() {
   sim.work(B, 3);
   sim.drain_all();
 
+  // first use on a FOREIGN stream (the sharded PoS request's gather buffer, shard_native.cpp):
+  // B takes the block (its stream gets the fence wait), THEN records the event the comm stream C
+  // waits on, and C writes the block -- C is ordered after A's old use through B's wait.  (Taken
+  // after the record, C's write would not be: the round-5 advisor's finding, fixed by taking the
+  // buffer before the record.)
+  sim.work(A, 6);
+  pool.put((void *)0x8000, 512, ss, 1);
+  assert(pool.take(512, B) == (void *)0x8000);
+  sim.new_owner(6);
+  {
+    const int ev = b.event_new();
+    b.record(ev, B);
+    b.wait(C, ev);
+    sim.work(C, 6);
+    sim.drain_all();  // aborts if C's write ran before A's use completed
+  }
+
   // a host taker (no stream) waits on the host
   sim.work(C, 4);
   int ss3[] = {C};
