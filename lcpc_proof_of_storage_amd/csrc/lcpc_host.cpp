@@ -131,8 +131,15 @@ lcpc_status h2d_blocks(Device *dev, uint8_t *d_dst, const uint8_t *h_src, size_t
   block = std::max<size_t>(block, 4096);
   const bool pinned = host_dev_ptr(h_src) != nullptr;
   t_last_upload.pinned = pinned;
+  // (A/B, round 6: LCPC_H2D_PAGEABLE=direct hands pageable blocks to the runtime's own
+  // pageable path instead of the staging slots)
+  static const bool direct = [] {
+    const char *v = getenv("LCPC_H2D_PAGEABLE");
+    return v && std::string(v) == "direct";
+  }();
+  const bool staged = !pinned && !direct;
   uint8_t *stg[2] = {nullptr, nullptr};
-  if (!pinned) {
+  if (staged) {
     const size_t slot = std::min(block, bytes);
     stg[0] = (uint8_t *)t_pin[PIN_STAGE].get(slot);
     stg[1] = (uint8_t *)t_pin[PIN_STAGE2].get(slot);
@@ -155,7 +162,7 @@ lcpc_status h2d_blocks(Device *dev, uint8_t *d_dst, const uint8_t *h_src, size_t
   for (size_t off = 0; off < bytes; off += block, k++) {
     const size_t n = std::min(block, bytes - off);
     const int j = (int)(k & 1);
-    if (pinned) {
+    if (!staged) {
       HIP_TRY(hipMemcpyAsync(d_dst + off, h_src + off, n, hipMemcpyHostToDevice, cs));
     } else {
       if (used[j]) HIP_TRY(hipEventSynchronize(slot_free[j]));  // its previous DMA has drained

@@ -38,7 +38,8 @@
 
 constexpr int ITERS = 16384;
 
-enum Mode { MAD = 0, ADDC, ADDCO, CND, MOV, ADD32, NOP_PAIR, HAZARD, NOP_ONLY, N_MODES };
+enum Mode { MAD = 0, ADDC, ADDCO, CND, MOV, ADD32, NOP_PAIR, HAZARD, NOP_ONLY, CND_SGPR, CND_CMP, BFI, SUBB_MASK,
+            N_MODES };
 static const char *NAMES[N_MODES] = {
     "v_mad_u64_u32",
     "v_addc_co_u32 (independent SGPR carries)",
@@ -49,10 +50,14 @@ static const char *NAMES[N_MODES] = {
     "v_add_u32 + s_nop 0 (pair)",
     "carry chain: add(c)_co + s_nop 0 per link",
     "s_nop 0 alone",
+    "v_cndmask_b32_e64 (SGPR-pair mask)",
+    "v_cmp_gt_u32 + v_cndmask_b32 (vcc just written)",
+    "v_bfi_b32 (VGPR mask select)",
+    "v_subb_co_u32 (0 - borrow: a VGPR mask)",
 };
 // instructions (VALU + s_nop) per stream per iteration, and VALU ones among them
-static const int INSTR[N_MODES] = {1, 1, 1, 1, 1, 1, 2, 2, 1};
-static const int VALU[N_MODES] = {1, 1, 1, 1, 1, 1, 1, 1, 0};
+static const int INSTR[N_MODES] = {1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 2, 1, 1};
+static const int VALU[N_MODES] = {1, 1, 1, 1, 1, 1, 1, 1, 0, 1, 2, 1, 1};
 
 struct WaveRec {
   uint64_t cycles;
@@ -147,8 +152,47 @@ __global__ __launch_bounds__(256) void k_issue(WaveRec *rec, uint32_t seed) {
           : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)
           : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7])
           : "s40", "s41");
-    } else {
+    } else if constexpr (MODE == NOP_ONLY) {
       asm volatile("s_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0");
+    } else if constexpr (MODE == CND_SGPR) {
+      asm volatile(
+          "v_cndmask_b32_e64 %0, %0, %8, s[40:41]\n\tv_cndmask_b32_e64 %1, %1, %9, s[40:41]\n\t"
+          "v_cndmask_b32_e64 %2, %2, %10, s[40:41]\n\tv_cndmask_b32_e64 %3, %3, %11, s[40:41]\n\t"
+          "v_cndmask_b32_e64 %4, %4, %12, s[40:41]\n\tv_cndmask_b32_e64 %5, %5, %13, s[40:41]\n\t"
+          "v_cndmask_b32_e64 %6, %6, %14, s[40:41]\n\tv_cndmask_b32_e64 %7, %7, %15, s[40:41]"
+          : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)
+          : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7])
+          : "s40", "s41");
+    } else if constexpr (MODE == CND_CMP) {  // the field add's pattern: a compare, then its select
+      asm volatile(
+          "v_cmp_gt_u32 vcc, %0, %8\n\tv_cndmask_b32 %0, %0, %8, vcc\n\t"
+          "v_cmp_gt_u32 vcc, %1, %9\n\tv_cndmask_b32 %1, %1, %9, vcc\n\t"
+          "v_cmp_gt_u32 vcc, %2, %10\n\tv_cndmask_b32 %2, %2, %10, vcc\n\t"
+          "v_cmp_gt_u32 vcc, %3, %11\n\tv_cndmask_b32 %3, %3, %11, vcc\n\t"
+          "v_cmp_gt_u32 vcc, %4, %12\n\tv_cndmask_b32 %4, %4, %12, vcc\n\t"
+          "v_cmp_gt_u32 vcc, %5, %13\n\tv_cndmask_b32 %5, %5, %13, vcc\n\t"
+          "v_cmp_gt_u32 vcc, %6, %14\n\tv_cndmask_b32 %6, %6, %14, vcc\n\t"
+          "v_cmp_gt_u32 vcc, %7, %15\n\tv_cndmask_b32 %7, %7, %15, vcc"
+          : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)
+          : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7])
+          : "vcc");
+    } else if constexpr (MODE == BFI) {
+      asm volatile(
+          "v_bfi_b32 %0, %8, %0, %9\n\tv_bfi_b32 %1, %9, %1, %10\n\tv_bfi_b32 %2, %10, %2, %11\n\t"
+          "v_bfi_b32 %3, %11, %3, %12\n\tv_bfi_b32 %4, %12, %4, %13\n\tv_bfi_b32 %5, %13, %5, %14\n\t"
+          "v_bfi_b32 %6, %14, %6, %15\n\tv_bfi_b32 %7, %15, %7, %8"
+          : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)
+          : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]));
+    } else {
+      asm volatile(
+          "v_subb_co_u32 %0, s[40:41], 0, %8, s[40:41]\n\tv_subb_co_u32 %1, s[42:43], 0, %9, s[42:43]\n\t"
+          "v_subb_co_u32 %2, s[44:45], 0, %10, s[44:45]\n\tv_subb_co_u32 %3, s[46:47], 0, %11, s[46:47]\n\t"
+          "v_subb_co_u32 %4, s[48:49], 0, %12, s[48:49]\n\tv_subb_co_u32 %5, s[50:51], 0, %13, s[50:51]\n\t"
+          "v_subb_co_u32 %6, s[52:53], 0, %14, s[52:53]\n\tv_subb_co_u32 %7, s[54:55], 0, %15, s[54:55]"
+          : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)
+          : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7])
+          : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53",
+            "s54", "s55");
     }
   }
 #undef V8
@@ -255,6 +299,10 @@ int main(int argc, char **argv) {
     rc |= run<NOP_PAIR>(k, n_cu, clock_mhz, js, false);
     rc |= run<HAZARD>(k, n_cu, clock_mhz, js, false);
     rc |= run<NOP_ONLY>(k, n_cu, clock_mhz, js, false);
+    rc |= run<CND_SGPR>(k, n_cu, clock_mhz, js, false);
+    rc |= run<CND_CMP>(k, n_cu, clock_mhz, js, false);
+    rc |= run<BFI>(k, n_cu, clock_mhz, js, false);
+    rc |= run<SUBB_MASK>(k, n_cu, clock_mhz, js, false);
     if (rc) return rc;
   }
   fprintf(js, "\n]}\n");
