@@ -178,11 +178,11 @@ lcpc_status lcpc_encode_rows_device(const lcpc_encoding *e, const void *d_src, s
  * encoded matrix, Merkle hashes) stays resident in HBM; `len` elements of host memory.  The rows
  * cross PCIe in ~8 MiB blocks on a copy stream, each block encoded as soon as it has landed;
  * page-locked memory (hipHostMalloc / hipHostRegister) is read by the DMA engine directly,
- * pageable memory (a Rust Vec) through two page-locked staging slots of the calling thread. */
+ * pageable memory (a Rust Vec) through the HIP runtime's own pageable path, block by block. */
 lcpc_status lcpc_commit_new(const lcpc_encoding *e, const uint64_t *coeffs, size_t len,
                             lcpc_commit **out);
 /* 1 if the calling thread's last host-input commit read a page-locked source directly, 0 if it
- * staged pageable memory (diagnostic) */
+ * took the pageable path (diagnostic) */
 int lcpc_last_upload_pinned(void);
 /* Same with the coefficients already in device memory (no PCIe transfer). */
 lcpc_status lcpc_commit_new_device(const lcpc_encoding *e, const void *d_coeffs, size_t len,
@@ -330,8 +330,8 @@ lcpc_status lcpc_pos_commit_bytes_device(const lcpc_encoding *e, const void *d_b
 /* The same commitment from a file image in HOST memory -- what the server has after reading the
  * file from disk on every proof request (networking/server.rs:670-679): the image crosses PCIe in
  * blocks of whole rows, and at the default dims each block is unpacked and encoded by the
- * one-pass kernel as soon as it has landed (pageable images through page-locked staging, as
- * lcpc_commit_new).  Any alignment. */
+ * one-pass kernel as soon as it has landed (page-locked or pageable, as lcpc_commit_new).  Any
+ * alignment. */
 lcpc_status lcpc_pos_commit_bytes(const lcpc_encoding *e, const uint8_t *bytes, size_t n_bytes,
                                   lcpc_commit **out);
 /* DataField::field_vec_to_byte_vec truncated to expected_len (data_field.rs:57-62,

@@ -87,17 +87,19 @@ lcpc_status make_sdig_encoding(int fid, int code, size_t n_per_row, size_t want_
 // each block handed to on_block(off, n) -- which queues the block's compute on `s` -- as soon as s
 // has been ordered after the block's copy: the DMA of block k + 1 overlaps the kernels of block k.
 // A page-locked source (hipHostMalloc / registered) is read by the DMA engine directly; a pageable
-// one goes through two of this thread's page-locked staging slots, the host filling one while the
-// engine drains the other (lcpc_commit_new's source is the caller's &[F], lcpc-2d/src/lib.rs:651:
-// normally pageable).  Returns with the copies queued; s is ordered after all of them.
+// one (lcpc_commit_new's source is the caller's &[F], lcpc-2d/src/lib.rs:651: normally pageable)
+// goes through the runtime's own pageable path, block by block (measured against staging it
+// through two page-locked slots of this thread: 40.5 / 40.8 against 38.9 / 40.2 GB/s at cfg3,
+// profiles/r06_h2d_pageable_ab.json).  Returns with the copies queued; s is ordered after all of
+// them.
 struct UploadStats {
   bool pinned = false;
   size_t blocks = 0;
 };
 inline thread_local UploadStats t_last_upload;
-// this thread's upload events (2 "block landed" + 2 "staging slot free"), per current device
+// this thread's upload events (one "block landed" event per block in flight), per current device
 struct UploadEvents {
-  hipEvent_t e[4] = {};
+  hipEvent_t e[2] = {};
   int dev = -1;
   ~UploadEvents() { reset(); }
   void reset() {
@@ -129,50 +131,25 @@ lcpc_status h2d_blocks(Device *dev, uint8_t *d_dst, const uint8_t *h_src, size_t
   t_last_upload = {};
   if (!bytes) return LCPC_OK;
   block = std::max<size_t>(block, 4096);
-  const bool pinned = host_dev_ptr(h_src) != nullptr;
-  t_last_upload.pinned = pinned;
-  // (A/B, round 6: LCPC_H2D_PAGEABLE=direct hands pageable blocks to the runtime's own
-  // pageable path instead of the staging slots)
-  static const bool direct = [] {
-    const char *v = getenv("LCPC_H2D_PAGEABLE");
-    return v && std::string(v) == "direct";
-  }();
-  const bool staged = !pinned && !direct;
-  uint8_t *stg[2] = {nullptr, nullptr};
-  if (staged) {
-    const size_t slot = std::min(block, bytes);
-    stg[0] = (uint8_t *)t_pin[PIN_STAGE].get(slot);
-    stg[1] = (uint8_t *)t_pin[PIN_STAGE2].get(slot);
-    if (!stg[0] || !stg[1]) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
-  }
+  t_last_upload.pinned = host_dev_ptr(h_src) != nullptr;
   if (!t_upload_ev.ready()) return fail(LCPC_ERR_DEVICE, "hipEventCreate");
-  hipEvent_t *landed = t_upload_ev.e, *slot_free = t_upload_ev.e + 2;
   hipStream_t cs = dev->acquire_stream(POOL_BULK);
   if (!cs) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   // (the copies stay queued on cs, and s waits on them: the stream goes back to the pool at once,
-  // work still queued on it ordered like any pooled stream's; the staging slots and events are
-  // this thread's, reused only after its caller drains s)
+  // work still queued on it ordered like any pooled stream's; the events are this thread's,
+  // reused only after its caller drains s)
   struct Release {
     Device *dev;
     hipStream_t cs;
     ~Release() { dev->release_stream(cs, POOL_BULK); }
   } rel{dev, cs};
-  bool used[2] = {false, false};
   size_t k = 0;
   for (size_t off = 0; off < bytes; off += block, k++) {
     const size_t n = std::min(block, bytes - off);
-    const int j = (int)(k & 1);
-    if (!staged) {
-      HIP_TRY(hipMemcpyAsync(d_dst + off, h_src + off, n, hipMemcpyHostToDevice, cs));
-    } else {
-      if (used[j]) HIP_TRY(hipEventSynchronize(slot_free[j]));  // its previous DMA has drained
-      std::memcpy(stg[j], h_src + off, n);
-      HIP_TRY(hipMemcpyAsync(d_dst + off, stg[j], n, hipMemcpyHostToDevice, cs));
-      HIP_TRY(hipEventRecord(slot_free[j], cs));
-      used[j] = true;
-    }
-    HIP_TRY(hipEventRecord(landed[j], cs));
-    HIP_TRY(hipStreamWaitEvent(s, landed[j], 0));
+    hipEvent_t landed = t_upload_ev.e[k & 1];
+    HIP_TRY(hipMemcpyAsync(d_dst + off, h_src + off, n, hipMemcpyHostToDevice, cs));
+    HIP_TRY(hipEventRecord(landed, cs));
+    HIP_TRY(hipStreamWaitEvent(s, landed, 0));
     lcpc_status st = on_block(off, n);
     if (st) return st;
   }

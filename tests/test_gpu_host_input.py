@@ -4,7 +4,7 @@ The reference's commit reads the caller's coefficients from host memory (`coeffs
 lcpc-2d/src/lib.rs:651-682), and the proof-of-storage server re-commits a file it has just read
 from disk on every proof request (networking/server.rs:670-679).  lcpc_commit_new /
 lcpc_pos_commit_bytes move the input across PCIe in row blocks on a copy stream, encoding each
-block as it lands; pageable memory is staged through page-locked slots, page-locked memory is read
+block as it lands; pageable memory takes the runtime's pageable path, page-locked memory is read
 by the DMA engine directly.  Every case must give the oracle's commitment bit for bit, and the
 same one as the device-resident entry points.
 """

@@ -39,7 +39,7 @@
 constexpr int ITERS = 16384;
 
 enum Mode { MAD = 0, ADDC, ADDCO, CND, MOV, ADD32, NOP_PAIR, HAZARD, NOP_ONLY, CND_SGPR, CND_CMP, BFI, SUBB_MASK,
-            N_MODES };
+            ADD32_E64, ADD32_LIT, CHAIN_VCC, MAD_VCC_CHAIN, N_MODES };
 static const char *NAMES[N_MODES] = {
     "v_mad_u64_u32",
     "v_addc_co_u32 (independent SGPR carries)",
@@ -54,10 +54,14 @@ static const char *NAMES[N_MODES] = {
     "v_cmp_gt_u32 + v_cndmask_b32 (vcc just written)",
     "v_bfi_b32 (VGPR mask select)",
     "v_subb_co_u32 (0 - borrow: a VGPR mask)",
+    "v_add_u32_e64 (the same add, 8-byte encoding)",
+    "v_add_u32_e32 + 32-bit literal (8 bytes)",
+    "carry chain through VCC, e32 forms (4 bytes)",
+    "mad_u64 (carry to VCC) + v_addc_co_u32_e32 fold",
 };
 // instructions (VALU + s_nop) per stream per iteration, and VALU ones among them
-static const int INSTR[N_MODES] = {1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 2, 1, 1};
-static const int VALU[N_MODES] = {1, 1, 1, 1, 1, 1, 1, 1, 0, 1, 2, 1, 1};
+static const int INSTR[N_MODES] = {1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 2, 1, 1, 1, 1, 1, 2};
+static const int VALU[N_MODES] = {1, 1, 1, 1, 1, 1, 1, 1, 0, 1, 2, 1, 1, 1, 1, 1, 2};
 
 struct WaveRec {
   uint64_t cycles;
@@ -183,6 +187,40 @@ __global__ __launch_bounds__(256) void k_issue(WaveRec *rec, uint32_t seed) {
           "v_bfi_b32 %6, %14, %6, %15\n\tv_bfi_b32 %7, %15, %7, %8"
           : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)
           : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]));
+    } else if constexpr (MODE == ADD32_E64) {
+      asm volatile(
+          "v_add_u32_e64 %0, %0, %8\n\tv_add_u32_e64 %1, %1, %9\n\tv_add_u32_e64 %2, %2, %10\n\tv_add_u32_e64 %3, %3, %11\n\t"
+          "v_add_u32_e64 %4, %4, %12\n\tv_add_u32_e64 %5, %5, %13\n\tv_add_u32_e64 %6, %6, %14\n\tv_add_u32_e64 %7, %7, %15"
+          : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)
+          : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]));
+    } else if constexpr (MODE == ADD32_LIT) {
+      asm volatile(
+          "v_add_u32 %0, 0x12345, %0\n\tv_add_u32 %1, 0x12346, %1\n\tv_add_u32 %2, 0x12347, %2\n\tv_add_u32 %3, 0x12348, %3\n\t"
+          "v_add_u32 %4, 0x12349, %4\n\tv_add_u32 %5, 0x1234a, %5\n\tv_add_u32 %6, 0x1234b, %6\n\tv_add_u32 %7, 0x1234c, %7"
+          : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7));
+    } else if constexpr (MODE == CHAIN_VCC) {  // two 4-limb additions, carries in VCC (e32)
+      asm volatile(
+          "v_add_co_u32_e32 %0, vcc, %0, %8\n\tv_addc_co_u32_e32 %1, vcc, %1, %9, vcc\n\t"
+          "v_addc_co_u32_e32 %2, vcc, %2, %10, vcc\n\tv_addc_co_u32_e32 %3, vcc, %3, %11, vcc\n\t"
+          "v_add_co_u32_e32 %4, vcc, %4, %12\n\tv_addc_co_u32_e32 %5, vcc, %5, %13, vcc\n\t"
+          "v_addc_co_u32_e32 %6, vcc, %6, %14, vcc\n\tv_addc_co_u32_e32 %7, vcc, %7, %15, vcc"
+          : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)
+          : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7])
+          : "vcc");
+    } else if constexpr (MODE == MAD_VCC_CHAIN) {  // product scanning with the carry folded via VCC
+      asm volatile(
+          "v_mad_u64_u32 %0, vcc, %8, %16, %0\n\tv_addc_co_u32_e32 %9, vcc, 0, %9, vcc\n\t"
+          "v_mad_u64_u32 %1, vcc, %10, %17, %1\n\tv_addc_co_u32_e32 %11, vcc, 0, %11, vcc\n\t"
+          "v_mad_u64_u32 %2, vcc, %12, %18, %2\n\tv_addc_co_u32_e32 %13, vcc, 0, %13, vcc\n\t"
+          "v_mad_u64_u32 %3, vcc, %14, %19, %3\n\tv_addc_co_u32_e32 %15, vcc, 0, %15, vcc\n\t"
+          "v_mad_u64_u32 %4, vcc, %8, %20, %4\n\tv_addc_co_u32_e32 %9, vcc, 0, %9, vcc\n\t"
+          "v_mad_u64_u32 %5, vcc, %10, %21, %5\n\tv_addc_co_u32_e32 %11, vcc, 0, %11, vcc\n\t"
+          "v_mad_u64_u32 %6, vcc, %12, %22, %6\n\tv_addc_co_u32_e32 %13, vcc, 0, %13, vcc\n\t"
+          "v_mad_u64_u32 %7, vcc, %14, %23, %7\n\tv_addc_co_u32_e32 %15, vcc, 0, %15, vcc"
+          : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]),
+            "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
+          : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7])
+          : "vcc");
     } else {
       asm volatile(
           "v_subb_co_u32 %0, s[40:41], 0, %8, s[40:41]\n\tv_subb_co_u32 %1, s[42:43], 0, %9, s[42:43]\n\t"
@@ -303,6 +341,10 @@ int main(int argc, char **argv) {
     rc |= run<CND_CMP>(k, n_cu, clock_mhz, js, false);
     rc |= run<BFI>(k, n_cu, clock_mhz, js, false);
     rc |= run<SUBB_MASK>(k, n_cu, clock_mhz, js, false);
+    rc |= run<ADD32_E64>(k, n_cu, clock_mhz, js, false);
+    rc |= run<ADD32_LIT>(k, n_cu, clock_mhz, js, false);
+    rc |= run<CHAIN_VCC>(k, n_cu, clock_mhz, js, false);
+    rc |= run<MAD_VCC_CHAIN>(k, n_cu, clock_mhz, js, false);
     if (rc) return rc;
   }
   fprintf(js, "\n]}\n");
