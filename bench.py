@@ -796,6 +796,17 @@ def roofline_objects(wl, iso, stats, args, traffic_rows_frac=1.0):
         if field == "Ft127" and ach:
             out["roofline_valu"]["mad_issue_peak"] = 20600.0 / 28
             out["roofline_valu"]["frac_of_mad_issue_peak"] = ach / (20600.0 / 28)
+        # the passes against the issue floor of their own instruction stream (round 6 model:
+        # per-class issue costs x instruction counts, tools/encode_cycle_model.py)
+        fpath = os.path.join(ROOT, "profiles", "issue_floor_encode.json")
+        try:
+            fl = json.load(open(fpath))
+            if (fl.get("config_len"), fl.get("field"), fl.get("code")) == wl.traffic_key and traffic_rows_frac == 1.0:
+                out["roofline_valu"]["issue_floor"] = {
+                    "frac": fl["frac_of_issue_floor"], "model_ms": fl["model_ms"], "measured_ms": fl["measured_ms"],
+                    "source": os.path.relpath(fpath, ROOT)}
+        except (OSError, ValueError, KeyError):
+            pass
     gb = getattr(wl, "gather_bytes", 0)
     if gb and enc_ms:
         # Brakedown: the levels gather every nonzero's input run (R rows) from HBM -- an expander

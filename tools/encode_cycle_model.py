@@ -13,7 +13,9 @@ Inputs (all measured on MI355X, committed under profiles/):
 
 Model: time = (waves / 1024 SIMDs) x sum_class(static count x cost) x (dynamic / static VALU).
 
-    python tools/encode_cycle_model.py ISSUE_COST.json PMC_DIR TRACE_STATS.csv [OUT.txt]
+    python tools/encode_cycle_model.py ISSUE_COST.json PMC_DIR TRACE_STATS.csv [OUT.txt [OUT.json]]
+
+OUT.json (profiles/issue_floor_encode.json) is what bench.py quotes in roofline_valu.issue_floor.
 """
 import collections
 import csv
@@ -120,6 +122,15 @@ def main():
     tot_meas = sum(dur.values())
     print(f"encode: model {tot_model:.3f} ms, measured {tot_meas:.3f} ms: the passes run at "
           f"{tot_model / tot_meas:.0%} of their VALU issue floor", file=out)
+    if len(sys.argv) > 5:
+        json.dump({"config_len": 1 << 24, "field": "Ft127", "code": "ligero",
+                   "model_ms": {k: round(v, 4) for k, v in res.items()},
+                   "measured_ms": {k: round(v, 4) for k, v in dur.items()},
+                   "frac_of_issue_floor": round(tot_model / tot_meas, 3),
+                   "source": "tools/encode_cycle_model.py: per-class issue cost at 4 waves/SIMD "
+                             "(tools/microbench/issue_cost.hip) x the passes' instruction counts x their dynamic VALU "
+                             "count (SQ_INSTS_VALU), against the fastest traced launch; profiles/r06_encode_cycle_model.txt"},
+                  open(sys.argv[5], "w"), indent=1)
 
 
 if __name__ == "__main__":
