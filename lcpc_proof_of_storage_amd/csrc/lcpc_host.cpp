@@ -141,15 +141,23 @@ lcpc_status h2d_blocks(Device *dev, uint8_t *d_dst, const uint8_t *h_src, size_t
   struct Release {
     Device *dev;
     hipStream_t cs;
-    ~Release() { dev->release_stream(cs, POOL_BULK); }
+    bool ordered = false;  // s waits on every copy queued so far
+    ~Release() {
+      // an early return may leave a copy that s never waited on: it writes a buffer the caller
+      // releases with a fence on s alone, so drain it here
+      if (!ordered) (void)hipStreamSynchronize(cs);
+      dev->release_stream(cs, POOL_BULK);
+    }
   } rel{dev, cs};
   size_t k = 0;
   for (size_t off = 0; off < bytes; off += block, k++) {
     const size_t n = std::min(block, bytes - off);
     hipEvent_t landed = t_upload_ev.e[k & 1];
+    rel.ordered = false;
     HIP_TRY(hipMemcpyAsync(d_dst + off, h_src + off, n, hipMemcpyHostToDevice, cs));
     HIP_TRY(hipEventRecord(landed, cs));
     HIP_TRY(hipStreamWaitEvent(s, landed, 0));
+    rel.ordered = true;
     lcpc_status st = on_block(off, n);
     if (st) return st;
   }
