@@ -737,24 +737,36 @@ def sharded_commit_prove_many(enc, comm: NativeComm, d_rows: Sequence[int], n_ro
                               lag: int = 0, keep_proofs: bool = True):
     """lcpc_sharded_commit_prove_many: pipelined commit + prove of len(d_rows) polynomials.
 
-    make_transcript(i, root) -> Transcript for polynomial i (called on its root rank, i % world);
-    returns (roots, proofs) with proofs[i] an LcEvalProof on the root rank of i, else None."""
+    make_transcript(i, root) -> the transcript for polynomial i (called on its root rank, i % world):
+    the library's Transcript, or the caller's own transcript object (CallerTranscript: its proof's
+    absorbs and squeezes go to it); returns (roots, proofs) with proofs[i] an LcEvalProof on the
+    root rank of i, else None."""
     from . import _native as N
-    from .lcpc2d import LcEvalProof, _elems
+    from .lcpc2d import CallerTranscript, LcEvalProof, Transcript, _elems, _transcript
     L = _lib()
     n = len(d_rows)
     o = np.ascontiguousarray(_elems(outer, enc.field))
     rows = (C.c_void_p * max(n, 1))(*[C.c_void_p(p) for p in d_rows])
     proofs = (C.c_void_p * max(n, 1))()
     roots = (C.c_uint8 * max(32 * n, 1))()
+    callers = []  # caller transcripts (their callbacks) live until the call returns
 
     def mk(user, i, root):
         tr = make_transcript(int(i), bytes(root[:32]))
-        return L.lcpc_transcript_clone(tr._h)  # the library owns (and frees) the clone
+        if isinstance(tr, Transcript):
+            return L.lcpc_transcript_clone(tr._h)  # the library owns (and frees) the clone
+        ct = _transcript(tr)
+        callers.append(ct)
+        # a second ops handle over the same callbacks: the library owns (and frees) it
+        return L.lcpc_transcript_from_ops(C.byref(ct._ops))
 
     cb = N.MAKE_TRANSCRIPT_FN(mk)
-    _check(L.lcpc_sharded_commit_prove_many(enc._h, rows, n, n_rows, o.ctypes.data_as(C.POINTER(C.c_uint64)),
-                                            comm._h, cb, None, lag, proofs if keep_proofs else None, roots))
+    rc = L.lcpc_sharded_commit_prove_many(enc._h, rows, n, n_rows, o.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                          comm._h, cb, None, lag, proofs if keep_proofs else None, roots)
+    for ct in callers:
+        if isinstance(ct, CallerTranscript):
+            ct.reraise(rc)
+    _check(rc)
     rb = bytes(roots)
     return ([rb[32 * i:32 * i + 32] for i in range(n)],
             [LcEvalProof(proofs[i]) if proofs[i] else None for i in range(n)])

@@ -221,3 +221,32 @@ def test_sharded_prove_over_caller_transcript(gpu, oracle, hipmem):
         del sc
     finally:
         hipmem.free(d)
+
+
+def test_pipelined_driver_over_caller_transcripts(gpu, oracle, hipmem):
+    """lcpc_sharded_commit_prove_many (one rank): each polynomial's proof on the caller's own
+    transcript -- the same proofs and end states as the oracle's."""
+    from lcpc_proof_of_storage_amd import shard
+    fid, n_per_row, n_cols, nco, ndt = 1, 256, 512, 24, 2
+    enc = gpu.RsEncoding.new(fid, n_per_row, n_cols, nco, ndt)
+    o_enc = oracle.Encoding.ligero(fid, n_per_row, n_cols, nco, ndt)
+    n_rows = 16
+    polys = [rand_elems(oracle, fid, n_rows * n_per_row, 31 + k) for k in range(3)]
+    outer = rand_elems(oracle, fid, n_rows, 32)
+    ds = [hipmem.to_device(p) for p in polys]
+    made = {}
+    try:
+        def make_tr(i, root):
+            made[i] = _prefix(CountingOracleTranscript(oracle), root, nco)
+            return made[i]
+
+        roots, proofs = shard.sharded_commit_prove_many(enc, shard.NativeComm.single(), ds, n_rows, outer, make_tr)
+        for i, p in enumerate(polys):
+            o = oracle.Commit(o_enc, p)
+            assert roots[i] == o.root()
+            o_tr = oracle.standard_transcript(nco, o.root())
+            _same_proof(proofs[i], o.prove(o_enc, outer, o_tr), oracle)
+            assert made[i].challenge_bytes(b"after", 32) == o_tr.challenge_bytes(b"after", 32)
+    finally:
+        for d in ds:
+            hipmem.free(d)
