@@ -9,12 +9,13 @@ row-combination coefficient, 309 column openings with Merkle paths): lcpc-2d/src
 and :1034-1123, dims 512 x 32768 -> 65536 (rho = 1/2, lcpc-ligero-pc/src/lib.rs:70-112).
 
 Engines (--mode; the default, auto, is sharded for --gpus > 1 and replicas on one GPU):
-  sharded (cfg3): every step is ONE commitment whose rows are split over the N ranks
-    (one process per GPU, RCCL over xGMI through liblcpc_mi's own communicator), run by the
-    library's pipelined driver lcpc_sharded_commit_prove_many (csrc/shard_native.cpp): the
-    exchanges of the steps in flight go out in one fixed order per tick, the transcript of step
-    i runs on rank i % N.  At N = 1 the same driver runs with no exchanges.  "scaling": "strong"
-    (the work of a step is fixed as N grows).
+  sharded (cfg3): every commitment's rows are split over the N ranks (one process per GPU,
+    RCCL over xGMI through liblcpc_mi's own communicator), run by the library's pipelined driver
+    lcpc_sharded_commit_prove_many (csrc/shard_native.cpp): the exchanges of the commitments in
+    flight go out in one fixed order per tick, the transcript of commitment i runs on rank i % N.
+    At N = 1 the same driver runs with no exchanges.  --sharded-scaling weak (default): a step is
+    N commitments (one commitment's work per GPU per step, "scaling": "weak"); strong: a step is
+    one commitment whatever N ("scaling": "strong", the round-5 line).
   replicas: every rank commits and opens its own polynomial (independent objects), host
     threads keep --pipeline commitments in flight; "scaling": "weak".
 
@@ -61,6 +62,11 @@ def parse():
                          "(the N = 1 base of the sharded N > 1 lines) and report it as \"sharded_n1\": "
                          "1 in a fresh child process (as an N > 1 rank starts), 2 in this process after "
                          "the replicas run, 0 off")
+    ap.add_argument("--sharded-scaling", choices=["weak", "strong"], default="weak",
+                    help="sharded engine: weak (default) = N row-sharded commitments per step, so each GPU "
+                         "does one commitment's work per step at every N; strong = one commitment per step "
+                         "(K = 20 then holds 20 commitments at every N, and the last one's serial "
+                         "transcript dominates an N = 8 run: DESIGN §6)")
     ap.add_argument("--lag", type=int, default=0,
                     help="sharded driver: ticks between a row-combination gather and the next challenge "
                          "broadcast (0: the library's choice)")
@@ -1073,10 +1079,13 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
     def barrier():
         sync_barrier(dist, torch.cuda.synchronize)
 
+    # commitments per step: N (weak scaling: one commitment's work per GPU per step) or 1 (strong)
+    pps = world if args.sharded_scaling == "weak" else 1
+    n_timed = args.steps * pps
     # the pools the timed run's pipeline depth needs (buffers, page-locked staging, streams: not
     # steps), then the warm-up (RCCL connections); polynomial 0's proof is kept on rank 0
-    S["reserve"](max(args.steps, args.warmup))
-    roots, proofs = S["run"](max(1, args.warmup), keep=True)
+    S["reserve"](max(args.steps, args.warmup) * pps)
+    roots, proofs = S["run"](max(1, args.warmup) * pps, keep=True)
     warm_proof = proofs[0]
     assert all(r == roots[0] for r in roots), "nondeterministic root across steps"
     prof_timed = args.prof_timed and not args.no_prof
@@ -1085,14 +1094,14 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
     barrier()
     t0 = time.perf_counter()
     c0, th0 = os.times(), cgroup_throttle()
-    troots, _ = S["run"](args.steps)
+    troots, _ = S["run"](n_timed)
     barrier()
     elapsed = time.perf_counter() - t0
     c1, th1 = os.times(), cgroup_throttle()
     L.prof_enable(False)
     stats = L.prof_stats() if prof_timed else {}
     # recorded, not asserted: the line still prints, and main() exits non-zero on a mismatch
-    steps_agree = len(troots) == args.steps and all(r == roots[0] for r in list(troots) + list(roots))
+    steps_agree = len(troots) == n_timed and all(r == roots[0] for r in list(troots) + list(roots))
     elapsed = max_over_ranks(dist, elapsed, "cpu" if backend == "gloo" else device)
 
     # one commitment's latency (serial, median of 3) and the roofline launches (HIP events on the
@@ -1117,11 +1126,12 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
         iso = L.prof_stats()
     lat_c.sort()
     lat_p.sort()
-    value = job_throughput(n, args.steps, 1, elapsed)
+    value = job_throughput(n, args.steps, pps, elapsed)
     out = {
         "metric": "committed field-elements/s (commit+open), 2^24-coeff Ligero, 1/2/4/8 GPU" + rho_note(args),
         "value": value, "unit": "field-elements/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": "strong",
+        "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": args.sharded_scaling,
+        "commitments_per_step": pps, "commitments_timed": n_timed,
         "vs_baseline": None, "dtype": f"u64x{B // 8} ({args.field} Montgomery limbs)",
         "data": f"synthetic: F::random(ChaCha20Rng::seed_from_u64({SEED:#x})), one polynomial, each rank's rows "
                 f"resident in its HBM",
@@ -1129,8 +1139,9 @@ def run_sharded(args, L, torch, dist, rank, world, device, backend, share):
                                f"{n_per_row}->{n_cols}, {nco} column opens, {ndt} degree tests, BLAKE3 Merkle",
                    "field": args.field, "len": n, "n_rows": n_rows, "n_per_row": n_per_row, "n_cols": n_cols,
                    "n_col_opens": nco, "n_degree_tests": ndt,
-                   "parallelism": (f"rows sharded x{world} (one commitment per step; lcpc_sharded_commit_prove_many, "
-                                   f"transcript of step i on rank i % {world})" if world > 1 else
+                   "parallelism": (f"rows sharded x{world} ({pps} commitment{'s' if pps > 1 else ''} per step, each "
+                                   f"row-sharded over all {world} ranks; lcpc_sharded_commit_prove_many, "
+                                   f"transcript of commitment i on rank i % {world})" if world > 1 else
                                    "one GPU (lcpc_sharded_commit_prove_many with one rank: pipelined steps)"),
                    "exchanges": S["comm_kind"], "lag": args.lag or None, "rows_on_rank0": nr},
         "mb_per_s": value * B / 1e6,

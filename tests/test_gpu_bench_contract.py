@@ -53,7 +53,7 @@ def test_bench_ligero_sharded_small(gpu):
     assert d["verify"]["parity_vs_oracle"] is True and d["verify"]["ms"] > 0
     assert d["config"]["n_rows"] * d["config"]["n_per_row"] == 1 << 16
     # the sharded driver line: the kept proof equals the oracle's, one commitment's latency
-    assert d["scaling"] == "strong" and d["parity_proof_vs_oracle"] is True
+    assert d["scaling"] == "weak" and d["commitments_per_step"] == 1 and d["parity_proof_vs_oracle"] is True
     assert d["latency"]["commit_ms"] > 0 and d["latency"]["prove_ms"] > 0
     assert "traffic_source" in d["roofline"] and d["world_formed"] == 1
     assert d["parity_ok"] is True and d["steps_agree"] is True
@@ -119,10 +119,14 @@ def _check_self_checking(d, world):
     N = 1 line's: at N > 1 the oracle runs once, as the checker)"""
     # one GPU box: the ranks share GPU 0 (the rehearsal), and the line says so rank by rank
     assert d["devices"] == [0] * world and d["rehearsal"] is True and len(d["ranks"]) == world
-    assert d["n_gpus"] == world and d["world_formed"] == world and d["scaling"] == "strong"
+    assert d["n_gpus"] == world and d["world_formed"] == world
+    # weak (the default): N row-sharded commitments per step; strong: one
+    pps = world if d["scaling"] == "weak" else 1
+    assert d["scaling"] in ("weak", "strong") and d["commitments_per_step"] == pps
+    assert d["commitments_timed"] == d["steps"] * pps
     assert d["parity_root_vs_oracle"] is True and d["parity_proof_vs_oracle"] is True
     ps = d["parity_steps_vs_oracle"]
-    assert ps["steps"] == d["steps"] + d["warmup"] and ps["equal"] == ps["steps"]
+    assert ps["steps"] == (d["steps"] + d["warmup"]) * pps and ps["equal"] == ps["steps"]
     assert d["steps_agree"] is True and d["parity_ok"] is True
     assert d["verify"]["parity_vs_oracle"] is True
     assert "cpu_baseline" not in d
@@ -134,7 +138,16 @@ def test_bench_sharded_two_ranks_one_gpu(gpu):
     host-staged gloo collectives (RCCL refuses two ranks on one device)."""
     d = _bench_ranks(2, {}, "--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1")
     _check_self_checking(d, 2)
-    assert "gloo" in d["config"]["exchanges"]
+    assert "gloo" in d["config"]["exchanges"] and d["scaling"] == "weak"
+
+
+@pytest.mark.timeout(300)
+def test_bench_sharded_two_ranks_one_gpu_strong(gpu):
+    """--sharded-scaling strong: one commitment per step at every N (the round-5 line)"""
+    d = _bench_ranks(2, {}, "--steps", "4", "--warmup", "2", "--log-len", "16", "--verify-reps", "1",
+                     "--sharded-scaling", "strong")
+    _check_self_checking(d, 2)
+    assert d["scaling"] == "strong"
 
 
 @pytest.mark.timeout(300)

@@ -39,7 +39,7 @@
 constexpr int ITERS = 16384;
 
 enum Mode { MAD = 0, ADDC, ADDCO, CND, MOV, ADD32, NOP_PAIR, HAZARD, NOP_ONLY, CND_SGPR, CND_CMP, BFI, SUBB_MASK,
-            ADD32_E64, ADD32_LIT, CHAIN_VCC, MAD_VCC_CHAIN, N_MODES };
+            ADD32_E64, ADD32_LIT, CHAIN_VCC, MAD_VCC_CHAIN, XOR32, ALIGNBIT, ADD3, PERM, BITOP3, N_MODES };
 static const char *NAMES[N_MODES] = {
     "v_mad_u64_u32",
     "v_addc_co_u32 (independent SGPR carries)",
@@ -58,10 +58,15 @@ static const char *NAMES[N_MODES] = {
     "v_add_u32_e32 + 32-bit literal (8 bytes)",
     "carry chain through VCC, e32 forms (4 bytes)",
     "mad_u64 (carry to VCC) + v_addc_co_u32_e32 fold",
+    "v_xor_b32",
+    "v_alignbit_b32 (rotate)",
+    "v_add3_u32",
+    "v_perm_b32",
+    "v_bitop3_b32 (3-input xor)",
 };
 // instructions (VALU + s_nop) per stream per iteration, and VALU ones among them
-static const int INSTR[N_MODES] = {1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 2, 1, 1, 1, 1, 1, 2};
-static const int VALU[N_MODES] = {1, 1, 1, 1, 1, 1, 1, 1, 0, 1, 2, 1, 1, 1, 1, 1, 2};
+static const int INSTR[N_MODES] = {1, 1, 1, 1, 1, 1, 2, 2, 1, 1, 2, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1};
+static const int VALU[N_MODES] = {1, 1, 1, 1, 1, 1, 1, 1, 0, 1, 2, 1, 1, 1, 1, 1, 2, 1, 1, 1, 1, 1};
 
 struct WaveRec {
   uint64_t cycles;
@@ -221,6 +226,30 @@ __global__ __launch_bounds__(256) void k_issue(WaveRec *rec, uint32_t seed) {
             "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
           : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7])
           : "vcc");
+    } else if constexpr (MODE == XOR32 || MODE == ALIGNBIT || MODE == ADD3 || MODE == PERM || MODE == BITOP3) {
+#define OP3(OPS)                                                                                              \
+  asm volatile(OPS : V8(0), V8(1), V8(2), V8(3), V8(4), V8(5), V8(6), V8(7)                                  \
+               : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]))
+      if constexpr (MODE == XOR32)
+        OP3("v_xor_b32 %0, %0, %8\n\tv_xor_b32 %1, %1, %9\n\tv_xor_b32 %2, %2, %10\n\tv_xor_b32 %3, %3, %11\n\t"
+            "v_xor_b32 %4, %4, %12\n\tv_xor_b32 %5, %5, %13\n\tv_xor_b32 %6, %6, %14\n\tv_xor_b32 %7, %7, %15");
+      else if constexpr (MODE == ALIGNBIT)
+        OP3("v_alignbit_b32 %0, %0, %0, 12\n\tv_alignbit_b32 %1, %1, %1, 12\n\tv_alignbit_b32 %2, %2, %2, 12\n\t"
+            "v_alignbit_b32 %3, %3, %3, 12\n\tv_alignbit_b32 %4, %4, %4, 12\n\tv_alignbit_b32 %5, %5, %5, 12\n\t"
+            "v_alignbit_b32 %6, %6, %6, 12\n\tv_alignbit_b32 %7, %7, %7, 12");
+      else if constexpr (MODE == ADD3)
+        OP3("v_add3_u32 %0, %0, %8, %9\n\tv_add3_u32 %1, %1, %9, %10\n\tv_add3_u32 %2, %2, %10, %11\n\t"
+            "v_add3_u32 %3, %3, %11, %12\n\tv_add3_u32 %4, %4, %12, %13\n\tv_add3_u32 %5, %5, %13, %14\n\t"
+            "v_add3_u32 %6, %6, %14, %15\n\tv_add3_u32 %7, %7, %15, %8");
+      else if constexpr (MODE == PERM)
+        OP3("v_perm_b32 %0, %0, %0, %8\n\tv_perm_b32 %1, %1, %1, %8\n\tv_perm_b32 %2, %2, %2, %8\n\t"
+            "v_perm_b32 %3, %3, %3, %8\n\tv_perm_b32 %4, %4, %4, %8\n\tv_perm_b32 %5, %5, %5, %8\n\t"
+            "v_perm_b32 %6, %6, %6, %8\n\tv_perm_b32 %7, %7, %7, %8");
+      else
+        OP3("v_bitop3_b32 %0, %0, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %9, %10 bitop3:0x96\n\tv_bitop3_b32 %2, %2, %10, %11 bitop3:0x96\n\t"
+            "v_bitop3_b32 %3, %3, %11, %12 bitop3:0x96\n\tv_bitop3_b32 %4, %4, %12, %13 bitop3:0x96\n\tv_bitop3_b32 %5, %5, %13, %14 bitop3:0x96\n\t"
+            "v_bitop3_b32 %6, %6, %14, %15 bitop3:0x96\n\tv_bitop3_b32 %7, %7, %15, %8 bitop3:0x96");
+#undef OP3
     } else {
       asm volatile(
           "v_subb_co_u32 %0, s[40:41], 0, %8, s[40:41]\n\tv_subb_co_u32 %1, s[42:43], 0, %9, s[42:43]\n\t"
@@ -345,6 +374,11 @@ int main(int argc, char **argv) {
     rc |= run<ADD32_LIT>(k, n_cu, clock_mhz, js, false);
     rc |= run<CHAIN_VCC>(k, n_cu, clock_mhz, js, false);
     rc |= run<MAD_VCC_CHAIN>(k, n_cu, clock_mhz, js, false);
+    rc |= run<XOR32>(k, n_cu, clock_mhz, js, false);
+    rc |= run<ALIGNBIT>(k, n_cu, clock_mhz, js, false);
+    rc |= run<ADD3>(k, n_cu, clock_mhz, js, false);
+    rc |= run<PERM>(k, n_cu, clock_mhz, js, false);
+    rc |= run<BITOP3>(k, n_cu, clock_mhz, js, false);
     if (rc) return rc;
   }
   fprintf(js, "\n]}\n");

@@ -1,5 +1,6 @@
-"""shard_model.py -- expected ms/step of the row-sharded cfg3 line (bench.py --gpus N, the driver's
-K = 20, W = 5) for N = 1, 2, 4, 8, from the pipelined driver's schedule and measured per-step costs.
+"""shard_model.py -- expected throughput of the row-sharded cfg3 line (bench.py --gpus N, the driver's
+K = 20, W = 5) for N = 1, 2, 4, 8, from the pipelined driver's schedule and measured per-step costs:
+strong (K commitments at every N) and weak (the bench's default: K steps of N commitments).
 
 The schedule (csrc/shard_native.cpp make_sched, replayed here and checked against the library's
 own lcpc_sharded_p2p_schedule in tests/test_shard_schedule.py): polynomial k's stage s goes out in
@@ -80,12 +81,18 @@ def predict(G, K=K_DEFAULT, lag=0):
 
 
 def main():
+    """strong: K commitments at every N (bench.py --sharded-scaling strong); weak (the bench's
+    default): K steps of N commitments, each row-sharded over all N ranks"""
     K = int(sys.argv[1]) if len(sys.argv) > 1 else K_DEFAULT
-    rows = [predict(G, K) for G in (1, 2, 4, 8)]
-    base = rows[0]["G_elements_per_s"]
-    for r in rows:
-        r["speedup_vs_1"] = r["G_elements_per_s"] / base
-    print(json.dumps(rows, indent=1))
+    base = predict(1, K)["G_elements_per_s"]
+    out = {}
+    for scaling in ("strong", "weak"):
+        rows = [predict(G, K if scaling == "strong" else K * G) for G in (1, 2, 4, 8)]
+        for r in rows:
+            r["speedup_vs_1"] = r["G_elements_per_s"] / base
+            r["efficiency"] = r["speedup_vs_1"] / r["G"]
+        out[scaling] = rows
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
