@@ -1,0 +1,153 @@
+// b3rot.hip -- BLAKE3 compression throughput on gfx950 with three ways to do the G function's
+// byte-aligned rotations (compute only, messages in registers, the leaf kernel's grid shape):
+//   0  every rotation by v_alignbit_b32 (what __builtin_rotateright32 gives; the library today)
+//   1  rotr 16 and rotr 8 by v_perm_b32 after the xor
+//   2  rotr 16 fused into the xor as two SDWA word xors (dst_sel WORD_1 / WORD_0)
+// Every variant's chaining values are checked against variant 0.
+// Build: hipcc -O3 -std=c++20 --offload-arch=gfx950 b3rot.hip -o b3rot
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+constexpr uint32_t IV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
+                            0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
+
+__host__ __device__ constexpr int sched(int r, int i) {
+  constexpr int P[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+  int x = i;
+  for (int k = 0; k < r; k++) x = P[x];
+  return x;
+}
+
+template <int V>
+__device__ __forceinline__ uint32_t xr16(uint32_t d, uint32_t a) {
+  if constexpr (V == 0) {
+    return __builtin_rotateright32(d ^ a, 16);
+  } else if constexpr (V == 1) {
+    return __builtin_amdgcn_perm(d ^ a, d ^ a, 0x01000302u);
+  } else {
+    uint32_t r;
+    asm volatile(
+        "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n\t"
+        "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1"
+        : "=&v"(r)
+        : "v"(d), "v"(a));
+    return r;
+  }
+}
+template <int V>
+__device__ __forceinline__ uint32_t xr8(uint32_t d, uint32_t a) {
+  if constexpr (V == 1) return __builtin_amdgcn_perm(d ^ a, d ^ a, 0x00030201u);
+  return __builtin_rotateright32(d ^ a, 8);
+}
+
+template <int V>
+__device__ __forceinline__ void g(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t mx, uint32_t my) {
+  a = a + b + mx;
+  d = xr16<V>(d, a);
+  c = c + d;
+  b = __builtin_rotateright32(b ^ c, 12);
+  a = a + b + my;
+  d = xr8<V>(d, a);
+  c = c + d;
+  b = __builtin_rotateright32(b ^ c, 7);
+}
+
+template <int V>
+__device__ __forceinline__ void compress(uint32_t cv[8], const uint32_t m[16], uint32_t counter, uint32_t flags) {
+  uint32_t s[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7],
+                    IV[0], IV[1], IV[2], IV[3], counter, 0u, 64u, flags};
+#pragma unroll
+  for (int r = 0; r < 7; r++) {
+    g<V>(s[0], s[4], s[8], s[12], m[sched(r, 0)], m[sched(r, 1)]);
+    g<V>(s[1], s[5], s[9], s[13], m[sched(r, 2)], m[sched(r, 3)]);
+    g<V>(s[2], s[6], s[10], s[14], m[sched(r, 4)], m[sched(r, 5)]);
+    g<V>(s[3], s[7], s[11], s[15], m[sched(r, 6)], m[sched(r, 7)]);
+    g<V>(s[0], s[5], s[10], s[15], m[sched(r, 8)], m[sched(r, 9)]);
+    g<V>(s[1], s[6], s[11], s[12], m[sched(r, 10)], m[sched(r, 11)]);
+    g<V>(s[2], s[7], s[8], s[13], m[sched(r, 12)], m[sched(r, 13)]);
+    g<V>(s[3], s[4], s[9], s[14], m[sched(r, 14)], m[sched(r, 15)]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) cv[i] = s[i] ^ s[i + 8];
+}
+
+// one thread = one (column, chunk): 16 compressions, as the leaf kernel's interior chunks
+template <int V>
+__global__ __launch_bounds__(256) void k_chunks(uint32_t *__restrict__ out, size_t n_cols, int n_chunks) {
+  const size_t col = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int chunk = 1 + blockIdx.y;
+  if (col >= n_cols || chunk > n_chunks) return;
+  uint32_t cv[8], msg[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) cv[i] = IV[i];
+#pragma unroll
+  for (int i = 0; i < 16; i++) msg[i] = (uint32_t)col * 0x9E3779B9u + i * 77 + chunk;
+  for (int b = 0; b < 16; b++) {
+    compress<V>(cv, msg, (uint32_t)chunk, b == 0 ? 1u : b == 15 ? 2u : 0u);
+    msg[b & 15] ^= cv[b & 7];
+  }
+  uint4 *o = reinterpret_cast<uint4 *>(out + ((size_t)(chunk - 1) * n_cols + col) * 8);
+  o[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+  o[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+}
+
+template <int V>
+static double run(uint32_t *d, size_t n_cols, int n_chunks, int reps) {
+  dim3 grid((unsigned)((n_cols + 255) / 256), (unsigned)n_chunks);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  hipLaunchKernelGGL(k_chunks<V>, grid, dim3(256), 0, 0, d, n_cols, n_chunks);
+  CK(hipGetLastError());
+  CK(hipEventRecord(a, 0));
+  for (int i = 0; i < reps; i++) hipLaunchKernelGGL(k_chunks<V>, grid, dim3(256), 0, 0, d, n_cols, n_chunks);
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  return ms / reps;
+}
+
+int main() {
+  const size_t n_cols = 65536;  // cfg3: 65536 columns x 8 interior chunks
+  const int n_chunks = 8, reps = 50;
+  const size_t words = (size_t)n_chunks * n_cols * 8;
+  uint32_t *d[3];
+  for (auto &x : d) CK(hipMalloc(&x, words * 4));
+  const double comps = (double)n_cols * n_chunks * 16;
+  const char *what[3] = {"alignbit for every rotation", "v_perm_b32 for rotr 16 and rotr 8",
+                         "rotr 16 as two SDWA word xors"};
+  double ms[3];
+  for (int rep = 0; rep < 2; rep++) {  // the second pass is reported (clocks settled)
+    ms[0] = run<0>(d[0], n_cols, n_chunks, reps);
+    ms[1] = run<1>(d[1], n_cols, n_chunks, reps);
+    ms[2] = run<2>(d[2], n_cols, n_chunks, reps);
+  }
+  std::vector<uint32_t> h0(words), h(words);
+  CK(hipMemcpy(h0.data(), d[0], words * 4, hipMemcpyDeviceToHost));
+  int bad = 0;
+  for (int v = 0; v < 3; v++) {
+    CK(hipMemcpy(h.data(), d[v], words * 4, hipMemcpyDeviceToHost));
+    const bool same = std::memcmp(h.data(), h0.data(), words * 4) == 0;
+    bad |= !same;
+    printf("variant %d (%s): %.4f ms, %.1f G compressions/s, chaining values %s\n", v, what[v], ms[v],
+           comps / (ms[v] * 1e6), same ? "equal to variant 0" : "DIFFER");
+  }
+  for (auto &x : d) CK(hipFree(x));
+  return bad;
+}
