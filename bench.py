@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--mode", choices=["auto", "sharded", "replicas"], default="auto",
-                    help="sharded: one commitment per step, rows split over the ranks (the library's "
+                    help="sharded: every commitment's rows split over the ranks, N commitments per step by "
+                         "default (--sharded-scaling; the library's "
                          "pipelined driver; the BASELINE cfg3 configuration); replicas: independent "
                          "commitments per rank on host threads; auto (default): sharded for --gpus > 1, "
                          "replicas on one GPU, where there is nothing to split and independent "

@@ -633,15 +633,21 @@ inline lcpc_status encode_rows_any(const lcpc_encoding *e, const uint32_t *src, 
     HIP_TRY(ntt_rows(e->plan, src, ss, nv, dst, ds, n_rows, s));
     return LCPC_OK;
   }
-  // SDIG: element-major working codeword, then back to rows
+  // SDIG: element-major working codeword, then back to rows.  The code is systematic (the
+  // codeword starts with the message, encode.rs:36-94), so the input transpose also writes the
+  // zero-padded message row-major into dst as it reads it, and only the parity part [np, nc) is
+  // transposed back (an in-place call with a full message has its message part in place already)
   const size_t nc = e->n_cols, np = e->n_per_row;
-  const int wb = field_bytes(e->fid);
+  const int wb = field_bytes(e->fid), nw = wb / 4;
   DBuf cw, tmp;
   HIP_TRY(cw.alloc(e->dev, nc * n_rows * wb));
   HIP_TRY(tmp.alloc(e->dev, e->sdig.tmp_elems * n_rows * wb));
-  HIP_TRY(transpose_elems(e->fid, src, n_rows, np, ss, nv < np ? nv : np, cw.as<uint32_t>(), n_rows, s));
+  const bool in_place = (const void *)src == (const void *)dst && ss == ds && nv >= np;
+  HIP_TRY(transpose_elems(e->fid, src, n_rows, np, ss, nv < np ? nv : np, cw.as<uint32_t>(), n_rows, s, TR_PLAIN,
+                          nullptr, SIZE_MAX, in_place ? nullptr : dst, ds));
   HIP_TRY(sdig_encode_cm(e->sdig, cw.as<uint32_t>(), n_rows, tmp.as<uint32_t>(), s));
-  HIP_TRY(transpose_elems(e->fid, cw.as<uint32_t>(), nc, n_rows, n_rows, n_rows, dst, ds, s));
+  HIP_TRY(transpose_elems(e->fid, cw.as<uint32_t>() + np * n_rows * nw, nc - np, n_rows, n_rows, n_rows,
+                          dst + np * nw, ds, s));
   return LCPC_OK;  // (cw / tmp go back to the pool fenced on s: no drain here)
 }
 

@@ -48,6 +48,49 @@ def test_sdig_encode_rows_batched(gpu, oracle):
         assert np.array_equal(got[r].reshape(-1), o.encode(rows[r].reshape(-1)))
 
 
+@pytest.mark.parametrize("fid", [0, 1, 3])
+@pytest.mark.parametrize("n_valid_of", ["full", "ragged"])
+def test_sdig_encode_rows_device_strided(gpu, oracle, hipmem, fid, n_valid_of):
+    """lcpc_encode_rows_device on SDIG with separate, strided source and destination rows and a
+    ragged message (n_valid < n_per_row: the rest of each message reads as zero).  The input
+    transpose writes the message part of every destination row, the output transpose only the
+    parity part; padding words past n_cols in a destination row stay untouched.  Also in place."""
+    n_per_row, seed, R = 1500, 11, 37
+    o = oracle.Encoding.sdig(fid, n_per_row, seed=seed, code_id=3)
+    g = gpu.SdigEncoding.new_from_dims(fid, n_per_row, o.n_cols, seed)
+    nl, nc = gpu.limbs(fid), o.n_cols
+    nv = n_per_row if n_valid_of == "full" else n_per_row - 123
+    ss, ds = n_per_row + 5, nc + 3
+    src = np.zeros((R, ss, nl), np.uint64)
+    for r in range(R):
+        src[r, :nv] = rand_elems(oracle, fid, nv, seed + r).reshape(-1, nl)
+    sentinel = np.uint64(0xA5A5A5A5A5A5A5A5)
+    dst = np.full((R, ds, nl), sentinel, np.uint64)
+    d_src, d_dst = hipmem.to_device(src), hipmem.to_device(dst)
+    try:
+        g.encode_rows_device(d_src, ss, nv, d_dst, ds, R)
+        got = hipmem.to_host(d_dst, np.empty_like(dst))
+    finally:
+        hipmem.free(d_src)
+        hipmem.free(d_dst)
+    assert np.all(got[:, nc:] == sentinel)
+    for r in range(R):
+        row = np.zeros((nc, nl), np.uint64)
+        row[:nv] = src[r, :nv]
+        assert np.array_equal(got[r, :nc].reshape(-1), o.encode(row.reshape(-1))), r
+    # in place: rows of n_cols whose message part holds the coefficients
+    rows = np.zeros((R, nc, nl), np.uint64)
+    rows[:, :n_per_row] = src[:, :n_per_row]
+    d = hipmem.to_device(rows)
+    try:
+        g.encode_rows_device(d, nc, n_per_row, d, nc, R)
+        got2 = hipmem.to_host(d, np.empty_like(rows))
+    finally:
+        hipmem.free(d)
+    for r in range(R):
+        assert np.array_equal(got2[r].reshape(-1), o.encode(rows[r].reshape(-1))), r
+
+
 def test_sdig_dims_and_errors(gpu, oracle):
     L = oracle.lib()
     for code in range(1, 7):
