@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <utility>
 
 #include "field_params.hpp"
 
@@ -270,16 +271,57 @@ __device__ __forceinline__ void fips_col_step(uint32_t lo, uint32_t hi, uint32_t
       : "v"(lo), "v"(hi), "v"(r2));
 }
 
+// Carry-free mads of column k of fe_mul_fips (bit s: product a_s b_(k-s) for s < N, reduction
+// m_(s-N) p_(k-s+N) for s >= N).  A column starts from an addend below 2^37 (the previous
+// column's high word and at most 2N + 1 carries).  A mad whose worst-case product keeps the
+// running sum below 2^64 cannot carry out, so its carry fold is dropped.  Such mads are taken
+// smallest bound first.  Every p has p_(N-1) < 2^31 (p < R / 2), so m p_(N-1) < 2^63; in the lazy
+// product b < p, so b_(N-1) <= p_(N-1) as well.  Ft127: the mads with p_1 (0.50 of 2^64),
+// p_3 (0.43) and, lazy, b_3 (0.43) -- 10 of the 28 mads need no fold (8 without b < p).
+template <class F, bool LAZY>
+__host__ __device__ constexpr uint32_t fips_free_mask(int k) {
+  constexpr int N = F::N;
+  using u128 = unsigned __int128;
+  const u128 lim = ((u128)1 << 64) - 1;
+  const u128 w = 0xffffffffu;
+  u128 bound[2 * N] = {};
+  bool cand[2 * N] = {};
+  for (int i = 0; i < N; i++) {
+    const int j = k - i;
+    if (j >= 0 && j < N) {
+      cand[i] = true;
+      bound[i] = w * ((LAZY && j == N - 1) ? (u128)F::P[N - 1] : w);
+    }
+    if (i < k && j >= 1 && j < N) {
+      cand[N + i] = true;
+      bound[N + i] = w * (u128)F::P[j];
+    }
+  }
+  u128 sum = (u128)1 << 37;
+  uint32_t mask = 0;
+  for (;;) {
+    int best = -1;
+    for (int s = 0; s < 2 * N; s++)
+      if (cand[s] && !((mask >> s) & 1u) && (best < 0 || bound[s] < bound[best])) best = s;
+    if (best < 0 || sum + bound[best] > lim) break;
+    sum += bound[best];
+    mask |= 1u << best;
+  }
+  return mask;
+}
+
 // Montgomery product for p = 1 mod 2^32 (every field the reference declares): finely integrated
 // product scanning.  Column k accumulates a_i b_(k-i) and m_i p_(k-i) into a 96-bit (acc, r2)
 // with one carry-out mad + one add-with-carry per product; for k < N the quotient word is
 // m_k = -acc mod 2^32 (-p^-1 = -1 mod 2^32) and m_k p_0 = m_k only clears the low word, leaving
 // a carry iff it was nonzero.  Each carry is folded into r2 one product later, so the SGPR a
 // mad writes is not read by the very next instruction.  tools/microbench/femul_variants.hip:
-// Ft127 366 -> 465 G mul/s on MI355X, bit-identical to the CIOS form.
+// Ft127 366 -> 465 G mul/s on MI355X, bit-identical to the CIOS form.  Round 6: the mads
+// fips_free_mask proves cannot carry go first in their column, without a fold.
 template <class F, bool LAZY = false>
 __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
   constexpr int N = F::N;
+  static_assert(F::P[N - 1] < 0x7fffff00u, "fips_free_mask's addend bound needs p < R / 2");
   uint32_t m[N], out[N];
   uint64_t acc = 0;
   uint32_t r2 = 0;
@@ -296,14 +338,27 @@ __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
         : "v"((uint32_t)p0), "v"((uint32_t)(p0 >> 32)));
     acc = nlo;
   }
+  auto column = [&]<int k>() {
+    constexpr uint32_t fm = fips_free_mask<F, LAZY>(k);
+    // the carry-free mads first: the same v_mad_u64_u32 with its carry-out mask left unread (the
+    // compiler's own 64-bit multiply-add selection adds a separate 64-bit add)
+    uint64_t unused;
 #pragma unroll
-  for (int k = 1; k < 2 * N; k++) {
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < N && ((fm >> i) & 1u)) acc = mad_co_vv(a.v[i], b.v[j], acc, unused);
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (i < k && j >= 1 && j < N && ((fm >> (N + i)) & 1u)) acc = mad_co_vs(m[i], F::P[j], acc, unused);
+    }
     uint64_t cprev = 0, ccur;
     bool have = false;
 #pragma unroll
     for (int i = 0; i < N; i++) {
       const int j = k - i;
-      if (j < 0 || j >= N) continue;
+      if (j < 0 || j >= N || ((fm >> i) & 1u)) continue;
       acc = mad_co_vv(a.v[i], b.v[j], acc, ccur);
       if (have) r2 = add_carry(r2, cprev);
       cprev = ccur;
@@ -312,14 +367,14 @@ __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
 #pragma unroll
     for (int i = 0; i < N; i++) {
       const int j = k - i;
-      if (i >= k || j < 1 || j >= N) continue;
+      if (i >= k || j < 1 || j >= N || ((fm >> (N + i)) & 1u)) continue;
       acc = mad_co_vs(m[i], F::P[j], acc, ccur);
       if (have) r2 = add_carry(r2, cprev);
       cprev = ccur;
       have = true;
     }
     if (have) r2 = add_carry(r2, cprev);
-    if (k < N) {
+    if constexpr (k < N) {
       uint32_t nlo, nhi;
       fips_col_step((uint32_t)acc, (uint32_t)(acc >> 32), r2, m[k], nlo, nhi);
       acc = ((uint64_t)nhi << 32) | nlo;
@@ -328,7 +383,10 @@ __device__ __forceinline__ Fe<F> fe_mul_fips(const Fe<F>& a, const Fe<F>& b) {
       acc = (acc >> 32) | ((uint64_t)r2 << 32);
     }
     r2 = 0;
-  }
+  };
+  [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
+    (column.template operator()<Ks + 1>(), ...);
+  }(std::make_integer_sequence<int, 2 * N - 1>{});
   // out + acc * 2^(32N) < 2p: one conditional subtraction
   Fe<F> u, r;
   if constexpr (LAZY) {  // a < 2p, b < p: the value is < p (1 + 2p/R) < 2p < R, so acc == 0

@@ -53,7 +53,7 @@ def issue_costs(path, k=4):
     return out
 
 
-def attribution(path=os.path.join(ROOT, "profiles", "r05_encode_isa_attribution.txt")):
+def attribution(path=os.path.join(ROOT, "profiles", "r06_encode_isa_attribution.txt")):
     passes, cur = {}, None
     for line in open(path):
         m = re.match(r"^(k_pass_[ab])<.*VALU (\d+), s_nop (\d+)", line)
