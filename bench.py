@@ -789,11 +789,12 @@ def roofline_objects(wl, iso, stats, args, traffic_rows_frac=1.0):
     if wl.mul_count:
         # the encode is bound by the 32-bit multiply-add pipe, not HBM: its VALU roofline is the
         # Montgomery-multiply rate of the field measured in isolation (tools/microbench/femul2.hip
-        # on MI355X: Ft63 1701, Ft127 503, Ft255 137 G/s; profiles/r01_femul2.txt); the hardware
+        # on MI355X, the library's product with its carry-free mads: Ft63 1909, Ft127 579, Ft255
+        # 154 G/s; profiles/r06_femul2.txt -- 1701 / 503 / 137 before, r01_femul2.txt); the hardware
         # v_mad_u64_u32 issue ceiling (20.6 T lane-ops/s, profiles/r01_mulbench.txt) over the 28
         # mads of an Ft127 product is the second peak
         field = args.field if args.code != "pos" else "Ft63"
-        peak = {"Ft63": 1701.0, "Ft127": 503.0, "Ft255": 137.0}.get(field)
+        peak = {"Ft63": 1909.0, "Ft127": 579.0, "Ft255": 154.0}.get(field)
         ach = wl.mul_count / (enc_ms * 1e-3) / 1e9 if enc_ms else None
         out["roofline_valu"] = {
             "kernel": wl.enc_kernel_desc, "bound": "valu (v_mad_u64_u32 Montgomery products)",

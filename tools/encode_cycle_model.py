@@ -7,7 +7,7 @@ Inputs (all measured on MI355X, committed under profiles/):
     occupancy: 97 VGPRs + AGPRs, 38 KiB LDS per 256-thread block) -- wall time per wave-instruction
     per SIMD, so the DVFS clock the VALU-dense loop runs at is inside the figure;
   * per-class static instruction counts of k_pass_a / k_pass_b<Ft127, 8, 3, 8>
-    (tools/isa_attribution.py -> profiles/r05_encode_isa_attribution.txt);
+    (tools/isa_attribution.py -> profiles/r06_encode_isa_attribution.txt, after the carry-free mads; r05 before);
   * the passes' dynamic VALU count per wave (SQ_INSTS_VALU / SQ_WAVES, tools/pmc_ntt.sh);
   * the passes' isolated durations (rocprofv3 kernel trace, fastest launch = a serial one).
 

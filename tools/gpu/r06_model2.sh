@@ -5,6 +5,7 @@ set -o pipefail
 O=gpurun_out/${1:-r06k}
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 120 ./tools/microbench/femul2 > $O/femul2.txt 2>&1 || { cat $O/femul2.txt; exit 1; }
 bash tools/pmc_ntt.sh ${1:-r06k}/pmc --code encode --log-len 24 || exit 1
 timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
   python3 bench.py --code encode --log-len 24 --steps 20 --warmup 5 --cpu-baseline off > $O/trace_bench.json 2> $O/trace_bench.err || { tail $O/trace_bench.err; exit 1; }
