@@ -838,8 +838,17 @@ lcpc_status prove_alloc(lcpc_sharded_commit *c, const uint64_t *outer, int root_
     c->p_random.resize(c->ndt * np * (wb / 8));
     c->p_eval.resize(np * (wb / 8));
   }
+  // The buffers above were taken on sp: a reused pool block's fence wait is queued there.  Two of
+  // them are first written on the comm stream instead -- bt (the root's challenge upload and the
+  // tensor broadcast) and didx (the index upload and broadcast) -- so those writes wait on this
+  // record, which follows every take (the ordering lcpc_sharded_pos_request gets by taking its
+  // gather buffer before its READY record)
+  HIP_TRY(hipEventRecord(EV(c, EV_READY, st_bcast(0)), c->sp));
   return LCPC_OK;
 }
+
+// the comm-stream writers of bt / didx wait for the prove buffers' takes (prove_alloc)
+hipEvent_t prove_taken(lcpc_sharded_commit *c) { return EV(c, EV_READY, st_bcast(0)); }
 
 lcpc_status prove_init(lcpc_sharded_commit *c, const uint64_t *outer, int root_rank, const lcpc_encoding *pe,
                        lcpc_transcript *tr, bool own_tr) {
@@ -868,6 +877,7 @@ Xop op_tensor_bcast(lcpc_sharded_commit *c, size_t r) {
   op.bytes = (r < c->ndt) ? c->n_rows * c->wb : 0;
   op.root = c->root_rank;
   op.s = c->sp;
+  op.ready = prove_taken(c);
   return op;
 }
 
@@ -877,6 +887,7 @@ hipStream_t upload_stream(const lcpc_sharded_commit *c) { return c->G == 1 ? c->
 // root: the challenge vector onto the comm stream before the exchange group is issued
 lcpc_status stage_tensor_upload(lcpc_sharded_commit *c, size_t r) {
   if (c->me != c->root_rank || r >= c->ndt) return LCPC_OK;
+  HIP_TRY(hipStreamWaitEvent(upload_stream(c), prove_taken(c), 0));
   HIP_TRY(h2d(c->bt.p, c->h_t.p, c->n_rows * c->wb, upload_stream(c)));
   return LCPC_OK;
 }
@@ -980,11 +991,13 @@ Xop op_idx_bcast(lcpc_sharded_commit *c) {
   op.bytes = c->nco * 8;
   op.root = c->root_rank;
   op.s = c->sp;
+  op.ready = prove_taken(c);
   return op;
 }
 
 lcpc_status stage_idx_upload(lcpc_sharded_commit *c) {
   if (c->me != c->root_rank || !c->nco) return LCPC_OK;
+  HIP_TRY(hipStreamWaitEvent(upload_stream(c), prove_taken(c), 0));
   HIP_TRY(h2d(c->didx.p, c->h_idx.p, c->nco * 8, upload_stream(c)));
   return LCPC_OK;
 }
