@@ -328,6 +328,16 @@ struct Lease {
   Lease &operator=(const Lease &) = delete;
 };
 
+// For a scope whose work runs on a caller's stream: the DBufs it allocates are taken (and
+// fenced at release) on that stream instead of the scope's lease stream
+struct StreamAs {
+  hipStream_t prev;
+  explicit StreamAs(hipStream_t x) : prev(t_stream) { t_stream = x; }
+  ~StreamAs() { t_stream = prev; }
+  StreamAs(const StreamAs &) = delete;
+  StreamAs &operator=(const StreamAs &) = delete;
+};
+
 // RAII device buffer from the stream-ordered pool.  It remembers the streams that use it -- the
 // one current when it was allocated (t_stream) and any added with use() -- and returns its block
 // with a fence on each (pool.hpp): the block's next owner is ordered after every write still

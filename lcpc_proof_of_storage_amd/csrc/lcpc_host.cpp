@@ -97,9 +97,10 @@ struct UploadStats {
   size_t blocks = 0;
 };
 inline thread_local UploadStats t_last_upload;
-// this thread's upload events (one "block landed" event per block in flight), per current device
+// this thread's upload events (one "block landed" event per block in flight, and the
+// destination's "taken" record on the consuming stream), per current device
 struct UploadEvents {
-  hipEvent_t e[2] = {};
+  hipEvent_t e[3] = {};
   int dev = -1;
   ~UploadEvents() { reset(); }
   void reset() {
@@ -149,6 +150,10 @@ lcpc_status h2d_blocks(Device *dev, uint8_t *d_dst, const uint8_t *h_src, size_t
       dev->release_stream(cs, POOL_BULK);
     }
   } rel{dev, cs};
+  // d_dst was taken from the pool on s (a reused block's fence wait is queued there): the copy
+  // stream writes it only after s has passed that point
+  HIP_TRY(hipEventRecord(t_upload_ev.e[2], s));
+  HIP_TRY(hipStreamWaitEvent(cs, t_upload_ev.e[2], 0));
   size_t k = 0;
   for (size_t off = 0; off < bytes; off += block, k++) {
     const size_t n = std::min(block, bytes - off);
@@ -648,6 +653,7 @@ lcpc_status lcpc_encode_rows_device(const lcpc_encoding *e, const void *d_src, s
   Lease lease(dev);
   HIP_TRY(hipSetDevice(dev->id));
   hipStream_t s = stream ? (hipStream_t)stream : lease.s;
+  StreamAs on_s(s);  // (SDIG's scratch codeword: taken and fenced on the stream that uses it)
   lcpc_status st = encode_rows_any(e, (const uint32_t *)d_src, src_stride, n_valid,
                                    (uint32_t *)d_dst, dst_stride, n_rows, s);
   if (st) return st;

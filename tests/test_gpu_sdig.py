@@ -89,6 +89,24 @@ def test_sdig_encode_rows_device_strided(gpu, oracle, hipmem, fid, n_valid_of):
         hipmem.free(d)
     for r in range(R):
         assert np.array_equal(got2[r].reshape(-1), o.encode(rows[r].reshape(-1))), r
+    # on a caller's stream (the scratch codeword is taken and fenced on that stream)
+    import ctypes as C
+    H = hipmem.L
+    H.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+    H.hipStreamSynchronize.argtypes = [C.c_void_p]
+    H.hipStreamDestroy.argtypes = [C.c_void_p]
+    st = C.c_void_p()
+    assert H.hipStreamCreate(C.byref(st)) == 0
+    d_src, d_dst = hipmem.to_device(src), hipmem.to_device(dst)
+    try:
+        g.encode_rows_device(d_src, ss, nv, d_dst, ds, R, stream=st.value)
+        assert H.hipStreamSynchronize(st) == 0
+        got3 = hipmem.to_host(d_dst, np.empty_like(dst))
+    finally:
+        hipmem.free(d_src)
+        hipmem.free(d_dst)
+        H.hipStreamDestroy(st)
+    assert np.array_equal(got3, got)
 
 
 def test_sdig_dims_and_errors(gpu, oracle):
