@@ -457,8 +457,16 @@ bool shard_prio_streams() { return true; }
 // polynomials' encode kernels overlap each other's tails (one-rank K = 20: 11.1 / 11.5 against
 // 11.0 / 11.3 G/s with one, interleaved runs, profiles/r04_sharded_bulk_streams_ab.json) while the
 // roots still arrive nearly in order
-constexpr size_t SHARD_BULK_STREAMS = 2;
-size_t shard_bulk_streams() { return SHARD_BULK_STREAMS; }
+// (LCPC_SHARD_BULK_STREAMS=1..4 overrides the count for A/B runs)
+constexpr size_t SHARD_BULK_STREAMS = 2, SHARD_BULK_MAX = 4;
+size_t shard_bulk_streams() {
+  static const size_t v = [] {
+    const char *e = getenv("LCPC_SHARD_BULK_STREAMS");
+    const long n = e ? strtol(e, nullptr, 10) : 0;
+    return (n >= 1 && n <= (long)SHARD_BULK_MAX) ? (size_t)n : SHARD_BULK_STREAMS;
+  }();
+  return v;
+}
 // the pool every stream of the sharded driver comes from (Device::acquire_stream): the
 // latency-side pool POOL_HIGH (verify, openings, this driver), apart from lcpc_prove's POOL_PROVER;
 // its priority equals the bulk pool's unless LCPC_PRIORITY_STREAMS=1
@@ -1576,25 +1584,22 @@ lcpc_status lcpc_sharded_commit_prove_many(const lcpc_encoding *e, const void *c
   TaskPool &pool = *comm->pool, &launch = *comm->launch, &encoder = *comm->encoder;
   // the encode streams (shard_bulk_streams(), taken in turn by polynomial)
   const size_t n_bulk = shard_bulk_streams();
-  hipStream_t bulks[2] = {nullptr, nullptr};
-  for (size_t i = 0; i < n_bulk; i++)
-    if (!(bulks[i] = e->dev->acquire_stream(kShardPool))) {
-      if (i) e->dev->release_stream(bulks[0], kShardPool);
-      return fail(LCPC_ERR_DEVICE, "no HIP stream");
-    }
+  hipStream_t bulks[SHARD_BULK_MAX] = {};
   struct BulkRelease {  // (destroyed after cs: returns the streams to the pool)
     Device *d;
     hipStream_t *s;
     ~BulkRelease() {
-      for (int i = 0; i < 2; i++)
+      for (size_t i = 0; i < SHARD_BULK_MAX; i++)
         if (s[i]) d->release_stream(s[i], kShardPool);
     }
   } bulk_release{e->dev, bulks};
+  for (size_t i = 0; i < n_bulk; i++)
+    if (!(bulks[i] = e->dev->acquire_stream(kShardPool))) return fail(LCPC_ERR_DEVICE, "no HIP stream");
   std::vector<ShardPtr> cs(n_polys);
   struct BulkDrain {  // (destroyed before cs: no polynomial is torn down under its running encode)
     hipStream_t *s;
     ~BulkDrain() {
-      for (int i = 0; i < 2; i++)
+      for (size_t i = 0; i < SHARD_BULK_MAX; i++)
         if (s[i]) (void)hipStreamSynchronize(s[i]);
     }
   } bulk_drain{bulks};
