@@ -116,6 +116,11 @@ def parse():
                          "Commits then finish in order and each proof's serial host "
                          "transcript starts while later commits run, instead of every commit of a wave "
                          "finishing together at its end")
+    ap.add_argument("--pos-eval", choices=("fused", "separate"), default="fused",
+                    help="--code pos with a device file image (--pos-commit bytes): fused = the commitment and "
+                         "u^T Enc(M) in one call (lcpc_pos_commit_eval_bytes_device: the evaluation summed in the "
+                         "leaf hashing's pass over the codeword); separate = lcpc_pos_commit_bytes_device, then "
+                         "lcpc_pos_eval_encoded's own pass")
     ap.add_argument("--input", choices=("device", "host", "host-pinned"), default="device",
                     help="replicas (ligero / sdig / pos): where each step's input is when it starts.  device "
                          "(default, the headline): resident in HBM.  host: pageable host memory, the caller's "
@@ -639,15 +644,27 @@ def pos_workload(args, L, torch, rank, local_rank):
             raise RuntimeError(f"pack failed {rc}: {_native.last_error()}")
         return L.LcCommit.commit_device(d_el.data_ptr(), n_rows * np_, enc)
 
+    fused = args.input == "device" and args.pos_commit == "bytes" and args.pos_eval == "fused"
+
+    def commit_eval(slot):
+        if fused:  # one call: the commitment and u^T Enc(M) (the evaluation rides on the leaf pass)
+            return L.LcCommit.commit_pos_bytes_device_eval(d_bytes.data_ptr(), n_bytes, enc, left)
+        c = commit(slot)
+        return c, P.verifiable_polynomial_evaluation(c, left)
+
     def step(slot):
         if gate is not None:
             gate.acquire()
         try:
-            c = commit(slot)
+            if fused:
+                c, _ = commit_eval(slot)
+            else:
+                c = commit(slot)
         finally:
             if gate is not None:
                 gate.release()
-        P.verifiable_polynomial_evaluation(c, left)
+        if not fused:
+            P.verifiable_polynomial_evaluation(c, left)
         c.open_columns(cols)
         return c.get_root()
 
@@ -665,8 +682,7 @@ def pos_workload(args, L, torch, rank, local_rank):
 
     def parity(O):
         """one request of this workload (untimed) against the oracle's answer on the whole file"""
-        c = commit(0)
-        ev = P.verifiable_polynomial_evaluation(c, left)
+        c, ev = commit_eval(0)
         opened = c.open_columns(cols)
         return pos_oracle_parity(O, host, np_, nc, n_rows, left, cols, c.get_root(), ev, opened)
 
@@ -682,6 +698,8 @@ def pos_workload(args, L, torch, rank, local_rank):
                             + INPUT_WORKLOAD[args.input],
                 "file_bytes": n_bytes, "n_rows": n_rows, "n_per_row": np_, "n_cols": nc, "soundness": snd,
                 "commit_call": ("lcpc_pos_commit_bytes (host file image, pipelined upload)" if args.input != "device"
+                                else "lcpc_pos_commit_eval_bytes_device (file image and u^T Enc(M) in one call)"
+                                if fused
                                 else "lcpc_pos_commit_bytes_device (file image in one call)" if args.pos_commit == "bytes"
                                 else "lcpc_pos_bytes_to_field_device + lcpc_commit_new_device")},
         step=step, cpu_baseline=cpu_baseline, parity=parity, input_bytes=n_bytes,

@@ -354,6 +354,16 @@ lcpc_status lcpc_pos_side_vectors(lcpc_field f, const uint64_t *x, size_t n_rows
  * over the ENCODED matrix (n_cols outputs; row-major commitments) */
 lcpc_status lcpc_pos_eval_encoded(const lcpc_commit *c, const uint64_t *left, size_t n_rows,
                                   uint64_t *out);
+/* One proof-of-storage request's GPU half in one call: lcpc_pos_commit_bytes_device on the
+ * device file image, then verifiable_polynomial_evaluation with `left` (n_rows elements, the
+ * commitment's row count) into eval_out (n_cols elements) -- the server's sequence
+ * (networking/server.rs:670-730: convert_file_data_to_commit, then lcpc_online.rs:454-484).
+ * The same commitment and the same values as the two calls.  The evaluation rides on the leaf
+ * hashing's pass over the codeword (each thread sums its (chunk, column)'s rows) instead of a
+ * second pass over it. */
+lcpc_status lcpc_pos_commit_eval_bytes_device(const lcpc_encoding *e, const void *d_bytes, size_t n_bytes,
+                                              const uint64_t *left, size_t n_rows, uint64_t *eval_out,
+                                              lcpc_commit **out);
 /* decode_row (lcpc_online.rs:568-574) = fffft ifft_oi on each of n_rows rows of len = 2^k
  * elements (in place); FFTError codes on bad lengths */
 lcpc_status lcpc_ifft_oi_rows(lcpc_field f, uint64_t *rows, size_t n_rows, size_t len);

@@ -143,6 +143,7 @@ SIGNATURES = {
     "lcpc_pos_bytes_to_field": (i32, [u8p, sz, u64p, szp]),
     "lcpc_pos_bytes_to_field_device": (i32, [vp, sz, vp, vp]),
     "lcpc_pos_commit_bytes_device": (i32, [vp, vp, sz, C.POINTER(vp)]),
+    "lcpc_pos_commit_eval_bytes_device": (i32, [vp, vp, sz, u64p, sz, u64p, C.POINTER(vp)]),
     "lcpc_pos_commit_bytes": (i32, [vp, u8p, sz, C.POINTER(vp)]),
     "lcpc_last_upload_pinned": (i32, []),
     "lcpc_pos_field_to_bytes": (i32, [u64p, sz, u8p, sz]),

@@ -121,9 +121,12 @@ __device__ __forceinline__ size_t cv_slot(size_t col, int chunk, int chunk0, int
 // row r at colp + (r - row0) row_stride).  Message word w of a column: w < 8 is the zero prefix,
 // else word (w-8) % N of element row (w-8) / N.  N in {2, 4, 8} divides both 8 and 16, so every
 // 16-word block holds whole elements.  A one-chunk message gets ROOT (it is the leaf).
-template <class F, bool CANON>
+// EVAL: also *acc = sum over the chunk's rows r of left[r] * element (Montgomery products of the
+// Montgomery left[r] and the canonical codeword: canonical results, as collapse_rows gives them).
+template <class F, bool CANON, bool EVAL = false>
 __device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, size_t n_rows, size_t row_stride,
-                                            size_t row0, int chunk, int n_chunks, uint32_t cv[8]) {
+                                            size_t row0, int chunk, int n_chunks, uint32_t cv[8],
+                                            const uint32_t *__restrict__ left = nullptr, Fe<F> *acc = nullptr) {
   constexpr int N = F::N;
   static_assert(16 % N == 0 && 8 % N == 0, "element must tile a BLAKE3 block");
   const size_t total_words = 8 + n_rows * N;
@@ -153,6 +156,14 @@ __device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, s
       for (int i = 0; i < N; i++) msg[k * N + i] = w[i];
     }
   };
+  // left[r] * element summed into *acc for the elements of rows r0, r0 + 1, ... (n of them)
+  auto eval_acc = [&](const Fe<F> *el, size_t r0, int n) {
+    if constexpr (EVAL) {
+#pragma unroll
+      for (int k = 0; k < EPB; k++)
+        if (k < n) *acc = fe_add<F>(*acc, fe_mul<F>(fe_load<F>(left, r0 + k), el[k]));
+    }
+  };
   // Interior chunks (a wave-uniform case: 16 full blocks, every row present, no zero prefix):
   // one strided pointer walk without per-element bounds checks, blocks in ping-pong pairs so
   // the next block's loads overlap this block's 7 rounds without register copies.
@@ -170,6 +181,7 @@ __device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, s
         for (int k = 0; k < EPB; k++) eb[k] = fe_load<F>(colp, e + k * row_stride);
         e += EPB * row_stride;
         to_msg(ea, msg);
+        eval_acc(ea, r_first + (size_t)b * EPB, EPB);
         compress(cv, msg, (uint64_t)chunk, 64u, b == 0 ? CHUNK_START : 0u);
         if (b + 2 < 16) {
 #pragma unroll
@@ -177,6 +189,7 @@ __device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, s
           e += EPB * row_stride;
         }
         to_msg(eb, msg);
+        eval_acc(eb, r_first + (size_t)(b + 1) * EPB, EPB);
         compress(cv, msg, (uint64_t)chunk, 64u, b + 1 == 15 ? CHUNK_END : 0u);
       }
       return;
@@ -197,10 +210,13 @@ __device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, s
       if (ew < 0 || (size_t)ew / N >= n_rows) {
 #pragma unroll
         for (int i = 0; i < N; i++) w[i] = 0;
-      } else if constexpr (CANON) {
-        fe_canon_repr_words<F>(cur[k], w);
       } else {
-        fe_repr_words<F>(cur[k], w);
+        if constexpr (CANON) {
+          fe_canon_repr_words<F>(cur[k], w);
+        } else {
+          fe_repr_words<F>(cur[k], w);
+        }
+        if constexpr (EVAL) *acc = fe_add<F>(*acc, fe_mul<F>(fe_load<F>(left, (size_t)ew / N), cur[k]));
       }
 #pragma unroll
       for (int i = 0; i < N; i++) msg[k * N + i] = w[i];
@@ -237,6 +253,28 @@ __global__ __launch_bounds__(256) void k_leaf_chunks(const uint32_t *__restrict_
   } else {
     store8(cvs + cv_slot(col, chunk, chunk0, chunk_end, n_cols, blk) * 8, cv);
   }
+}
+
+// k_leaf_chunks over a whole canonical row-major codeword (one rank, every row present) that also
+// leaves each (chunk, column)'s share of u^T Enc(M) in partials[chunk][col]: the proof-of-storage
+// request's evaluation (lcpc_online.rs:454-484) without a second pass over the codeword
+template <class F>
+__global__ __launch_bounds__(256) void k_leaf_chunks_eval(const uint32_t *__restrict__ m, size_t n_rows,
+                                                          size_t n_cols, size_t row_stride,
+                                                          uint32_t *__restrict__ cvs, uint8_t *__restrict__ leaves,
+                                                          int n_chunks, const uint32_t *__restrict__ left,
+                                                          uint32_t *__restrict__ partials) {
+  const size_t col = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int chunk = blockIdx.y;
+  if (col >= n_cols || chunk >= n_chunks) return;
+  uint32_t cv[8];
+  Fe<F> acc = fe_zero<F>();
+  chunk_cv_rm<F, true, true>(m + col * F::N, n_rows, row_stride, 0, chunk, n_chunks, cv, left, &acc);
+  if (n_chunks == 1 && leaves)
+    store8(reinterpret_cast<uint32_t *>(leaves + 32 * col), cv);
+  else
+    store8(cvs + ((size_t)chunk * n_cols + col) * 8, cv);
+  fe_store<F>(partials, (size_t)chunk * n_cols + col, acc);
 }
 
 // The same chunks for a column-major matrix ([column][row], a column's message words contiguous
@@ -696,6 +734,28 @@ hipError_t leaf_hashes(int fid, const uint32_t *m, size_t n_rows, size_t n_cols,
                        uint8_t *leaves, void *scratch, hipStream_t s, bool canon) {
   return leaf_hashes_strided(fid, m, n_rows, n_cols, stride, 1, leaves, scratch, s, canon);
 }
+
+hipError_t leaf_hashes_eval(int fid, const uint32_t *m, size_t n_rows, size_t n_cols, size_t stride,
+                            uint8_t *leaves, void *scratch, const uint32_t *left, uint32_t *partials,
+                            hipStream_t s) {
+  if (n_cols == 0) return hipSuccess;
+  const int n_chunks = (int)leaf_n_chunks(fid, n_rows);
+  const dim3 grid((unsigned)((n_cols + 255) / 256), (unsigned)n_chunks);
+  hipError_t e = dispatch_field(fid, [&]<class F>() -> hipError_t {
+    if constexpr (16 % F::N == 0 && 8 % F::N == 0) {
+      prof::Scope ps("leaf_chunks", s);
+      hipLaunchKernelGGL((k_leaf_chunks_eval<F>), grid, dim3(256), 0, s, m, n_rows, n_cols, stride,
+                         (uint32_t *)scratch, leaves, n_chunks, left, partials);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;  // (callers check leaf_eval_fusable first)
+    }
+  });
+  if (e != hipSuccess || n_chunks == 1) return e;
+  return launch_leaf_merge((uint32_t *)scratch, n_cols, n_chunks, leaves, s);
+}
+
+bool leaf_eval_fusable(int fid) { return field_words(fid) == 2 || field_words(fid) == 4 || field_words(fid) == 8; }
 
 hipError_t leaf_hashes_cols(int fid, const uint32_t *cols, size_t n_rows, size_t n_cols,
                             uint8_t *leaves, void *scratch, hipStream_t s, bool canon) {

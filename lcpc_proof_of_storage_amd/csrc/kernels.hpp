@@ -91,6 +91,14 @@ hipError_t leaf_chunk_cvs(int fid, const uint32_t *m, size_t row0, size_t n_rows
 // leaf digests from all n_chunks chaining values ([chunk][col] layout; cvs is clobbered)
 hipError_t leaves_from_cvs(uint32_t *cvs, size_t n_cols, int n_chunks, uint8_t *leaves,
                            hipStream_t s);
+// leaf_hashes of a canonical row-major codeword that also writes each (chunk, column)'s share of
+// u^T Enc(M): partials[chunk][col] = sum over the chunk's rows r of left[r] * m[r][col]
+// (Montgomery left, canonical results; leaf_n_chunks(fid, n_rows) x n_cols elements).  Fields
+// whose element tiles a BLAKE3 block only (leaf_eval_fusable).
+bool leaf_eval_fusable(int fid);
+hipError_t leaf_hashes_eval(int fid, const uint32_t *m, size_t n_rows, size_t n_cols, size_t stride,
+                            uint8_t *leaves, void *scratch, const uint32_t *left, uint32_t *partials,
+                            hipStream_t s);
 // same, for a [column][row] matrix (opened columns of a proof)
 hipError_t leaf_hashes_cols(int fid, const uint32_t *cols, size_t n_rows, size_t n_cols,
                             uint8_t *leaves, void *scratch, hipStream_t s, bool canon = false);

@@ -179,8 +179,12 @@ inline size_t upload_block(size_t row_bytes) {
 // src_bytes != 0: d_src is a device proof-of-storage file image of src_bytes bytes, 7 per
 // WriteableFt63 element (len = ceil(src_bytes / 7)), packed as DataField::from_byte_vec does
 // (fields/data_field.rs:38-46) -- at the PoS default dims straight into the one-pass encode
+// eval_left / eval_out (n_rows / n_cols elements, host): also u^T Enc(M) over the new codeword
+// (lcpc_online.rs:454-484, as lcpc_pos_eval_encoded), fused into the leaf hashing's pass over
+// the codeword where the leaf kernel can carry it (leaf_eval_fusable), else one more pass after it
 lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is_host, size_t len,
-                          lcpc_commit **out, size_t src_bytes = 0) {
+                          lcpc_commit **out, size_t src_bytes = 0, const uint64_t *eval_left = nullptr,
+                          uint64_t *eval_out = nullptr) {
   prof::HostScope hs_total("host_commit_total");
   if (!e || !out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
   const size_t np = e->n_per_row, nc = e->n_cols;
@@ -319,15 +323,42 @@ lcpc_status commit_device(const lcpc_encoding *e, const void *d_src, bool src_is
   // Merkle tree (:685-697, merkleize :720-734); leaves past n_cols stay zero digests
   HIP_TRY(c->hashes.alloc(dev, c->n_hashes * 32));
   if (np2 > nc) HIP_TRY(hipMemsetAsync(c->hashes.as<uint8_t>() + nc * 32, 0, (np2 - nc) * 32, s));
-  DBuf scratch;
+  DBuf scratch, dleft, partials, dsum;
   HIP_TRY(scratch.alloc(dev, leaf_hash_scratch_bytes(fid, n_rows, nc)));
-  if (c->col_major)
+  const bool eval = eval_left && eval_out;
+  const bool fused = eval && !c->col_major && c->canon && leaf_eval_fusable(fid);
+  if (eval) {
+    if (c->col_major) return fail(LCPC_ERR_UNSUPPORTED, "u^T Enc(M): row-major (Ligero) commitments only");
+    lcpc_status st = upload(dev, dleft, eval_left, n_rows * wb);
+    if (st) return st;
+    HIP_TRY(dsum.alloc(dev, nc * wb));
+  }
+  if (c->col_major) {
     HIP_TRY(leaf_hashes_cols(fid, c->comm.as<uint32_t>(), n_rows, nc, c->hashes.as<uint8_t>(), scratch.p, s,
                              c->canon));
-  else
+  } else if (fused) {
+    // the leaf pass also sums each (chunk, column)'s share of u^T Enc(M); the shares fold below
+    const size_t n_chunks = leaf_n_chunks(fid, n_rows);
+    HIP_TRY(partials.alloc(dev, n_chunks * nc * wb));
+    HIP_TRY(leaf_hashes_eval(fid, c->comm.as<uint32_t>(), n_rows, nc, nc, c->hashes.as<uint8_t>(), scratch.p,
+                             dleft.as<uint32_t>(), partials.as<uint32_t>(), s));
+    HIP_TRY(collapse_fold_rows(fid, partials.as<uint32_t>(), n_chunks, nc, dsum.as<uint32_t>(), s));
+  } else {
     HIP_TRY(leaf_hashes(fid, c->comm.as<uint32_t>(), n_rows, nc, nc, c->hashes.as<uint8_t>(), scratch.p, s,
                         c->canon));
+    if (eval) {
+      DBuf cs;
+      HIP_TRY(cs.alloc(dev, collapse_scratch_bytes(fid, n_rows, nc, 1)));
+      HIP_TRY(collapse_rows(fid, c->comm.as<uint32_t>(), n_rows, nc, dleft.as<uint32_t>(), 1, dsum.as<uint32_t>(),
+                            cs.p, s));
+    }
+  }
   HIP_TRY(merkle_tree(c->hashes.as<uint8_t>(), np2, s));
+  if (eval) {
+    // over a canonical matrix the Montgomery products come out as canonical values
+    if (c->canon) HIP_TRY(convert(fid, dsum.as<uint32_t>(), dsum.as<uint32_t>(), nc, true, s));
+    HIP_TRY(d2h_staged(eval_out, dsum.p, nc * wb, s));
+  }
   uint8_t *h_root = (uint8_t *)t_pin[PIN_OUTER].get(32);
   if (!h_root) return fail(LCPC_ERR_OUT_OF_MEMORY, "pinned host staging");
   HIP_TRY(d2h(h_root, c->hashes.as<uint8_t>() + (c->n_hashes - 1) * 32, 32, s));
@@ -679,6 +710,17 @@ lcpc_status lcpc_pos_commit_bytes_device(const lcpc_encoding *e, const void *d_b
   if (!d_bytes || !n_bytes) return fail(LCPC_ERR_INVALID_ARG, "null or empty file image");
   if ((uintptr_t)d_bytes & 7) return fail(LCPC_ERR_INVALID_ARG, "device file image must be 8-byte aligned");
   return commit_device(e, d_bytes, false, (n_bytes + 6) / 7, out, n_bytes);  // 7 data bytes per element
+}
+
+lcpc_status lcpc_pos_commit_eval_bytes_device(const lcpc_encoding *e, const void *d_bytes, size_t n_bytes,
+                                              const uint64_t *left, size_t n_rows, uint64_t *eval_out,
+                                              lcpc_commit **out) {
+  if (!e || !d_bytes || !n_bytes || !left || !eval_out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if ((uintptr_t)d_bytes & 7) return fail(LCPC_ERR_INVALID_ARG, "device file image must be 8-byte aligned");
+  const size_t len = (n_bytes + 6) / 7;
+  if (!e->n_per_row || n_rows != (len + e->n_per_row - 1) / e->n_per_row)
+    return fail(LCPC_ERR_INVALID_ARG, "left vector length != the commitment's n_rows");
+  return commit_device(e, d_bytes, false, len, out, n_bytes, left, eval_out);
 }
 
 lcpc_status lcpc_pos_commit_bytes(const lcpc_encoding *e, const uint8_t *bytes, size_t n_bytes, lcpc_commit **out) {

@@ -485,6 +485,20 @@ class LcCommit:
         return cls(h.value, enc.field)
 
     @classmethod
+    def commit_pos_bytes_device_eval(cls, d_bytes: int, n_bytes: int, enc: LcEncoding, left):
+        """one proof-of-storage request's commitment and u^T Enc(M) in one call
+        (lcpc_pos_commit_eval_bytes_device; networking/server.rs:670-730): the commitment of
+        commit_pos_bytes_device and the n_cols values of pos.verifiable_polynomial_evaluation
+        with `left` (n_rows elements), the evaluation summed during the leaf hashing's pass"""
+        nl = limbs(enc.field)
+        u = np.ascontiguousarray(left, dtype=np.uint64).reshape(-1, nl)
+        out = np.zeros((enc.n_cols, nl), np.uint64)
+        h = C.c_void_p()
+        _raise(N.load().lcpc_pos_commit_eval_bytes_device(enc._h, d_bytes, n_bytes, _p64(u), u.shape[0], _p64(out),
+                                                          C.byref(h)))
+        return cls(h.value, enc.field), out
+
+    @classmethod
     def commit_pos_bytes(cls, data, enc: LcEncoding) -> "LcCommit":
         """the same commitment from a file image in host memory (lcpc_pos_commit_bytes: the
         server's per-request commit of the file it just read, networking/server.rs:670-679);

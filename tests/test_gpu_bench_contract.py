@@ -174,8 +174,10 @@ def test_bench_sdig_small(gpu):
     assert "cpu_baseline" not in d
 
 
-def test_bench_pos_small(gpu):
-    d = _bench("--code", "pos", "--steps", "2", "--warmup", "2", "--pos-bytes", str(1 << 20))
+@pytest.mark.parametrize("pos_eval", ["fused", "separate"])
+def test_bench_pos_small(gpu, pos_eval):
+    d = _bench("--code", "pos", "--steps", "2", "--warmup", "2", "--pos-bytes", str(1 << 20), "--pos-eval", pos_eval)
+    assert ("lcpc_pos_commit_eval_bytes_device" in d["config"]["commit_call"]) == (pos_eval == "fused")
     _check_common(d, 2)
     _check_cpu(d)
     assert d["parity_root_vs_oracle"] and d["parity_eval_vs_oracle"] and d["parity_cols_vs_oracle"]

@@ -108,6 +108,49 @@ def test_eval_identity_and_parity(gpu, pos, oracle, np_, nc):
     assert got == want
 
 
+@pytest.mark.parametrize("n_bytes,dims", [
+    (7 * 16384 * 20 + 12345, None),      # the default dims of the file length: the one-pass encode
+    (7 * 16384 * 3, (16384, 32768)),      # whole rows, the one-pass encode
+    (7 * 100 * 37 + 3, (100, 256)),       # other dims: packed, then the four-step encode; ragged row
+    (13, (4, 8)),                         # two elements, one chunk per leaf (no merge)
+    (7 * 1000 * 260 + 1, (1000, 2048)),   # many chunks per leaf, ragged last chunk
+])
+def test_commit_eval_fused(gpu, pos, oracle, hipmem, n_bytes, dims):
+    """lcpc_pos_commit_eval_bytes_device (the request's commitment with u^T Enc(M) summed in the
+    leaf pass) == lcpc_pos_commit_bytes_device + lcpc_pos_eval_encoded == the oracle"""
+    rng = np.random.default_rng(n_bytes)
+    data = rng.integers(0, 256, n_bytes, dtype=np.uint8)
+    np_, nc = dims if dims else pos.get_aspect_ratio_default_from_file_len(n_bytes)[:2]
+    enc = gpu.LigeroEncoding.new_from_dims(FT63, np_, nc)
+    n_el = -(-n_bytes // 7)
+    n_rows = -(-n_el // np_)
+    x = oracle.ChaCha(seed_u64=1337, rounds=8).field_random(FT63, 1)
+    left, _ = pos.form_side_vectors_for_polynomial_evaluation_from_point(x, n_rows, nc)
+    d = hipmem.to_device(np.concatenate([data, np.zeros((-n_bytes) % 8 + 8, np.uint8)]))
+    try:
+        fc, fev = gpu.LcCommit.commit_pos_bytes_device_eval(d, n_bytes, enc, left)
+        sc = gpu.LcCommit.commit_pos_bytes_device(d, n_bytes, enc)
+    finally:
+        hipmem.free(d)
+    sev = pos.verifiable_polynomial_evaluation(sc, left)
+    assert fc.get_root() == sc.get_root()
+    assert np.array_equal(fev, sev)
+    el = oracle.pos_bytes_to_field(data.tobytes())
+    oc = oracle.Commit(oracle.Encoding.ligero(FT63, np_, nc), el)
+    assert fc.get_root() == oc.root()
+    assert np.array_equal(fev.reshape(-1), oracle.collapse(FT63, oc.comm, left, oc.n_rows, nc))
+
+
+def test_commit_eval_fused_rejects(gpu, pos, hipmem):
+    enc = gpu.LigeroEncoding.new_from_dims(FT63, 64, 128)
+    d = hipmem.to_device(np.ones(7 * 64 * 3, np.uint8))
+    try:
+        with pytest.raises(gpu.LcpcError):  # left must have the commitment's n_rows (3) elements
+            gpu.LcCommit.commit_pos_bytes_device_eval(d, 7 * 64 * 3, enc, np.zeros(4, np.uint64))
+    finally:
+        hipmem.free(d)
+
+
 def test_request_types(gpu, pos, oracle):
     """CommitRequestType::{Leaves, ColumnsWithoutPath, ColumnsWithPath} (lcpc_online.rs:80-239)."""
     coeffs = oracle.random_coeffs(FT63, 5000, 3)
