@@ -116,11 +116,12 @@ def parse():
                          "Commits then finish in order and each proof's serial host "
                          "transcript starts while later commits run, instead of every commit of a wave "
                          "finishing together at its end")
-    ap.add_argument("--pos-eval", choices=("fused", "separate"), default="fused",
-                    help="--code pos with a device file image (--pos-commit bytes): fused = the commitment and "
-                         "u^T Enc(M) in one call (lcpc_pos_commit_eval_bytes_device: the evaluation summed in the "
-                         "leaf hashing's pass over the codeword); separate = lcpc_pos_commit_bytes_device, then "
-                         "lcpc_pos_eval_encoded's own pass")
+    ap.add_argument("--pos-eval", choices=("fused", "separate"), default="separate",
+                    help="--code pos with a device file image (--pos-commit bytes): separate (default) = "
+                         "lcpc_pos_commit_bytes_device, then lcpc_pos_eval_encoded's own HBM-bound pass, which "
+                         "overlaps the other requests' VALU-bound kernels; fused = both in one call "
+                         "(lcpc_pos_commit_eval_bytes_device: the evaluation summed in the leaf hashing's pass), "
+                         "4 %% faster for one request alone, not faster with 4 in flight (DESIGN §5a)")
     ap.add_argument("--input", choices=("device", "host", "host-pinned"), default="device",
                     help="replicas (ligero / sdig / pos): where each step's input is when it starts.  device "
                          "(default, the headline): resident in HBM.  host: pageable host memory, the caller's "

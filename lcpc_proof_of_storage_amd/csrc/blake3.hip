@@ -117,6 +117,18 @@ __device__ __forceinline__ size_t cv_slot(size_t col, int chunk, int chunk0, int
   return blk ? ((col / blk) * (size_t)(chunk_end - chunk0) + c) * blk + col % blk : c * n_cols + col;
 }
 
+// acc += sum_k u[k] el[k] R^-1 over k in [K0, EPB), in fe_dot groups of at most fe_dot_kmax
+// products per reduction (bit-identical to summing fe_mul products: the same values mod p)
+template <class F, int K0, int EPB>
+__device__ __forceinline__ void dot_groups(Fe<F> &acc, const Fe<F> *u, const Fe<F> *el) {
+  if constexpr (K0 < EPB) {
+    constexpr int KM = fe_dot_kmax<F>() < 1 ? 1 : fe_dot_kmax<F>();
+    constexpr int G = (EPB - K0) < KM ? (EPB - K0) : KM;
+    acc = fe_add<F>(acc, fe_dot<F, G>(u + K0, el + K0));
+    dot_groups<F, K0 + G, EPB>(acc, u, el);
+  }
+}
+
 // The chaining value of chunk `chunk` of one column's leaf message (column pointer colp, element
 // row r at colp + (r - row0) row_stride).  Message word w of a column: w < 8 is the zero prefix,
 // else word (w-8) % N of element row (w-8) / N.  N in {2, 4, 8} divides both 8 and 16, so every
@@ -157,11 +169,12 @@ __device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, s
     }
   };
   // left[r] * element summed into *acc for the elements of rows r0, r0 + 1, ... (n of them)
-  auto eval_acc = [&](const Fe<F> *el, size_t r0, int n) {
+  auto eval_acc = [&](const Fe<F> *el, size_t r0) {  // a whole block of EPB rows
     if constexpr (EVAL) {
+      Fe<F> u[EPB];
 #pragma unroll
-      for (int k = 0; k < EPB; k++)
-        if (k < n) *acc = fe_add<F>(*acc, fe_mul<F>(fe_load<F>(left, r0 + k), el[k]));
+      for (int k = 0; k < EPB; k++) u[k] = fe_load<F>(left, r0 + k);
+      dot_groups<F, 0, EPB>(*acc, u, el);
     }
   };
   // Interior chunks (a wave-uniform case: 16 full blocks, every row present, no zero prefix):
@@ -181,7 +194,7 @@ __device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, s
         for (int k = 0; k < EPB; k++) eb[k] = fe_load<F>(colp, e + k * row_stride);
         e += EPB * row_stride;
         to_msg(ea, msg);
-        eval_acc(ea, r_first + (size_t)b * EPB, EPB);
+        eval_acc(ea, r_first + (size_t)b * EPB);
         compress(cv, msg, (uint64_t)chunk, 64u, b == 0 ? CHUNK_START : 0u);
         if (b + 2 < 16) {
 #pragma unroll
@@ -189,7 +202,7 @@ __device__ __forceinline__ void chunk_cv_rm(const uint32_t *__restrict__ colp, s
           e += EPB * row_stride;
         }
         to_msg(eb, msg);
-        eval_acc(eb, r_first + (size_t)(b + 1) * EPB, EPB);
+        eval_acc(eb, r_first + (size_t)(b + 1) * EPB);
         compress(cv, msg, (uint64_t)chunk, 64u, b + 1 == 15 ? CHUNK_END : 0u);
       }
       return;
