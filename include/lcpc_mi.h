@@ -420,7 +420,10 @@ lcpc_status lcpc_pos_encode_file_batched(const uint8_t *data, size_t n_bytes, si
  * digests, tree = MerkleTree::to_bytes; either may be NULL.  Rows are encoded and written as
  * soon as the data is known to continue past them, the last ones at finalize.  When the file
  * must grow, the caller re-lays it out (EncodedFileReader::set_new_capacity, reader.rs:348-381)
- * and passes the new image with set_target. */
+ * and passes the new image with set_target.  porenc = NULL with row_capacity = 0 is a digest-only
+ * writer: the rows are encoded and hashed into the column digests but written nowhere
+ * (RowGeneratorIter::get_column_digests / convert_to_commit_root over a byte stream,
+ * row_generator_iter.rs:29-41, 68-77; ColumnDigestAccumulator, column_digest_accumulator.rs:62-118). */
 typedef struct lcpc_pos_writer lcpc_pos_writer;
 lcpc_status lcpc_pos_writer_new(size_t pre, size_t enc, uint8_t *porenc, size_t row_capacity,
                                 size_t batch_rows, lcpc_pos_writer **out);

@@ -2200,7 +2200,7 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
     const size_t B = rr1 - r0;
     if (B > w->buf_rows) return fail(LCPC_ERR_INVALID_ARG, "internal: batch larger than its buffers");
     if (B) {
-      if (r0 + B > w->row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row capacity exceeded");
+      if (w->porenc && r0 + B > w->row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row capacity exceeded");
       // rows r0..r0+B are data bytes [rb (r0 - pend_row0), ...) of pend (the last may be short)
       const size_t b0 = (r0 - pend_row0) * rb;
       const size_t b1 = std::min(w->pend_len, b0 + B * rb);
@@ -2212,7 +2212,8 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
       // canonical codeword: the file's repr words and the leaves' input without conversion
       HIP_TRY(ntt_rows(w->e->plan, w->coeffs.as<uint32_t>(), pre, pre, w->comm.as<uint32_t>(), enc, B, s,
                        nullptr, 0, true));
-      HIP_TRY(transpose_elems(fid, w->comm.as<uint32_t>(), B, enc, enc, enc, w->dout.as<uint32_t>(), B, s));
+      if (w->porenc)  // (digest-only writers keep no image)
+        HIP_TRY(transpose_elems(fid, w->comm.as<uint32_t>(), B, enc, enc, enc, w->dout.as<uint32_t>(), B, s));
     }
     // column-digest chunks of these rows (ColumnDigestAccumulator::update, :62-87)
     HIP_TRY(leaf_chunk_cvs(fid, w->comm.as<uint32_t>(), r0, n_rows_cv, enc, enc, c_lo, c_hi,
@@ -2221,7 +2222,7 @@ lcpc_status writer_run(lcpc_pos_writer *w, size_t c_end, size_t n_rows_cv, size_
     const size_t cv_off = w->cvs.size();
     w->cvs.resize(cv_off + cv_bytes);
     HIP_TRY(hipMemcpyAsync(w->cvs.data() + cv_off, w->dcv.p, cv_bytes, hipMemcpyDeviceToHost, s));
-    if (B) {
+    if (B && w->porenc) {
       const int slot = k & 1;
       HIP_TRY(hipMemcpyAsync(w->stg[slot].p, w->dout.p, B * enc * POS_WB, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipEventRecord(w->ev.e[slot], s));
@@ -2319,7 +2320,7 @@ lcpc_status lcpc_pos_writer_finalize(lcpc_pos_writer *w, uint8_t *digests, uint8
   if (w->finalized) return fail(LCPC_ERR_INVALID_ARG, "writer already finalized");
   const size_t rb = pos_row_bytes(w);
   const size_t n_rows = w->rows_done + (w->pend_len + rb - 1) / rb;
-  if (n_rows > w->row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row capacity exceeded");
+  if (w->porenc && n_rows > w->row_capacity) return fail(LCPC_ERR_INVALID_ARG, "row capacity exceeded");
   const int fid = POS_FID;
   const size_t n_chunks = leaf_n_chunks(fid, n_rows);
   lcpc_status st = writer_run(w, n_chunks, n_rows, n_rows);

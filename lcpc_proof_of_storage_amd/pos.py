@@ -4,6 +4,7 @@ Mirrors the functions of the reference's proof-of-storage crate that feed / cons
 commitment (names kept):
   fields::convert_byte_vec_to_field_elements_vec        fields.rs:109-112, data_field.rs:38-46
   fields::convert_field_elements_vec_to_byte_vec        fields.rs:114-121
+  fields::field_generator_iter::FieldGeneratorIter      fields/field_generator_iter.rs:5-55
   networking::server::get_aspect_ratio_default_from_field_len / _from_file_len
                                                          networking/server.rs:1139-1182
   networking::client::get_column_indicies_from_random_seed   networking/client.rs:443-456
@@ -56,6 +57,70 @@ def convert_field_elements_vec_to_byte_vec(elems: np.ndarray, expected_length: i
     out = (C.c_uint8 * max(expected_length, 1))()
     _raise(N.load().lcpc_pos_field_to_bytes(_p64(a), a.size, C.cast(out, N.u8p), expected_length))
     return bytes(out)[:expected_length]
+
+
+class FieldGeneratorIter:
+    """FieldGeneratorIter<I, WriteableFt63> (fields/field_generator_iter.rs:5-55): an iterator of
+    bytes (ints 0..255, or bytes-like blocks) to field elements, DATA_BYTE_CAPACITY = 7 bytes each,
+    the last one zero padded -- the elements convert_byte_vec_to_field_elements_vec gives for the
+    same bytes.  Bytes are packed a block at a time by the library (lcpc_pos_bytes_to_field);
+    elements come out as uint64 raw limbs.  `byte_blocks()` hands a consumer the remaining bytes
+    themselves in blocks of whole elements (RowGeneratorIter's digest path)."""
+
+    BLOCK = DATA_BYTE_CAPACITY * 65536
+
+    def __init__(self, inner):
+        if isinstance(inner, (bytes, bytearray, memoryview)):
+            mv = memoryview(inner).cast("B")
+            inner = (bytes(mv[i:i + self.BLOCK]) for i in range(0, len(mv), self.BLOCK))
+        self._inner = iter(inner)
+        self._carry = b""          # bytes read but not yet packed (fewer than a whole block)
+        self._elems = np.zeros(0, np.uint64)
+        self._pos = 0
+        self._done = False
+
+    def _read(self, want: int) -> bytes:
+        """Up to `want` bytes (fewer only at the end of the input)."""
+        parts, have = [self._carry], len(self._carry)
+        while have < want and not self._done:
+            try:
+                x = next(self._inner)
+            except StopIteration:
+                self._done = True
+                break
+            b = bytes(x) if isinstance(x, (bytes, bytearray, memoryview)) else bytes((x,))
+            parts.append(b)
+            have += len(b)
+        buf = b"".join(parts)
+        self._carry = buf[want:]
+        return buf[:want]
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> np.uint64:
+        if self._pos == self._elems.size:
+            block = self._read(self.BLOCK)
+            if not block:
+                raise StopIteration
+            self._elems = convert_byte_vec_to_field_elements_vec(block).reshape(-1)
+            self._pos = 0
+        v = self._elems[self._pos]
+        self._pos += 1
+        return v
+
+    def byte_blocks(self):
+        """The rest of the input as bytes: first the elements already packed but not yet taken
+        (7 little-endian bytes each), then the unread bytes in blocks."""
+        if self._pos < self._elems.size:
+            rest = self._elems[self._pos:]
+            self._pos = self._elems.size
+            yield rest.astype("<u8").view(np.uint8).reshape(-1, 8)[:, :DATA_BYTE_CAPACITY].tobytes()
+        while True:
+            block = self._read(self.BLOCK)
+            if not block:
+                return
+            yield block
 
 
 def get_aspect_ratio_default_from_field_len(field_len: int):

@@ -11,6 +11,8 @@ formats of the reference's proof-of-storage/src/lcpc_online (names kept):
   MerkleTree            merkle_tree.rs:7-86             (digests = leaves || parents)
   read_tree / write_tree_to_file                         file_handler.rs:714-735
   get_encoded_file_size_from_rate / get_decoded_file_size_from_rate   reader.rs:384-407
+  RowGeneratorIter      row_generator_iter.rs:8-165     (new_ligero, next, get_column_digests,
+                        get_specified_column_digests, convert_to_commit_root, get_full_columns)
 
 Layout of a `.porenc` file (WriteableFt63): column c occupies row_capacity * 8 bytes starting at
 byte c * row_capacity * 8; its first rows_written elements are the canonical little-endian repr
@@ -23,6 +25,7 @@ the files and hands the library pointers into them.
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 import json
 import mmap
 import os
@@ -32,6 +35,7 @@ from typing import List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
+from . import lcpc2d as L
 from .lcpc2d import _raise
 
 WRITTEN_BYTES_WIDTH = 8   # size_of::<WriteableFt63>() (data_field.rs:24)
@@ -325,6 +329,129 @@ class EncodedFileWriter:
             with open(target_digest_file, "wb") as f:
                 write_tree_to_file(f, mt)
         return meta, mt
+
+
+# ---------------------------------------------------------------- streamed rows
+class RowGeneratorIter:
+    """RowGeneratorIter<WriteableFt63, I, LigeroEncoding> (row_generator_iter.rs:8-165).
+
+    Iterating yields the encoded rows (num_encoded elements each, uint64 raw limbs): every
+    num_pre_encoded elements of `field_iterator` (the last row zero padded) Ligero-encoded, as
+    `next` (:138-164) does row by row.  Here up to `batch_rows` rows are taken from the iterator at
+    once and encoded in one GPU call (lcpc_encode_rows), then handed out one by one.
+
+    The consuming methods work on the rows not yet yielded:
+      get_column_digests / get_specified_column_digests / convert_to_commit_root (:29-77) stream
+        them through a digest-only PoS writer (lcpc_pos_writer_new with no image), so memory stays
+        one batch however long the input;
+      get_full_columns (:79-107) commits to them and opens the columns.  Like the reference, it
+        returns the columns in REVERSE order of `specified_columns` (it pops the last first,
+        :99-104).
+    Digests stream only from a FieldGeneratorIter, whose elements are whole 7-byte data words.
+    For any other element iterator the remaining elements are collected and committed in one call
+    (same digests)."""
+
+    def __init__(self, field_iterator, num_pre_encoded: int, num_encoded: int, batch_rows: int = 1024):
+        if not (num_encoded > 0 and num_encoded & (num_encoded - 1) == 0) or not 0 < num_pre_encoded < num_encoded:
+            raise ValueError("bad Ligero dimensions")
+        self.field_iterator = field_iterator
+        self.unencoded_len = num_pre_encoded
+        self.encoded_len = num_encoded
+        self.encoding = L.LigeroEncoding.new_from_dims(L.FT63, num_pre_encoded, num_encoded)
+        self.batch_rows = max(1, batch_rows)
+        self._elems = np.zeros(0, np.uint64)   # unencoded elements of the rows in _rows
+        self._rows = np.zeros((0, num_encoded), np.uint64)
+        self._next = 0
+
+    @classmethod
+    def new_ligero(cls, field_iterator, num_pre_encoded: int, num_encoded: int) -> "RowGeneratorIter":
+        return cls(field_iterator, num_pre_encoded, num_encoded)
+
+    def _take(self, n: int) -> np.ndarray:
+        return np.fromiter(itertools.islice(self.field_iterator, n), dtype=np.uint64)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> np.ndarray:
+        if self._next == self._rows.shape[0]:
+            pre, enc = self.unencoded_len, self.encoded_len
+            el = self._take(self.batch_rows * pre)
+            if el.size == 0:  # the empty case (:148-151)
+                raise StopIteration
+            n = -(-el.size // pre)
+            flat = np.zeros(n * pre, np.uint64)
+            flat[:el.size] = el
+            m = np.zeros((n, enc), np.uint64)
+            m[:, :pre] = flat.reshape(n, pre)
+            self._rows = self.encoding.encode_rows(m).reshape(n, enc)
+            self._elems = el
+            self._next = 0
+        row = self._rows[self._next].copy()
+        self._next += 1
+        return row
+
+    def _rest_elements(self) -> np.ndarray:
+        """The unencoded elements of every row not yet yielded (consumes the iterator)."""
+        pre = self.unencoded_len
+        head = self._elems[self._next * pre:]
+        self._rows, self._elems, self._next = self._rows[:0], self._elems[:0], 0
+        tail = np.fromiter(self.field_iterator, dtype=np.uint64)
+        return np.concatenate([head, tail])
+
+    def _rest_byte_blocks(self):
+        """The rows not yet yielded as data bytes (FieldGeneratorIter inputs only)."""
+        pre = self.unencoded_len
+        head = self._elems[self._next * pre:]
+        self._rows, self._elems, self._next = self._rows[:0], self._elems[:0], 0
+        if head.size:
+            yield head.astype("<u8").view(np.uint8).reshape(-1, 8)[:, :DATA_BYTE_CAPACITY].tobytes()
+        yield from self.field_iterator.byte_blocks()
+
+    def _digests_and_tree(self):
+        from .pos import FieldGeneratorIter
+        w = self.encoded_len
+        digests = np.zeros((w, DIGEST_BYTES), np.uint8)
+        tree = np.zeros((2 * w - 1, DIGEST_BYTES), np.uint8)
+        if not isinstance(self.field_iterator, FieldGeneratorIter):
+            el = self._rest_elements()
+            if el.size == 0:
+                raise ValueError("no rows left to hash")
+            comm = L.LcCommit.commit(el.reshape(-1, 1), self.encoding)
+            h = np.frombuffer(comm.hashes, np.uint8).reshape(-1, DIGEST_BYTES)
+            return h[:w].copy(), h.copy()
+        h = N.vp()
+        _raise(N.load().lcpc_pos_writer_new(self.unencoded_len, w, None, 0, 0, C.byref(h)))
+        try:
+            pushed = 0
+            for block in self._rest_byte_blocks():
+                p, keep = _bytes_ptr(block)
+                _raise(N.load().lcpc_pos_writer_push_bytes(h, p, len(block)))
+                pushed += len(block)
+            if pushed == 0:
+                raise ValueError("no rows left to hash")
+            rows, nbytes = C.c_size_t(), C.c_size_t()
+            _raise(N.load().lcpc_pos_writer_finalize(h, _u8(digests), _u8(tree), C.byref(rows), C.byref(nbytes)))
+        finally:
+            N.load().lcpc_pos_writer_free(h)
+        return digests, tree
+
+    def get_column_digests(self) -> List[bytes]:
+        d, _ = self._digests_and_tree()
+        return [r.tobytes() for r in d]
+
+    def get_specified_column_digests(self, column_indices) -> List[bytes]:
+        d = self.get_column_digests()
+        return [d[i] for i in column_indices]
+
+    def convert_to_commit_root(self) -> bytes:
+        _, t = self._digests_and_tree()
+        return t[-1].tobytes()
+
+    def get_full_columns(self, specified_columns) -> List["L.LcColumn"]:
+        el = self._rest_elements()
+        comm = L.LcCommit.commit(el.reshape(-1, 1), self.encoding)
+        return comm.open_columns(list(specified_columns))[::-1]
 
 
 # ---------------------------------------------------------------- reader
