@@ -433,6 +433,24 @@ size_t lcpc_pos_writer_rows_written(const lcpc_pos_writer *w);
 lcpc_status lcpc_pos_writer_push_bytes(lcpc_pos_writer *w, const uint8_t *bytes, size_t n);
 lcpc_status lcpc_pos_writer_finalize(lcpc_pos_writer *w, uint8_t *digests, uint8_t *tree,
                                      size_t *rows_written, size_t *bytes_of_data);
+/* ColumnDigestAccumulator<Blake3, F> with ColumnsToCareAbout::All (column_digest_accumulator.rs:
+ * 17-118; the server's upload path, server.rs:433, and RowGeneratorIter): column digests of a
+ * matrix pushed a batch of encoded rows at a time (row-major, width elements each, Montgomery
+ * limbs as everywhere else).  Each column's digest is BLAKE3(32 zero bytes || repr of its elements),
+ * hashed on the GPU in 1-KiB chunks as they complete, so memory stays one batch of rows.  finalize
+ * writes the width digests (get_column_digests) and / or the Merkle tree (finalize_to_merkle_tree:
+ * 2 width - 1 digests, root last; width a power of two >= 2); either may be NULL.  Fields whose
+ * elements tile a chunk (not Ft191).  ColumnsToCareAbout::Only is not offered: the reference's
+ * update checks the row length against the tracked count and indexes the digests by column
+ * number (:63-84), so it only works when it equals All, and no caller uses it. */
+typedef struct lcpc_column_digests lcpc_column_digests;
+/* batch_rows: rows buffered before a GPU pass hashes their complete chunks (0 = about 256 MiB) */
+lcpc_status lcpc_column_digests_new(lcpc_field f, size_t width, size_t batch_rows,
+                                    lcpc_column_digests **out);
+void lcpc_column_digests_free(lcpc_column_digests *a);
+size_t lcpc_column_digests_width(const lcpc_column_digests *a);      /* get_width :58-60 */
+lcpc_status lcpc_column_digests_update(lcpc_column_digests *a, const uint64_t *rows, size_t n_rows);
+lcpc_status lcpc_column_digests_finalize(lcpc_column_digests *a, uint8_t *digests, uint8_t *tree);
 /* EncodedFileReader::process_file_to_merkle_tree (encoded_file_reader.rs:328-346).
  * LCPC_ERR_INVALID_ARG if an element is not canonical (from_repr(..).unwrap() panics there). */
 lcpc_status lcpc_pos_porenc_tree(const uint8_t *porenc, size_t enc, size_t rows_written,

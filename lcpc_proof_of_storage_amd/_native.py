@@ -161,6 +161,11 @@ SIGNATURES = {
     "lcpc_pos_encode_file_batched": (i32, [u8p, sz, sz, sz, sz, u8p, u8p, szp, sz]),
     "lcpc_pos_writer_new": (i32, [sz, sz, u8p, sz, sz, C.POINTER(vp)]),
     "lcpc_pos_writer_free": (None, [vp]),
+    "lcpc_column_digests_new": (i32, [i32, sz, sz, C.POINTER(vp)]),
+    "lcpc_column_digests_free": (None, [vp]),
+    "lcpc_column_digests_width": (sz, [vp]),
+    "lcpc_column_digests_update": (i32, [vp, u64p, sz]),
+    "lcpc_column_digests_finalize": (i32, [vp, u8p, u8p]),
     "lcpc_pos_writer_set_target": (i32, [vp, u8p, sz]),
     "lcpc_pos_writer_rows_written": (sz, [vp]),
     "lcpc_pos_writer_push_bytes": (i32, [vp, u8p, sz]),

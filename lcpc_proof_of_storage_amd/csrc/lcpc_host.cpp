@@ -2573,3 +2573,115 @@ lcpc_status lcpc_pos_decode_porenc(const uint8_t *porenc, size_t pre, size_t enc
 }
 
 }  // extern "C"
+
+// ColumnDigestAccumulator<Blake3, F> with ColumnsToCareAbout::All (column_digest_accumulator.rs:
+// 17-118): encoded rows pushed one batch at a time; every column's message is the 32 zero bytes
+// then the repr of its elements, hashed in 1-KiB BLAKE3 chunks on the GPU as soon as a chunk is
+// complete and the message is known to continue past it (so no chunk is hashed as the only one).
+struct lcpc_column_digests {
+  Device *dev = nullptr;
+  int fid = 0;
+  size_t width = 0, chunks_done = 0, rows_in = 0, batch_rows = 0;
+  std::vector<uint64_t> pend;  // rows from leaf_chunk_first_row(chunks_done) on
+  std::vector<uint8_t> cvs;    // [chunk][column] chaining values of the chunks done
+  bool finalized = false;
+};
+
+namespace {
+
+constexpr size_t ACC_BATCH_BYTES = (size_t)256 << 20;  // default rows per GPU pass: about this much input
+
+// hash chunks [a->chunks_done, c_end) of messages n_rows_cv rows long (exact, or any count past
+// the covered rows while the message continues) from the pending rows
+lcpc_status acc_run(lcpc_column_digests *a, size_t c_end, size_t n_rows_cv) {
+  if (c_end <= a->chunks_done) return LCPC_OK;
+  const int fid = a->fid;
+  const size_t nl = (size_t)field_bytes(fid) / 8, w = a->width;
+  const size_t r0 = lcpc_leaf_chunk_first_row((lcpc_field)fid, a->chunks_done);
+  const size_t r1 = std::min(a->rows_in, lcpc_leaf_chunk_first_row((lcpc_field)fid, c_end));
+  Lease lease(a->dev);
+  HIP_TRY(hipSetDevice(a->dev->id));
+  DBuf drows, dcv;
+  lcpc_status st;
+  if ((st = upload(a->dev, drows, a->pend.data(), (r1 - r0) * w * nl * 8))) return st;
+  HIP_TRY(dcv.alloc(a->dev, (c_end - a->chunks_done) * w * 32));
+  HIP_TRY(leaf_chunk_cvs(fid, drows.as<uint32_t>(), r0, n_rows_cv, w, w, a->chunks_done, c_end,
+                         dcv.as<uint32_t>(), lease.s));
+  const size_t off = a->cvs.size();
+  a->cvs.resize(off + (c_end - a->chunks_done) * w * 32);
+  HIP_TRY(hipMemcpyAsync(a->cvs.data() + off, dcv.p, (c_end - a->chunks_done) * w * 32, hipMemcpyDeviceToHost,
+                         lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  a->pend.erase(a->pend.begin(), a->pend.begin() + (r1 - r0) * w * nl);
+  a->chunks_done = c_end;
+  return LCPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+lcpc_status lcpc_column_digests_new(lcpc_field f, size_t width, size_t batch_rows, lcpc_column_digests **out) {
+  if (!out) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (!valid_field(f) || !field_gpu_supported(f)) return fail(LCPC_ERR_UNSUPPORTED, "field");
+  if (992 % field_bytes(f)) return fail(LCPC_ERR_UNSUPPORTED, "elements that straddle BLAKE3 chunks (Ft191)");
+  if (!width) return fail(LCPC_ERR_INVALID_ARG, "width must be > 0");
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  auto a = std::make_unique<lcpc_column_digests>();
+  a->dev = dev;
+  a->fid = f;
+  a->width = width;
+  a->batch_rows = batch_rows ? batch_rows : std::max<size_t>(1, ACC_BATCH_BYTES / (width * field_bytes(f)));
+  *out = a.release();
+  return LCPC_OK;
+}
+
+void lcpc_column_digests_free(lcpc_column_digests *a) { delete a; }
+
+size_t lcpc_column_digests_width(const lcpc_column_digests *a) { return a ? a->width : 0; }
+
+lcpc_status lcpc_column_digests_update(lcpc_column_digests *a, const uint64_t *rows, size_t n_rows) {
+  // update (:62-87), for n_rows encoded rows of `width` elements at once
+  if (!a || (!rows && n_rows)) return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (a->finalized) return fail(LCPC_ERR_INVALID_ARG, "accumulator already finalized");
+  const size_t nl = (size_t)field_bytes(a->fid) / 8, w = a->width;
+  a->pend.insert(a->pend.end(), rows, rows + n_rows * w * nl);
+  a->rows_in += n_rows;
+  // chunks that end at or before the last row but one: complete, and not their column's last
+  size_t c_end = a->chunks_done;
+  while (lcpc_leaf_chunk_first_row((lcpc_field)a->fid, c_end + 1) < a->rows_in) c_end++;
+  const size_t r0 = lcpc_leaf_chunk_first_row((lcpc_field)a->fid, a->chunks_done);
+  if (lcpc_leaf_chunk_first_row((lcpc_field)a->fid, c_end) - r0 < a->batch_rows) return LCPC_OK;  // keep buffering
+  return acc_run(a, c_end, a->rows_in);
+}
+
+lcpc_status lcpc_column_digests_finalize(lcpc_column_digests *a, uint8_t *digests, uint8_t *tree) {
+  // get_column_digests (:89-96) into digests (width x 32 B), and / or finalize_to_merkle_tree
+  // (:109-118) into tree (MerkleTree::to_bytes: 2 width - 1 digests, root last; width a power
+  // of two >= 2, MerkleTree::new's requirement); either may be NULL
+  if (!a) return fail(LCPC_ERR_INVALID_ARG, "null accumulator");
+  if (a->finalized) return fail(LCPC_ERR_INVALID_ARG, "accumulator already finalized");
+  const size_t w = a->width;
+  if (tree && (w < 2 || (w & (w - 1)))) return fail(LCPC_ERR_INVALID_ARG, "Input needs to be a power of two, at least two.");
+  const size_t n_chunks = leaf_n_chunks(a->fid, a->rows_in);
+  lcpc_status st = acc_run(a, n_chunks, a->rows_in);
+  if (st) return st;
+  a->finalized = true;
+  Lease lease(a->dev);
+  HIP_TRY(hipSetDevice(a->dev->id));
+  DBuf dc, hashes;
+  if ((st = upload(a->dev, dc, a->cvs.data(), a->cvs.size()))) return st;
+  HIP_TRY(hashes.alloc(a->dev, (2 * w - 1) * 32));
+  HIP_TRY(leaves_from_cvs(dc.as<uint32_t>(), w, (int)n_chunks, hashes.as<uint8_t>(), lease.s));
+  if (tree) {
+    HIP_TRY(merkle_tree(hashes.as<uint8_t>(), w, lease.s));
+    HIP_TRY(hipMemcpyAsync(tree, hashes.p, (2 * w - 1) * 32, hipMemcpyDeviceToHost, lease.s));
+  }
+  if (digests) HIP_TRY(hipMemcpyAsync(digests, hashes.p, w * 32, hipMemcpyDeviceToHost, lease.s));
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  return LCPC_OK;
+}
+
+}  // extern "C"

@@ -13,6 +13,7 @@ formats of the reference's proof-of-storage/src/lcpc_online (names kept):
   get_encoded_file_size_from_rate / get_decoded_file_size_from_rate   reader.rs:384-407
   RowGeneratorIter      row_generator_iter.rs:8-165     (new_ligero, next, get_column_digests,
                         get_specified_column_digests, convert_to_commit_root, get_full_columns)
+  ColumnDigestAccumulator, ColumnsToCareAbout   column_digest_accumulator.rs:9-118
 
 Layout of a `.porenc` file (WriteableFt63): column c occupies row_capacity * 8 bytes starting at
 byte c * row_capacity * 8; its first rows_written elements are the canonical little-endian repr
@@ -332,6 +333,83 @@ class EncodedFileWriter:
 
 
 # ---------------------------------------------------------------- streamed rows
+class ColumnsToCareAbout:
+    """column_digest_accumulator.rs:9-15.  Only(indices) is kept as a type; the accumulator
+    refuses it (see ColumnDigestAccumulator)."""
+    All = "All"
+
+    @dataclass
+    class Only:
+        indices: List[int]
+
+
+class ColumnDigestAccumulator:
+    """ColumnDigestAccumulator<Blake3, F> (column_digest_accumulator.rs:17-118) over the GPU
+    accumulator (lcpc_column_digests_*): every column's digest is BLAKE3(32 zero bytes || repr of
+    its elements), hashed in 1-KiB chunks as they complete, so memory stays one batch of rows.
+    update takes one encoded row (num_encoded elements) or a (k, num_encoded) batch of them.
+
+    ColumnsToCareAbout.Only raises NotImplementedError: the reference's update checks the row
+    length against the number of tracked columns and then indexes the digests by column number
+    (:63-84), so it only works where it equals All; no caller uses it."""
+
+    def __init__(self, number_of_encoded_columns: int, columns_to_care_about=ColumnsToCareAbout.All,
+                 field: int = 0, batch_rows: int = 0):
+        if isinstance(columns_to_care_about, ColumnsToCareAbout.Only):
+            raise NotImplementedError("ColumnsToCareAbout::Only (unusable in the reference; see the class doc)")
+        self.field = field
+        self._nl = L.limbs(field)
+        h = N.vp()
+        _raise(N.load().lcpc_column_digests_new(field, number_of_encoded_columns, batch_rows, C.byref(h)))
+        self._h = h
+        self._done = False
+
+    def get_width(self) -> int:
+        return N.load().lcpc_column_digests_width(self._h)
+
+    def update(self, encoded_row) -> None:
+        if self._done:
+            raise RuntimeError("accumulator already finalized")
+        a = np.ascontiguousarray(encoded_row, dtype=np.uint64)
+        w = self.get_width()
+        if a.size % (w * self._nl):
+            raise ValueError("incorrect length of input")  # ensure! (:63-66)
+        n = a.size // (w * self._nl)
+        _raise(N.load().lcpc_column_digests_update(self._h, L._p64(a.reshape(-1)) if n else None, n))
+
+    def _finalize(self, want_digests: bool, want_tree: bool):
+        if self._done:
+            raise RuntimeError("accumulator already finalized")
+        w = self.get_width()
+        digests = np.zeros((w, DIGEST_BYTES), np.uint8) if want_digests else None
+        tree = np.zeros((2 * w - 1, DIGEST_BYTES), np.uint8) if want_tree else None
+        try:
+            _raise(N.load().lcpc_column_digests_finalize(self._h, _u8(digests) if want_digests else None,
+                                                         _u8(tree) if want_tree else None))
+        finally:
+            self._done = True
+            N.load().lcpc_column_digests_free(self._h)
+        return digests, tree
+
+    def get_column_digests(self) -> List[bytes]:
+        d, _ = self._finalize(True, False)
+        return [r.tobytes() for r in d]
+
+    def finalize_to_commit(self) -> bytes:
+        return self.finalize_to_merkle_tree().root()
+
+    def finalize_to_merkle_tree(self) -> MerkleTree:
+        _, t = self._finalize(False, True)
+        return MerkleTree(t)
+
+    def __del__(self):
+        if getattr(self, "_done", True) is False:
+            try:
+                N.load().lcpc_column_digests_free(self._h)
+            except Exception:
+                pass
+
+
 class RowGeneratorIter:
     """RowGeneratorIter<WriteableFt63, I, LigeroEncoding> (row_generator_iter.rs:8-165).
 
@@ -347,9 +425,9 @@ class RowGeneratorIter:
       get_full_columns (:79-107) commits to them and opens the columns.  Like the reference, it
         returns the columns in REVERSE order of `specified_columns` (it pops the last first,
         :99-104).
-    Digests stream only from a FieldGeneratorIter, whose elements are whole 7-byte data words.
-    For any other element iterator the remaining elements are collected and committed in one call
-    (same digests)."""
+    From a FieldGeneratorIter (whole 7-byte data words) the data bytes go straight to the
+    writer.  Any other element iterator streams its encoded rows through a
+    ColumnDigestAccumulator, as the reference does (:33-40)."""
 
     def __init__(self, field_iterator, num_pre_encoded: int, num_encoded: int, batch_rows: int = 1024):
         if not (num_encoded > 0 and num_encoded & (num_encoded - 1) == 0) or not 0 < num_pre_encoded < num_encoded:
@@ -414,22 +492,23 @@ class RowGeneratorIter:
         digests = np.zeros((w, DIGEST_BYTES), np.uint8)
         tree = np.zeros((2 * w - 1, DIGEST_BYTES), np.uint8)
         if not isinstance(self.field_iterator, FieldGeneratorIter):
-            el = self._rest_elements()
-            if el.size == 0:
-                raise ValueError("no rows left to hash")
-            comm = L.LcCommit.commit(el.reshape(-1, 1), self.encoding)
-            h = np.frombuffer(comm.hashes, np.uint8).reshape(-1, DIGEST_BYTES)
-            return h[:w].copy(), h.copy()
+            acc = ColumnDigestAccumulator(w, ColumnsToCareAbout.All, L.FT63)
+            batch = []
+            for row in self:
+                batch.append(row)
+                if len(batch) == self.batch_rows:
+                    acc.update(np.stack(batch))
+                    batch = []
+            if batch:
+                acc.update(np.stack(batch))
+            tree = acc.finalize_to_merkle_tree()
+            return tree.digests[:w].copy(), tree.digests.copy()
         h = N.vp()
         _raise(N.load().lcpc_pos_writer_new(self.unencoded_len, w, None, 0, 0, C.byref(h)))
         try:
-            pushed = 0
             for block in self._rest_byte_blocks():
                 p, keep = _bytes_ptr(block)
                 _raise(N.load().lcpc_pos_writer_push_bytes(h, p, len(block)))
-                pushed += len(block)
-            if pushed == 0:
-                raise ValueError("no rows left to hash")
             rows, nbytes = C.c_size_t(), C.c_size_t()
             _raise(N.load().lcpc_pos_writer_finalize(h, _u8(digests), _u8(tree), C.byref(rows), C.byref(nbytes)))
         finally:

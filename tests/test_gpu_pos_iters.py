@@ -7,6 +7,7 @@ in-memory path and the oracle's commitment.  Ports of the reference's own tests:
   is_row_iterator_the_same_root         :286-329
   read_file_to_root_with_iterator       :331-364 (a synthetic 100000-byte file in place of
                                         test_files/100000_byte_file.bytes, which is not committed)
+and the ColumnDigestAccumulator (column_digest_accumulator.rs) against the oracle's column hashes.
 The reference fills its inputs from a thread RNG; here they are seeded."""
 import io
 import itertools
@@ -92,7 +93,7 @@ def test_row_iterator_is_the_same_root(P, n, pre, enc, batch):
     data = _bytes(n, 6)
     root = _commit(P, data, pre, enc).get_root()
     assert _rows(P, data, pre, enc, batch).convert_to_commit_root() == root
-    # any element iterator (not a FieldGeneratorIter): the collected-elements path
+    # any element iterator (not a FieldGeneratorIter): encoded rows through the accumulator
     el = pos.convert_byte_vec_to_field_elements_vec(data).reshape(-1)
     assert PF.RowGeneratorIter(iter(el.tolist()), pre, enc, batch).convert_to_commit_root() == root
 
@@ -141,3 +142,58 @@ def test_get_full_columns(P, oracle):
         want = comm.open_column(c)
         assert np.array_equal(col.col, want.col) and list(col.path) == list(want.path)
         assert L.verify_column_path(FT63, col, c, comm.get_root())
+
+
+# ---------------------------------------------------------------- ColumnDigestAccumulator
+@pytest.mark.parametrize("fid,n_rows,width,batch_rows,pushes", [
+    (0, 1, 8, 0, [1]),
+    (0, 124, 16, 0, [124]),              # exactly one chunk per column (Ft63: 124 rows)
+    (0, 125, 16, 1, [1] * 125),          # two chunks, hashed as they complete
+    (0, 1000, 64, 100, [7, 300, 1, 692]),
+    (0, 2000, 32, 128, [2000]),
+    (1, 300, 32, 50, [62, 63, 175]),     # Ft127: 62 rows in chunk 0
+    (3, 97, 8, 16, [31, 66]),            # Ft255
+    (4, 40, 4, 8, [40]),                 # Ft253_192 (big-endian repr)
+])
+def test_column_digest_accumulator(P, oracle, fid, n_rows, width, batch_rows, pushes):
+    pos, PF, L = P
+    nl = L.limbs(fid)
+    m = oracle.random_coeffs(fid, n_rows * width, 17 + n_rows).reshape(n_rows, width * nl)
+    want = oracle.hash_columns(fid, m, n_rows, width)
+    acc = PF.ColumnDigestAccumulator(width, PF.ColumnsToCareAbout.All, fid, batch_rows)
+    assert acc.get_width() == width
+    r = 0
+    for k in pushes:
+        acc.update(m[r:r + k])
+        r += k
+    assert r == n_rows
+    assert b"".join(acc.get_column_digests()) == want
+    # finalize_to_merkle_tree: the lcpc-2d tree over the same leaves
+    acc = PF.ColumnDigestAccumulator(width, PF.ColumnsToCareAbout.All, fid, batch_rows)
+    for row in m:  # update one row at a time, as the reference does
+        acc.update(row)
+    tree = acc.finalize_to_merkle_tree()
+    assert tree.to_bytes() == want + L.merkle_tree(want)
+
+
+def test_column_digest_accumulator_commit_root_and_errors(P, oracle):
+    pos, PF, L = P
+    data = _bytes(50000, 10)
+    comm = _commit(P, data, 64, 128)
+    acc = PF.ColumnDigestAccumulator(128, batch_rows=10)
+    for r in comm.comm.reshape(comm.get_n_rows(), 128):
+        acc.update(r)
+    assert acc.finalize_to_commit() == comm.get_root()
+    # no rows: every digest is BLAKE3 of the 32 zero bytes alone
+    assert PF.ColumnDigestAccumulator(4).get_column_digests() == [oracle.blake3(bytes(32))] * 4
+    acc = PF.ColumnDigestAccumulator(8)
+    with pytest.raises(ValueError):
+        acc.update(np.zeros(7, np.uint64))            # ensure!(encoded_row.len() == width)
+    with pytest.raises(NotImplementedError):
+        PF.ColumnDigestAccumulator(8, PF.ColumnsToCareAbout.Only([1, 2]))
+    acc = PF.ColumnDigestAccumulator(6)
+    acc.update(np.arange(6, dtype=np.uint64))
+    with pytest.raises(L.LcpcError):
+        acc.finalize_to_merkle_tree()                  # MerkleTree::new: not a power of two
+    with pytest.raises(L.LcpcError):
+        PF.ColumnDigestAccumulator(8, field=2)         # Ft191 elements straddle chunks
