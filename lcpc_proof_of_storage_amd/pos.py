@@ -5,6 +5,11 @@ commitment (names kept):
   fields::convert_byte_vec_to_field_elements_vec        fields.rs:109-112, data_field.rs:38-46
   fields::convert_field_elements_vec_to_byte_vec        fields.rs:114-121
   fields::field_generator_iter::FieldGeneratorIter      fields/field_generator_iter.rs:5-55
+  fields::{read_file_to_field_elements_vec, stream_file_to_field_elements_vec_sync,
+           read_file_path_to_field_elements_vec, field_elements_vec_to_file,
+           random_writeable_field_vec, evaluate_field_polynomial_at_point[_with_elevated_degree],
+           vector_multiply, is_power_of_two}          fields.rs:25-194
+  lcpc_online::dims_ok                                   lcpc_online.rs:71-76
   networking::server::get_aspect_ratio_default_from_field_len / _from_file_len
                                                          networking/server.rs:1139-1182
   networking::client::get_column_indicies_from_random_seed   networking/client.rs:443-456
@@ -121,6 +126,63 @@ class FieldGeneratorIter:
             if not block:
                 return
             yield block
+
+
+def read_file_to_field_elements_vec(file) -> tuple:
+    """fields.rs:25-35: (bytes read, elements) of a whole binary file object."""
+    data = file.read()
+    return len(data), convert_byte_vec_to_field_elements_vec(data)
+
+
+def stream_file_to_field_elements_vec_sync(file) -> tuple:
+    """fields.rs:72-106: the same elements, read in buffers of 1000 whole elements (7000 bytes,
+    the reference's BufReader size), each buffer packed by the library.  (file size, elements)."""
+    buf = 1000 * DATA_BYTE_CAPACITY
+    parts, total = [], 0
+    while True:
+        b = file.read(buf)
+        if not b:
+            break
+        total += len(b)
+        parts.append(convert_byte_vec_to_field_elements_vec(b))
+    return total, (np.concatenate(parts) if parts else np.zeros((0, 1), np.uint64))
+
+
+def read_file_path_to_field_elements_vec(path: str) -> np.ndarray:
+    """fields.rs:122-127."""
+    with open(path, "rb") as f:
+        return read_file_to_field_elements_vec(f)[1]
+
+
+def field_elements_vec_to_file(path: str, field_elements) -> None:
+    """fields.rs:129-146: each element's 7 data bytes in turn; the last element's trailing zero
+    bytes are dropped (an empty vector gives an empty file)."""
+    a = np.ascontiguousarray(field_elements, dtype=np.uint64).reshape(-1)
+    data = convert_field_elements_vec_to_byte_vec(a, a.size * DATA_BYTE_CAPACITY) if a.size else b""
+    if a.size:
+        head, last = data[:-DATA_BYTE_CAPACITY], data[-DATA_BYTE_CAPACITY:].rstrip(b"\0")
+        data = head + last
+    with open(path, "wb") as f:
+        f.write(data)
+
+
+def random_writeable_field_vec(log_len: int, seed: int = 0) -> np.ndarray:
+    """fields.rs:148-158: 7 * 2^log_len random bytes packed to 2^log_len elements (the
+    reference draws them from a thread RNG; here a seeded one)."""
+    data = np.random.default_rng(seed).integers(0, 256, DATA_BYTE_CAPACITY << log_len, dtype=np.uint8).tobytes()
+    return convert_byte_vec_to_field_elements_vec(data)
+
+
+def is_power_of_two(x: int) -> bool:
+    """fields.rs:192-194 (true for 0, as x & (x - 1) is)."""
+    return x & (x - 1) == 0 if x else True
+
+
+def dims_ok(num_pre_encoded_columns: int, num_encoded_columns: int) -> bool:
+    """lcpc_online.rs:71-76: a power-of-two width >= 2, >= 1 column, rate at most 1/2."""
+    return (num_encoded_columns > 0 and num_encoded_columns & (num_encoded_columns - 1) == 0
+            and num_pre_encoded_columns >= 1 and num_encoded_columns >= 2
+            and num_encoded_columns >= 2 * num_pre_encoded_columns)
 
 
 def get_aspect_ratio_default_from_field_len(field_len: int):
@@ -249,6 +311,34 @@ def convert_file_data_to_commit(field_data: np.ndarray, what_to_extract, dimensi
         b = bytes(leaves)
         return [b[32 * i:32 * i + 32] for i in range(len(idx))]
     return cols[:len(idx)]
+
+
+def vector_multiply(a, b, field: int = FT63) -> np.ndarray:
+    """fields.rs:188-190 = field_dot."""
+    return field_dot(a, b, field)
+
+
+def evaluate_field_polynomial_at_point_with_elevated_degree(field_elements, point, degree_offset: int,
+                                                            field: int = FT63) -> np.ndarray:
+    """fields.rs:172-186: sum_i c_i x^(i + degree_offset), on the GPU (the powers from
+    lcpc_pos_side_vectors, the sum a one-column collapse)."""
+    nl = limbs(field)
+    c = np.ascontiguousarray(field_elements, dtype=np.uint64).reshape(-1, nl)
+    n = c.shape[0]
+    if n == 0:
+        return np.zeros((1, nl), np.uint64)
+    # left = [1, x^d] (n_rows 2, n_cols d) gives x^d; right = [1, x, ..., x^(n-1)]
+    _, right = form_side_vectors_for_polynomial_evaluation_from_point(point, 1, n, field)
+    v = field_dot(c, right, field)
+    if degree_offset:
+        left, _ = form_side_vectors_for_polynomial_evaluation_from_point(point, 2, degree_offset, field)
+        v = field_dot(v, left[1], field)
+    return v
+
+
+def evaluate_field_polynomial_at_point(field_elements, point, field: int = FT63) -> np.ndarray:
+    """fields.rs:160-170: sum_i c_i x^i (coefficients little-endian: c_0 first)."""
+    return evaluate_field_polynomial_at_point_with_elevated_degree(field_elements, point, 0, field)
 
 
 def server_retreive_columns(comm: LcCommit, requested_columns: Sequence[int]) -> List[LcColumn]:
