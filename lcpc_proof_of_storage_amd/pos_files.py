@@ -741,6 +741,18 @@ class FileHandler:
         return self.pre_encoded_size * DATA_BYTE_CAPACITY
 
     # -- raw data
+    def left_multiply_unencoded_matrix_by_vector(self, left_vector) -> np.ndarray:
+        """file_handler.rs:614-638: u^T M over the stored file's unencoded rows (left_vector has
+        rows_written elements).  The reference's result vector is never sized, so it returns an
+        empty vector; this returns the sum it is written to accumulate (pos.py's function)."""
+        from .pos import left_multiply_unencoded_matrix_by_vector
+        left = np.asarray(left_vector, dtype=np.uint64).reshape(-1)
+        if left.size != self.rows_written:
+            raise ValueError(f"left_vector incorrect size, expected {self.rows_written} and received {left.size}")
+        with open(self.unencoded_file_handle, "rb") as f:
+            data = f.read(self.total_data_bytes)
+        return left_multiply_unencoded_matrix_by_vector(data, self.pre_encoded_size, left)
+
     def get_unencoded_bytes(self, byte_start: int, byte_end: int) -> bytes:
         with open(self.unencoded_file_handle, "rb") as f:
             f.seek(byte_start)

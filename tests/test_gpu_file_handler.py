@@ -176,3 +176,25 @@ def test_append_from_empty_and_on_row_boundaries(PF, oracle, tmp_path, chunks):
             fh.verify_all_files_agree()
             _check_against_oracle(fh, oracle, bytes(contents))
     fh.delete_all_files()
+
+
+def test_left_multiply_unencoded_matrix_by_vector(PF, oracle, tmp_path):
+    """FileHandler::left_multiply_unencoded_matrix_by_vector (file_handler.rs:614-638): u^T M
+    over the stored rows, against the oracle's row combination of the same elements (the
+    reference's own returns an empty vector), and its size check."""
+    data = _bytes_10000(5)
+    src = tmp_path / "lm.bin"
+    src.write_bytes(data)
+    pre, enc = 16, 32
+    fh = PF.FileHandler.create_from_unencoded_file("01LEFTMULTIPLY000000000000", str(src), pre, enc,
+                                                   directory=str(tmp_path / "files"))
+    rows = fh.get_dimensions()[2]
+    left = oracle.random_coeffs(0, rows, 99)
+    el = oracle.pos_bytes_to_field(data)
+    m = np.zeros(rows * pre, np.uint64)
+    m[:el.size] = el
+    got = fh.left_multiply_unencoded_matrix_by_vector(left)
+    assert np.array_equal(np.asarray(got).reshape(-1), oracle.collapse(0, m, left.reshape(-1), rows, pre))
+    with pytest.raises(ValueError):
+        fh.left_multiply_unencoded_matrix_by_vector(left[:-1])
+    fh.delete_all_files()
