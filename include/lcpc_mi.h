@@ -194,6 +194,13 @@ size_t lcpc_commit_n_rows(const lcpc_commit *c);      /* get_n_rows   :309-311 *
 size_t lcpc_commit_n_cols(const lcpc_commit *c);      /* get_n_cols   :304-306 */
 size_t lcpc_commit_n_per_row(const lcpc_commit *c);   /* get_n_per_row :299-301 */
 size_t lcpc_commit_n_hashes(const lcpc_commit *c);
+/* LcCommit's serde Deserialize (WrappedLcCommit, lib.rs:193-229): a commitment from its fields --
+ * comm (n_rows x n_cols) and coeffs (n_rows x n_per_row) as row-major Montgomery limbs, the
+ * n_hashes = 2 next_pow2(n_cols) - 1 digests in commit order (root last) -- loaded into HBM so
+ * prove / open_column run on it.  Other sizes: LCPC_ERR_INVALID_ARG. */
+lcpc_status lcpc_commit_from_parts(lcpc_field f, size_t n_rows, size_t n_cols, size_t n_per_row,
+                                   const uint64_t *comm, const uint64_t *coeffs, const uint8_t *hashes,
+                                   size_t n_hashes, lcpc_commit **out);
 /* copies of the public fields comm / coeffs / hashes (:180-190) to host memory */
 lcpc_status lcpc_commit_copy_comm(const lcpc_commit *c, uint64_t *out);
 lcpc_status lcpc_commit_copy_coeffs(const lcpc_commit *c, uint64_t *out);

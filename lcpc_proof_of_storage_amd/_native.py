@@ -102,6 +102,7 @@ SIGNATURES = {
     "lcpc_commit_n_cols": (sz, [vp]),
     "lcpc_commit_n_per_row": (sz, [vp]),
     "lcpc_commit_n_hashes": (sz, [vp]),
+    "lcpc_commit_from_parts": (i32, [i32, sz, sz, sz, u64p, u64p, u8p, sz, C.POINTER(vp)]),
     "lcpc_commit_copy_comm": (i32, [vp, u64p]),
     "lcpc_commit_copy_coeffs": (i32, [vp, u64p]),
     "lcpc_commit_copy_hashes": (i32, [vp, u8p]),

@@ -791,6 +791,42 @@ lcpc_status lcpc_commit_copy_hashes(const lcpc_commit *c, uint8_t *out) {
   return copy_out(c, out, c->hashes.p, c->n_hashes * 32);
 }
 
+lcpc_status lcpc_commit_from_parts(lcpc_field f, size_t n_rows, size_t n_cols, size_t n_per_row,
+                                   const uint64_t *comm, const uint64_t *coeffs, const uint8_t *hashes,
+                                   size_t n_hashes, lcpc_commit **out) {
+  // LcCommit's Deserialize (WrappedLcCommit::unwrap, lcpc-2d/src/lib.rs:193-229): the fields as
+  // given (row-major Montgomery comm and coeffs, the hashes in commit order, root last), loaded
+  // into HBM so that prove / open_column run on them.  The reference takes any lengths and fails
+  // later (check_comm, or a panic in open_column); here the lengths must be the ones commit
+  // produces, else LCPC_ERR_INVALID_ARG.
+  if (!out || (!comm && n_rows * n_cols) || (!coeffs && n_rows * n_per_row) || !hashes)
+    return fail(LCPC_ERR_INVALID_ARG, "null argument");
+  if (!valid_field(f) || !field_gpu_supported(f)) return fail(LCPC_ERR_UNSUPPORTED, "field");
+  if (!n_rows || !n_cols || n_per_row > n_cols || n_hashes != 2 * next_pow2(n_cols) - 1)
+    return fail(LCPC_ERR_INVALID_ARG, "commitment parts of inconsistent sizes");
+  lcpc_status st;
+  Device *dev = current_device(&st);
+  if (!dev) return st;
+  Lease lease(dev);
+  HIP_TRY(hipSetDevice(dev->id));
+  auto c = std::make_unique<lcpc_commit>();
+  c->fid = f;
+  c->dev = dev;
+  c->n_rows = n_rows;
+  c->n_cols = n_cols;
+  c->n_per_row = n_per_row;
+  c->n_hashes = n_hashes;
+  const size_t wb = field_bytes(f);
+  if ((st = upload(dev, c->comm, comm, n_rows * n_cols * wb))) return st;
+  if ((st = upload(dev, c->coeffs, coeffs, n_rows * n_per_row * wb))) return st;
+  if ((st = upload(dev, c->hashes, hashes, n_hashes * 32))) return st;
+  std::memcpy(c->root, hashes + (n_hashes - 1) * 32, 32);
+  HIP_TRY(hipStreamSynchronize(lease.s));
+  for (auto *b : {&c->comm, &c->coeffs, &c->hashes}) b->settle();
+  *out = c.release();
+  return LCPC_OK;
+}
+
 lcpc_status lcpc_check_comm(const lcpc_commit *c, const lcpc_encoding *e) {
   // check_comm (lcpc-2d/src/lib.rs:703-718); buffer sizes hold by construction
   if (!c || !e) return fail(LCPC_ERR_INVALID_ARG, "null argument");

@@ -443,10 +443,104 @@ class SdigEncoding(LcEncoding):
 
 
 # ---------------------------------------------------------------- commitment / proof
+# serde + bincode 1.3 encodings of the reference's wrapped types (fixed-width little-endian
+# integers, u64 lengths; an element is ff_derive's [u64; N] newtype, i.e. its Montgomery limbs;
+# a digest is WrappedOutput { bytes: serde_bytes }, lib.rs:376-381)
+_q = struct.Struct("<Q").pack
+
+
+def _ser_vec_f(a, nl: int) -> bytes:
+    a = np.ascontiguousarray(a, dtype="<u8").reshape(-1, nl)
+    return _q(a.shape[0]) + a.tobytes()
+
+
+def _ser_digest(d: bytes) -> bytes:
+    return _q(len(d)) + bytes(d)
+
+
+class _Reader:
+    def __init__(self, data: bytes):
+        self.data, self.off = data, 0
+
+    def u64(self) -> int:
+        if self.off + 8 > len(self.data):
+            raise LcpcError(30, "truncated bincode input")
+        v = struct.unpack_from("<Q", self.data, self.off)[0]
+        self.off += 8
+        return v
+
+    def vec_f(self, nl: int) -> np.ndarray:
+        n = self.u64()
+        if self.off + 8 * n * nl > len(self.data):
+            raise LcpcError(30, "truncated bincode input")
+        a = np.frombuffer(self.data, dtype="<u8", count=n * nl, offset=self.off).astype(np.uint64).reshape(n, nl)
+        self.off += 8 * n * nl
+        return a
+
+    def digest(self) -> bytes:
+        n = self.u64()
+        # Output<Blake3> is a 32-byte GenericArray: collecting another length panics (lib.rs:388-389)
+        if n != 32 or self.off + n > len(self.data):
+            raise LcpcError(30, "a serialized digest is not 32 bytes")
+        d = bytes(self.data[self.off:self.off + n])
+        self.off += n
+        return d
+
+    def end(self):
+        if self.off != len(self.data):
+            raise LcpcError(30, "trailing bytes after a serialized value")
+
+
+class LcRoot:
+    """LcRoot<Blake3, E> (lcpc-2d/src/lib.rs:331-422): a commitment root digest, with its serde
+    form (WrappedOutput: 8-byte length 32, then the bytes)."""
+
+    def __init__(self, root: bytes):
+        if len(root) != 32:
+            raise LcpcError(30, "a root is 32 bytes")
+        self.root = bytes(root)
+
+    @classmethod
+    def new_from_root_digest(cls, root: bytes) -> "LcRoot":
+        return cls(root)
+
+    def into_raw(self) -> bytes:
+        return self.root
+
+    def as_ref(self) -> bytes:
+        return self.root
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, LcRoot) and self.root == other.root
+
+    def to_bincode(self) -> bytes:
+        return _ser_digest(self.root)
+
+    @classmethod
+    def from_bincode(cls, data: bytes) -> "LcRoot":
+        r = _Reader(data)
+        root = r.digest()
+        r.end()
+        return cls(root)
+
+
 @dataclass
 class LcColumn:
     col: np.ndarray          # (n_rows, limbs)
     path: List[bytes]        # log2(n_cols) digests
+
+    def to_bincode(self, field: int) -> bytes:
+        """WrappedLcColumn (lib.rs:457-463): col as Vec<F>, path as Vec<WrappedOutput>."""
+        return (_ser_vec_f(self.col, limbs(field)) + _q(len(self.path))
+                + b"".join(_ser_digest(d) for d in self.path))
+
+    @classmethod
+    def from_bincode(cls, field: int, data: bytes) -> "LcColumn":
+        r = _Reader(data)
+        col = r.vec_f(limbs(field))
+        path = [r.digest() for _ in range(r.u64())]
+        r.end()
+        return cls(col, path)
 
 
 class LcCommit:
@@ -512,6 +606,34 @@ class LcCommit:
         out = (C.c_uint8 * 32)()
         _raise(N.load().lcpc_commit_get_root(self._h, C.cast(out, N.u8p)))
         return bytes(out)
+
+    def to_bincode(self) -> bytes:
+        """serde Serialize via WrappedLcCommit (lib.rs:193-283): comm, coeffs (Vec<F>), n_rows,
+        n_cols, n_per_row (u64), hashes (Vec<WrappedOutput>)."""
+        nl = limbs(self.field)
+        h = self.hashes
+        return b"".join([_ser_vec_f(self.comm, nl), _ser_vec_f(self.coeffs, nl), _q(self.get_n_rows()),
+                         _q(self.get_n_cols()), _q(self.get_n_per_row()), _q(len(h) // 32)]
+                        + [_ser_digest(h[i:i + 32]) for i in range(0, len(h), 32)])
+
+    @classmethod
+    def from_bincode(cls, field: int, data: bytes) -> "LcCommit":
+        """serde Deserialize (WrappedLcCommit::unwrap): the fields loaded into HBM
+        (lcpc_commit_from_parts), so prove / open_column work on the result."""
+        nl = limbs(field)
+        r = _Reader(data)
+        comm, coeffs = r.vec_f(nl), r.vec_f(nl)
+        n_rows, n_cols, n_per_row = r.u64(), r.u64(), r.u64()
+        hashes = b"".join(r.digest() for _ in range(r.u64()))
+        r.end()
+        if comm.shape[0] != n_rows * n_cols or coeffs.shape[0] != n_rows * n_per_row:
+            raise LcpcError(30, "serialized commitment: vector lengths disagree with its dims")
+        hp, keep = _bytes_ptr(hashes)
+        h = C.c_void_p()
+        _raise(N.load().lcpc_commit_from_parts(field, n_rows, n_cols, n_per_row,
+                                               _p64(np.ascontiguousarray(comm)), _p64(np.ascontiguousarray(coeffs)),
+                                               hp, len(hashes) // 32, C.byref(h)))
+        return cls(h.value, field)
 
     def get_n_rows(self) -> int:
         return N.load().lcpc_commit_n_rows(self._h)
