@@ -66,3 +66,39 @@ class _HipMem:
 @pytest.fixture(scope="session")
 def hipmem(gpu):
     return _HipMem()
+
+
+def collect_ranks(procs, q, world, timeout=280, label="ranks"):
+    """The reports of `world` spawned ranks from queue q, as {rank: report}.  A rank that exits
+    without reporting (a crash, or the sharded watchdog's status 75) fails the caller within
+    seconds, with the exit codes, instead of leaving it waiting out the timeout; ranks still alive
+    at the end are killed."""
+    import queue
+    import time
+    res, deadline = {}, time.monotonic() + timeout
+    try:
+        while len(res) < world:
+            try:
+                r, v = q.get(timeout=5)
+                res[r] = v
+                continue
+            except queue.Empty:
+                pass
+            silent = [(i, p.exitcode) for i, p in enumerate(procs) if i not in res and p.exitcode is not None]
+            if silent:
+                raise AssertionError(f"{label}: rank(s) exited without reporting (rank, exit code): {silent}")
+            if time.monotonic() > deadline:
+                raise AssertionError(f"{label}: no report from ranks {sorted(set(range(world)) - set(res))} "
+                                     f"within {timeout} s")
+    finally:
+        for p in procs:
+            p.join(timeout=60 if len(res) == world else 5)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    return res
+
+
+# rendezvous bound for spawned gloo groups: a rank that cannot form the group reports instead of
+# waiting forever
+RENDEZVOUS_TIMEOUT_S = 60

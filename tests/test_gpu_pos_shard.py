@@ -11,6 +11,7 @@ GPU with host-staged gloo collectives, and eight ranks on the one GPU through RC
 distinct NCCL_HOSTID per rank: RCCL then connects the ranks over its socket transport instead of
 refusing two ranks on one GPU) -- cfg5's N = 8 exchange pattern.
 """
+import datetime
 import hashlib
 import os
 import socket
@@ -90,7 +91,9 @@ def _worker(rank, world, port, args, q, rccl=False):
     import lcpc_proof_of_storage_amd as L
     from conftest import _HipMem
     from lcpc_proof_of_storage_amd import shard
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from conftest import RENDEZVOUS_TIMEOUT_S
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=RENDEZVOUS_TIMEOUT_S))
     try:
         L.set_device(0)
         comm = shard.NativeComm.rccl(dist) if rccl else shard.NativeComm.host(dist)
@@ -112,10 +115,8 @@ def _spawn(args, world, timeout=280, rccl=False):
     procs = [ctx.Process(target=_worker, args=(r, world, port, args, q, rccl)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=timeout) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-    return res
+    from conftest import collect_ranks
+    return collect_ranks(procs, q, world, timeout, "pos request")
 
 
 @pytest.mark.timeout(300)

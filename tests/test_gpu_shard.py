@@ -1,5 +1,6 @@
 """GPU: the row-sharded protocol (shard.py) with the product backend reproduces the single-GPU
 commit / prove bit for bit -- one rank, and two ranks (gloo) sharing the one GPU."""
+import datetime
 import os
 import socket
 import sys
@@ -63,7 +64,10 @@ def _worker(rank, world, port, case, q, device="cpu"):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     import lcpc_proof_of_storage_amd as L
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, HERE)
+    from conftest import RENDEZVOUS_TIMEOUT_S
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=RENDEZVOUS_TIMEOUT_S))
     try:
         L.set_device(0)
         fid, n = CASES[case]
@@ -90,8 +94,7 @@ def test_sharded_world2_one_gpu(gpu, case, device):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q, device)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=280) for _ in range(2))
-    for p in procs:
-        p.join(timeout=60)
+    from conftest import collect_ranks
+    res = collect_ranks(procs, q, 2, 280, "sharded world 2")
     assert res[1] is None or "error" not in res[1], res[1]
     assert all(v is True for v in res[0].values()), res[0]

@@ -10,6 +10,7 @@ against the single-GPU commit / prove and the CPU oracle (every commit + prove c
 * cfg3 at BASELINE's full size (Ft127, 2^24, 512 x 32768 -> 65536) split over two ranks, against
   the oracle's commit and proof (tests/test_gpu_fullsize.py holds the unsharded cfg3 / cfg4 / cfg5).
 """
+import datetime
 import os
 import socket
 import sys
@@ -228,7 +229,9 @@ def _worker(rank, world, port, job, args, q):
     import lcpc_proof_of_storage_amd as L
     from conftest import _HipMem
     from lcpc_proof_of_storage_amd import shard
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from conftest import RENDEZVOUS_TIMEOUT_S
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=RENDEZVOUS_TIMEOUT_S))
     try:
         L.set_device(0)
         comm = shard.NativeComm.rccl(dist) if rccl else shard.NativeComm.host(dist)
@@ -248,6 +251,7 @@ def _worker(rank, world, port, job, args, q):
 
 def _spawn(job, args, timeout=280, world=2):
     import torch.multiprocessing as mp
+    from conftest import collect_ranks
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -256,10 +260,7 @@ def _spawn(job, args, timeout=280, world=2):
     procs = [ctx.Process(target=_worker, args=(r, world, port, job, args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=timeout) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-    return res
+    return collect_ranks(procs, q, world, timeout, job)
 
 
 @pytest.mark.timeout(300)
