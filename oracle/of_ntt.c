@@ -30,6 +30,7 @@
 #include "oracle.h"
 #include "of_internal.h"
 
+#if !LCPC_FFT_OUTPUT_BITREV
 /* x[j] <-> x[bitrev_lg(j)] (the LCPC_FFT_OUTPUT_BITREV = 0 convention's reordering) */
 static void bitrev_permute(uint64_t *x, int lg, int nl) {
   const size_t n = (size_t)1 << lg;
@@ -44,6 +45,7 @@ static void bitrev_permute(uint64_t *x, int lg, int nl) {
       }
   }
 }
+#endif
 
 static int log2_exact(size_t len, int *lg) {
   if (len == 0 || (len & (len - 1))) return 0;
