@@ -104,7 +104,13 @@ __device__ __forceinline__ void lo_stage(Fe<F> *x, const uint2 *wtab) {
 // there -- k_pack7 fused into the encode (no element image written and read back).
 constexpr int ROW_BYTES = 7 << 14;  // one row of the file image
 
-template <class F, bool CANON, bool COPY, bool BYTES>
+// PF (file images): at the start of round 3 each thread touches one 128-byte line of
+// the image row PF_DIST rows ahead (LDS-DMA into a 4 KiB scratch block: 139 KiB of LDS, still one
+// workgroup per CU) -- the row the XCD's next free CU most likely takes next
+// (workgroups go round-robin over the 8 XCDs, 32 CUs each) -- so that its byte load hits L2
+constexpr int PF_DIST = 256;
+
+template <class F, bool CANON, bool COPY, bool BYTES, bool PF = false>
 __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__ src, size_t src_stride,
                                                     size_t n_valid, uint32_t *__restrict__ dst, size_t dst_stride,
                                                     const uint32_t *__restrict__ tw,
@@ -210,6 +216,16 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
       xchg(1);
     }
     // ---- round 3: thread (hi, mid) holds lo = 0..31; twiddles w^(jm << s) = wtab[jm << (s - 5)]
+    if constexpr (BYTES && PF) {
+      // an LDS-DMA load (no VGPR destination, nothing waits on it until the next barrier): one
+      // dword of each 128-byte line, into a scratch block no one reads
+      __shared__ uint32_t pf_scratch[1024];
+      const size_t b = (row + PF_DIST) * (size_t)ROW_BYTES + 128 * (size_t)tid;
+      if (row + PF_DIST < gridDim.x && tid < ROW_BYTES / 128 && b + 4 <= n_valid)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void *)(reinterpret_cast<const uint8_t *>(src) + b),
+            (__attribute__((address_space(3))) void *)(pf_scratch + (tid & ~63)), 4, 0, 0);
+    }
     const int mid = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
     lo_stage<F, 10>(x, wtab);
     lo_stage<F, 11>(x, wtab);
@@ -244,13 +260,13 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
   }
 }
 
-template <class F, bool CANON, bool COPY, bool BYTES>
+template <class F, bool CANON, bool COPY, bool BYTES, bool PF = false>
 hipError_t launch_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                     size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
   const uint32_t *tw0 = CANON ? p.d_tw_canon : p.d_tw;
   prof::Scope ps("ntt_row1", s);
-  hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES>), dim3((unsigned)n_rows), dim3(1024), 0, s, src, ss, nv, dst,
-                     ds, p.d_tw, tw0, cp, cs);
+  hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, PF>), dim3((unsigned)n_rows), dim3(1024), 0, s, src, ss, nv,
+                     dst, ds, p.d_tw, tw0, cp, cs);
   return hipGetLastError();
 }
 
@@ -265,9 +281,23 @@ hipError_t launch(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, u
 
 // the proof-of-storage commit from the file image (BYTES above): canonical output, coefficient copy;
 // the file's ragged last row (if any) is zero padded as it is staged
+// the L2 prefetch above is the default: the kernel 2.51 -> 2.34 ms per 1 GiB request serially,
+// the cfg5 line's median 36.1 -> 37.6 G el/s over eight interleaved pairs
+// (profiles/r06_row1_prefetch_ab.json); LCPC_ROW1_PREFETCH=0 turns it off for A/B runs (read once)
+inline bool row1_prefetch() {
+  static const bool on = [] {
+    const char *e = std::getenv("LCPC_ROW1_PREFETCH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <class F>
 hipError_t launch_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst, size_t ds,
                         size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
+  if (row1_prefetch())
+    return launch_t<F, true, true, true, true>(p, reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds,
+                                               n_rows, s, cp, cs);
   return launch_t<F, true, true, true>(p, reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds, n_rows, s,
                                        cp, cs);
 }
