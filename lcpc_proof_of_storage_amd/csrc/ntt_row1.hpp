@@ -110,7 +110,19 @@ constexpr int ROW_BYTES = 7 << 14;  // one row of the file image
 // (workgroups go round-robin over the 8 XCDs, 32 CUs each) -- so that its byte load hits L2
 constexpr int PF_DIST = 256;
 
-template <class F, bool CANON, bool COPY, bool BYTES, bool PF = false>
+// one dword of each 128-byte line of image row `ahead` by LDS-DMA (no VGPR destination; nothing
+// waits on it before the next barrier), into a scratch block no one reads
+__device__ __forceinline__ void pf_row(const uint32_t *src, size_t n_valid, size_t ahead, int tid, uint32_t *scratch) {
+  const size_t b = ahead * (size_t)ROW_BYTES + 128 * (size_t)tid;
+  if (ahead < gridDim.x && tid < ROW_BYTES / 128 && b + 4 <= n_valid)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void *)(reinterpret_cast<const uint8_t *>(src) + b),
+        (__attribute__((address_space(3))) void *)(scratch + (tid & ~63)), 4, 0, 0);
+}
+
+// PF: where the prefetch is issued -- 0 none, 1 round 3's start (the default), 2 round 2's start,
+// 3 the output phase's start (A/B: LCPC_ROW1_PREFETCH)
+template <class F, bool CANON, bool COPY, bool BYTES, int PF = 0>
 __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__ src, size_t src_stride,
                                                     size_t n_valid, uint32_t *__restrict__ dst, size_t dst_stride,
                                                     const uint32_t *__restrict__ tw,
@@ -119,6 +131,7 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
   static_assert(F::N == 2, "8-byte fields");
   __shared__ __align__(16) uint2 xbuf[16384];  // half a row
   __shared__ uint2 wtab[512];                   // w^(32 k)
+  __shared__ uint32_t pf_scratch[BYTES && PF ? 1024 : 1];
   const int tid = threadIdx.x;
   const size_t row = blockIdx.x;
   if (tid < 512) wtab[tid] = reinterpret_cast<const uint2 *>(tw)[32 * tid];
@@ -191,6 +204,7 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
       xchg(1);
     }
     // ---- round 2: thread (hi, lo) holds mid = 0..31; twiddles w^(((jm << 5) | lo) << s)
+    if constexpr (BYTES && PF == 2) pf_row(src, n_valid, row + PF_DIST, tid, pf_scratch);
     {
       const int lo = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
       reg_stage<F, 16>(x, [&](int jm) { return lds_ld<F>(wtab, (jm << 5) | lo); });
@@ -216,16 +230,7 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
       xchg(1);
     }
     // ---- round 3: thread (hi, mid) holds lo = 0..31; twiddles w^(jm << s) = wtab[jm << (s - 5)]
-    if constexpr (BYTES && PF) {
-      // an LDS-DMA load (no VGPR destination, nothing waits on it until the next barrier): one
-      // dword of each 128-byte line, into a scratch block no one reads
-      __shared__ uint32_t pf_scratch[1024];
-      const size_t b = (row + PF_DIST) * (size_t)ROW_BYTES + 128 * (size_t)tid;
-      if (row + PF_DIST < gridDim.x && tid < ROW_BYTES / 128 && b + 4 <= n_valid)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void *)(reinterpret_cast<const uint8_t *>(src) + b),
-            (__attribute__((address_space(3))) void *)(pf_scratch + (tid & ~63)), 4, 0, 0);
-    }
+    if constexpr (BYTES && PF == 1) pf_row(src, n_valid, row + PF_DIST, tid, pf_scratch);
     const int mid = ((tid >> 9) << 4) | ((tid >> 4) & 15), hi = (((tid >> 8) & 1) << 4) | (tid & 15);
     lo_stage<F, 10>(x, wtab);
     lo_stage<F, 11>(x, wtab);
@@ -235,6 +240,7 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
     {
       // ---- out: through LDS in halves (hi >> 4), 16-byte units u = ((hi & 15) << 9) | (mid << 4) | (lo >> 1)
       //      stored at u ^ (hi & 7): a ds_write's 64 lanes land on 8 distinct 16-byte bank slots
+      if constexpr (BYTES && PF == 3) pf_row(src, n_valid, row + PF_DIST, tid, pf_scratch);
       uint4 *ubuf = reinterpret_cast<uint4 *>(xbuf);
       uint4 *out = reinterpret_cast<uint4 *>(dst + row * dst_stride * 2);
       auto store_half = [&](int ph) {
@@ -260,7 +266,7 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
   }
 }
 
-template <class F, bool CANON, bool COPY, bool BYTES, bool PF = false>
+template <class F, bool CANON, bool COPY, bool BYTES, int PF = 0>
 hipError_t launch_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                     size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
   const uint32_t *tw0 = CANON ? p.d_tw_canon : p.d_tw;
@@ -284,22 +290,24 @@ hipError_t launch(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, u
 // the L2 prefetch above is the default: the kernel 2.51 -> 2.34 ms per 1 GiB request serially,
 // the cfg5 line's median 36.1 -> 37.6 G el/s over eight interleaved pairs
 // (profiles/r06_row1_prefetch_ab.json); LCPC_ROW1_PREFETCH=0 turns it off for A/B runs (read once)
-inline bool row1_prefetch() {
-  static const bool on = [] {
+inline int row1_prefetch() {
+  static const int mode = [] {
     const char *e = std::getenv("LCPC_ROW1_PREFETCH");
-    return !(e && e[0] == '0');
+    return (e && e[0] >= '0' && e[0] <= '3' && !e[1]) ? e[0] - '0' : 1;
   }();
-  return on;
+  return mode;
 }
 
 template <class F>
 hipError_t launch_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst, size_t ds,
                         size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
-  if (row1_prefetch())
-    return launch_t<F, true, true, true, true>(p, reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds,
-                                               n_rows, s, cp, cs);
-  return launch_t<F, true, true, true>(p, reinterpret_cast<const uint32_t *>(bytes), 0, n_bytes, dst, ds, n_rows, s,
-                                       cp, cs);
+  const uint32_t *b = reinterpret_cast<const uint32_t *>(bytes);
+  switch (row1_prefetch()) {
+    case 0: return launch_t<F, true, true, true, 0>(p, b, 0, n_bytes, dst, ds, n_rows, s, cp, cs);
+    case 2: return launch_t<F, true, true, true, 2>(p, b, 0, n_bytes, dst, ds, n_rows, s, cp, cs);
+    case 3: return launch_t<F, true, true, true, 3>(p, b, 0, n_bytes, dst, ds, n_rows, s, cp, cs);
+    default: return launch_t<F, true, true, true, 1>(p, b, 0, n_bytes, dst, ds, n_rows, s, cp, cs);
+  }
 }
 
 }  // namespace ntt_row1
