@@ -702,7 +702,11 @@ def pos_workload(args, L, torch, rank, local_rank):
                                 else "lcpc_pos_commit_eval_bytes_device (file image and u^T Enc(M) in one call)"
                                 if fused
                                 else "lcpc_pos_commit_bytes_device (file image in one call)" if args.pos_commit == "bytes"
-                                else "lcpc_pos_bytes_to_field_device + lcpc_commit_new_device")},
+                                else "lcpc_pos_bytes_to_field_device + lcpc_commit_new_device"),
+                "row_kernel": (("one-pass (ntt_row1), L2 prefetch of the row 256 ahead: "
+                                + {"0": "off", "2": "at round 2", "3": "at the output phase"}.get(
+                                    os.environ.get("LCPC_ROW1_PREFETCH", "1"), "at round 3"))
+                               if row1_active(nc, fi) else "four-step (ntt_pass_a + ntt_pass_b)")},
         step=step, cpu_baseline=cpu_baseline, parity=parity, input_bytes=n_bytes,
         enc_kernels=("ntt_pass_a", "ntt_pass_b", "ntt_small", "ntt_row1"),
         enc_kernel_desc=(f"ntt_encode = ntt_row1 (one launch per commit, all {n_rows} rows)" if row1_active(nc, fi) else
