@@ -121,8 +121,10 @@ __device__ __forceinline__ void pf_row(const uint32_t *src, size_t n_valid, size
 }
 
 // PF: where the prefetch is issued -- 0 none, 1 round 3's start (the default), 2 round 2's start,
-// 3 the output phase's start (A/B: LCPC_ROW1_PREFETCH)
-template <class F, bool CANON, bool COPY, bool BYTES, int PF = 0>
+// 3 the output phase's start (A/B: LCPC_ROW1_PREFETCH).  GLDS: a whole row's bytes are staged by
+// LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no ds_write) instead of loads + ds_write
+// (A/B: LCPC_ROW1_GLDS)
+template <class F, bool CANON, bool COPY, bool BYTES, int PF = 0, bool GLDS = false>
 __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__ src, size_t src_stride,
                                                     size_t n_valid, uint32_t *__restrict__ dst, size_t dst_stride,
                                                     const uint32_t *__restrict__ tw,
@@ -145,6 +147,17 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
         const size_t row0 = row * (size_t)ROW_BYTES;
         const uint8_t *rb = reinterpret_cast<const uint8_t *>(src) + row0;
         uint4 *sb = reinterpret_cast<uint4 *>(xbuf);
+        if (GLDS && row0 + ROW_BYTES <= n_valid) {
+          // a wave's 64 lanes take 64 consecutive 16-byte units: LDS base + lane x 16 is sb[i]
+#pragma unroll
+          for (int k = 0; k < ROW_BYTES / 16 / 1024; k++) {
+            const int i = tid + 1024 * k;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(rb + 16 * (size_t)i),
+                (__attribute__((address_space(3))) void *)(sb + (i & ~63)), 16, 0, 0);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else
         for (int i = tid; i < ROW_BYTES / 16; i += 1024) {
           const size_t b = row0 + 16 * (size_t)i;
           if (b + 16 <= n_valid) {
@@ -266,12 +279,12 @@ __global__ __launch_bounds__(1024) void k_row_ntt15(const uint32_t *__restrict__
   }
 }
 
-template <class F, bool CANON, bool COPY, bool BYTES, int PF = 0>
+template <class F, bool CANON, bool COPY, bool BYTES, int PF = 0, bool GLDS = false>
 hipError_t launch_t(const NttPlan &p, const uint32_t *src, size_t ss, size_t nv, uint32_t *dst, size_t ds,
                     size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
   const uint32_t *tw0 = CANON ? p.d_tw_canon : p.d_tw;
   prof::Scope ps("ntt_row1", s);
-  hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, PF>), dim3((unsigned)n_rows), dim3(1024), 0, s, src, ss, nv,
+  hipLaunchKernelGGL((k_row_ntt15<F, CANON, COPY, BYTES, PF, GLDS>), dim3((unsigned)n_rows), dim3(1024), 0, s, src, ss, nv,
                      dst, ds, p.d_tw, tw0, cp, cs);
   return hipGetLastError();
 }
@@ -298,10 +311,23 @@ inline int row1_prefetch() {
   return mode;
 }
 
+// the LDS-DMA staging is the default with the round-3 prefetch: the kernel 2.36 -> 2.29 ms per
+// 1 GiB request serially, the cfg5 line's median 35.1 -> 36.3 G el/s over four interleaved pairs
+// (profiles/r06_row1_glds_ab.json); LCPC_ROW1_GLDS=0 stages through VGPRs + ds_write (read once)
+inline bool row1_glds() {
+  static const bool on = [] {
+    const char *e = std::getenv("LCPC_ROW1_GLDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <class F>
 hipError_t launch_bytes(const NttPlan &p, const uint8_t *bytes, size_t n_bytes, uint32_t *dst, size_t ds,
                         size_t n_rows, hipStream_t s, uint32_t *cp, size_t cs) {
   const uint32_t *b = reinterpret_cast<const uint32_t *>(bytes);
+  if (row1_glds() && row1_prefetch() == 1)
+    return launch_t<F, true, true, true, 1, true>(p, b, 0, n_bytes, dst, ds, n_rows, s, cp, cs);
   switch (row1_prefetch()) {
     case 0: return launch_t<F, true, true, true, 0>(p, b, 0, n_bytes, dst, ds, n_rows, s, cp, cs);
     case 2: return launch_t<F, true, true, true, 2>(p, b, 0, n_bytes, dst, ds, n_rows, s, cp, cs);

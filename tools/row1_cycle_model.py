@@ -26,8 +26,9 @@ import isa_count as IC  # noqa: E402
 
 ROWS = 9363                      # 1 GiB file at the default dims (16384 -> 32768 Ft63 per row)
 WAVES_PER_ROW = 16
-# CANON, COPY (the commit's coeffs), BYTES, PF (the L2 prefetch, the default since round 6)
-KERNEL = "k_row_ntt15<lcpc::Ft63, true, true, true, true>"
+# CANON, COPY (the commit's coeffs), BYTES, PF = 1 (the L2 prefetch at round 3), GLDS (LDS-DMA
+# staging): the file-image kernel's defaults since round 6
+KERNEL = "k_row_ntt15<lcpc::Ft63, true, true, true, 1, true>"
 
 
 def main():
