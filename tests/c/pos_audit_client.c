@@ -14,8 +14,11 @@
  *           (encoded_file_reader.rs:328-346); decode_to_target_file (:59-91)
  * Checks: the .portree root is the commitment root; every opened column's leaf and path lead to
  * it; every opened column agrees with the evaluation; a tampered evaluation fails exactly its
- * column; the .porenc image decodes to the file; after a one-byte edit and a row re-encode the
- * re-hashed .porenc tree is the new commitment's root and differs from the old one.
+ * column; the commitment rebuilt from its fields (lcpc_commit_from_parts, LcCommit's serde
+ * form) has the same root and opens the same columns; the encoded rows streamed through a
+ * ColumnDigestAccumulator (lcpc_column_digests_*) give the .portree leaves; the .porenc image
+ * decodes to the file; after a one-byte edit and a row re-encode the re-hashed .porenc tree is
+ * the new commitment's root and differs from the old one.
  * Usage: pos_audit_client [n_bytes]   (exit 0 and "pos audit ok" on success)
  */
 #include <stdio.h>
@@ -117,6 +120,37 @@ int main(int argc, char **argv) {
   leaves[0] ^= 1;
   CHECK(lcpc_verify_leaf_paths(leaves, paths, n_open, log_enc, idx, root, ok));
   EXPECT(ok[0] == 0, "a tampered leaf was accepted");
+
+  /* the commitment's fields (serde Serialize) rebuild it (Deserialize: lcpc_commit_from_parts),
+   * and the encoded rows streamed through a ColumnDigestAccumulator give the .portree leaves */
+  {
+    const size_t n_hashes = lcpc_commit_n_hashes(c);
+    uint64_t *comm = malloc(rows * enc * 8), *coeffs = malloc(rows * pre * 8);
+    uint8_t *hashes = malloc(n_hashes * 32), *digests = malloc(enc * 32), root3[32];
+    EXPECT(comm && coeffs && hashes && digests, "allocation");
+    CHECK(lcpc_commit_copy_comm(c, comm));
+    CHECK(lcpc_commit_copy_coeffs(c, coeffs));
+    CHECK(lcpc_commit_copy_hashes(c, hashes));
+    lcpc_commit *c2 = NULL;
+    CHECK(lcpc_commit_from_parts(f, rows, enc, pre, comm, coeffs, hashes, n_hashes, &c2));
+    CHECK(lcpc_commit_get_root(c2, root3));
+    EXPECT(!memcmp(root3, root, 32), "the rebuilt commitment has another root");
+    uint64_t *cols2 = malloc(n_open * rows * 8);
+    uint8_t *paths2 = malloc(n_open * log_enc * 32 + 1);
+    EXPECT(cols2 && paths2, "allocation");
+    CHECK(lcpc_open_columns(c2, idx, n_open, cols2, paths2));
+    EXPECT(!memcmp(cols2, cols, n_open * rows * 8) && !memcmp(paths2, paths, n_open * log_enc * 32),
+           "the rebuilt commitment opens other columns");
+    lcpc_column_digests *acc = NULL;
+    CHECK(lcpc_column_digests_new(f, enc, 64, &acc));
+    for (size_t r = 0; r < rows; r += 100) /* ragged batches of encoded rows */
+      CHECK(lcpc_column_digests_update(acc, comm + r * enc, rows - r < 100 ? rows - r : 100));
+    CHECK(lcpc_column_digests_finalize(acc, digests, NULL));
+    EXPECT(!memcmp(digests, tree, enc * 32), "the accumulator's digests are not the .portree leaves");
+    lcpc_column_digests_free(acc);
+    lcpc_commit_free(c2);
+    free(comm); free(coeffs); free(hashes); free(digests); free(cols2); free(paths2);
+  }
 
   /* the stored image decodes to the file */
   uint8_t *back = malloc(rows * pre * 7);
