@@ -13,7 +13,7 @@ import collections
 import csv
 import json
 
-SHORT = ["k_pass_a", "k_pass_b", "k_leaf_chunks", "k_leaf_merge", "k_merkle", "k_collapse_partial", "k_collapse_mfma", "k_tensor_digits",
+SHORT = ["k_row_ntt15", "k_spmm", "k_transpose", "k_pass_a", "k_pass_b", "k_leaf_chunks", "k_leaf_merge", "k_merkle", "k_collapse_partial", "k_collapse_mfma", "k_tensor_digits",
          "k_collapse_fold", "k_convert", "k_gather_cols", "k_gather_paths", "k_ntt_small", "k_copy_words",
          "copyBuffer", "fillBuffer", "k_tw_table", "k_column_checks", "k_path_checks", "k_dot"]
 
