@@ -32,7 +32,7 @@ def _worker(rank, world, port, q):
         seeds = [None] * w
         dist.all_gather_object(seeds, bench.replica_seed(r))
         bench.sync_barrier(dist)
-        q.put((r, elapsed, seeds, bench.job_throughput(1 << 24, 10, w, elapsed)))
+        q.put((r, (r, elapsed, seeds, bench.job_throughput(1 << 24, 10, w, elapsed))))
     finally:
         dist.destroy_process_group()
 
@@ -46,9 +46,10 @@ def test_bench_plumbing_world2():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=100) for _ in range(2))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from conftest import collect_ranks
+    res = sorted(collect_ranks(procs, q, 2, 100, "bench plumbing").values())
     for p in procs:
-        p.join(timeout=30)
         assert p.exitcode == 0
     for r, elapsed, seeds, thr in res:
         assert elapsed == 2.0                      # max over ranks

@@ -3,6 +3,7 @@ gloo on the CPU, with the compute steps supplied by the oracle (OracleBackend be
 sharded root and proof must equal the single-process oracle's commit / prove bit for bit; the
 GPU run of the same protocol uses GpuBackend (tests/test_gpu_shard.py).
 """
+import datetime
 import os
 import socket
 import sys
@@ -153,7 +154,9 @@ def _worker(rank, world, port, case, q):
     import torch.distributed as dist
     import oracle_ffi as O
     from lcpc_proof_of_storage_amd.shard import Comm, RowShardedCommit
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from conftest import RENDEZVOUS_TIMEOUT_S
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=RENDEZVOUS_TIMEOUT_S))
     try:
         c = CASES[case]
         comm_ref, outer, pf_ref = reference(case)
@@ -200,9 +203,9 @@ def test_row_sharded_protocol_world2(case):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=280) for _ in range(2))
+    from conftest import collect_ranks
+    res = collect_ranks(procs, q, 2, 280, "sharded world 2")
     for p in procs:
-        p.join(timeout=30)
         assert p.exitcode == 0
     r0 = res[0]
     assert r0["root"] and r0["p_eval"] and r0["p_random"] and r0["cols"] and r0["paths"], r0
@@ -218,7 +221,9 @@ def _worker_concurrent(rank, world, port, case, q):
     import torch.distributed as dist
     import oracle_ffi as O
     from lcpc_proof_of_storage_amd.shard import Comm, RowShardedCommit
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from conftest import RENDEZVOUS_TIMEOUT_S
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=RENDEZVOUS_TIMEOUT_S))
     try:
         c = CASES[case]
         comm_ref, outer, pf_ref = reference(case)
@@ -257,8 +262,8 @@ def test_row_sharded_concurrent_groups_world2():
     procs = [ctx.Process(target=_worker_concurrent, args=(r, 2, port, "ft127", q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=280) for _ in range(2))
+    from conftest import collect_ranks
+    res = collect_ranks(procs, q, 2, 280, "sharded world 2")
     for p in procs:
-        p.join(timeout=30)
         assert p.exitcode == 0
     assert res[0] == [True, True], res[0]
