@@ -136,3 +136,36 @@ def test_pos_commit_bytes_device_sdig(gpu, oracle, hipmem):
     finally:
         hipmem.free(d)
         hipmem.free(de)
+
+
+def test_row1_runtime_modes_agree(gpu, oracle):
+    """the file-image kernel's runtime knobs (ntt_row1.hpp row1_prefetch / row1_glds, read once
+    per process, so one child process per setting): every prefetch placement, with and without
+    the LDS-DMA staging, gives the default's commitment -- whole rows, a ragged last row that the
+    prefetch of row + 256 reaches, a partial last element, a one-row file -- and the default's
+    root is the oracle's"""
+    import json
+    import os
+    import subprocess
+    import sys
+    sizes = [7 * NP * 5 + 1001, 7 * NP * 300 + 11, 7 * NP * 600, 13]
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_row1_modes_child.py")
+    results = {}
+    for pf, glds in [(None, None), ("0", None), ("2", None), ("3", None), ("1", "0"), ("0", "0")]:
+        env = {k: v for k, v in os.environ.items() if k not in ("LCPC_ROW1_PREFETCH", "LCPC_ROW1_GLDS")}
+        if pf is not None:
+            env["LCPC_ROW1_PREFETCH"] = pf
+        if glds is not None:
+            env["LCPC_ROW1_GLDS"] = glds
+        r = subprocess.run([sys.executable, child, *map(str, sizes)], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, (pf, glds, r.stderr[-2000:])
+        results[(pf, glds)] = json.loads(r.stdout.strip().splitlines()[-1])
+    default = results[(None, None)]
+    for key, got in results.items():
+        assert got == default, key
+    n_bytes = sizes[0]
+    data = np.random.default_rng(n_bytes).integers(0, 256, n_bytes, dtype=np.uint8)
+    data[-1] = 0xff
+    o = oracle.Commit(oracle.Encoding.ligero(0, NP, NC, 16, 2), oracle.pos_bytes_to_field(data.tobytes()))
+    assert default[str(n_bytes)][0] == o.root().hex()
