@@ -9,6 +9,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import lcpc_proof_of_storage_amd as L  # noqa: E402
 
 
@@ -47,6 +48,19 @@ def main():
     data = np.random.default_rng(n_bytes).integers(0, 256, n_bytes, dtype=np.uint8)
     c = L.LcCommit.commit_pos_bytes(data, L.RsEncoding.new(0, 16384, 32768, 16, 2))
     out["pos_bytes"] = [c.get_root().hex(), hashlib.sha256(c.get_root() + c.comm.tobytes() + c.coeffs.tobytes()).hexdigest()]
+    # the sharded driver at one rank (lcpc_sharded_commit_prove_many), pipelined over 4 polynomials
+    from conftest import _HipMem
+    from lcpc_proof_of_storage_amd import shard
+    hm = _HipMem()
+    enc = L.RsEncoding.new(1, 256, 512, 24, 2)
+    polys = [L.field_random(1, 64 * 256, 50 + k) for k in range(4)]
+    ds = [hm.to_device(p) for p in polys]
+    roots, proofs = shard.sharded_commit_prove_many(enc, shard.NativeComm.single(), ds, 64, L.field_random(1, 64, 60),
+                                                    lambda i, root: tr(root))
+    h = hashlib.sha256(b"".join(roots))
+    for p in proofs:
+        h.update(p.to_bincode())
+    out["sharded_n1"] = [roots[0].hex(), h.hexdigest()]
     print(json.dumps(out))
 
 

@@ -1,7 +1,7 @@
 """GPU: the library's runtime knobs change how the work is scheduled or which kernel variant runs,
 never the result.  Each knob is read once per process, so each setting gets its own child process
 (tests/_runtime_knobs_child.py: Ligero commit / prove / verify over all five fields, Brakedown over
-Ft63 and Ft127, a proof-of-storage file-image commit); every setting must return what the default
+Ft63 and Ft127, a proof-of-storage file-image commit, the sharded driver at one rank); every setting must return what the default
 returns, and the default's roots are the oracle's."""
 import json
 import os
@@ -22,6 +22,8 @@ SETTINGS = [
     {"LCPC_HOST_WAIT": "blocking"},     # host threads sleep on the GPU instead of the runtime's default
     {"LCPC_KECCAK": "scalar"},          # the transcript's scalar permutation
     {"LCPC_KECCAK": "avx512"},          # the vector one where the host has AVX-512
+    {"LCPC_SHARD_BULK_STREAMS": "1"},   # the sharded driver's bulk streams: one ...
+    {"LCPC_SHARD_BULK_STREAMS": "4"},   # ... or the most it takes
 ]
 
 
